@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Training-step throughput of the HD-GNN/S engine on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+A step = hdg_fwd_bwd + (RCCL all-reduce of the flat gradient when N > 1) + hdg_adam_tf
+on 100 resident synthetic glide-shaped commits per GPU (weak scaling).  Rank 0 prints
+one JSON line.  Per-kernel durations come from HIP events recorded on the launch stream;
+the CPU baseline is oracle/literal.py (the TF graph's op sequence on torch-CPU).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hd-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "training-step commits/sec, glide Ne=200 Nc=74 batch=100; 1/2/4/8 GPU"
+FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_commit(ne, nc):
+    """Algorithmic FLOPs per commit of each kernel (DESIGN.md section 5 derives them).
+    One add / max / compare / select = 1 FLOP, one FMA = 2.  Diagonal and padding
+    work the kernels do is NOT counted."""
+    H = 20
+    pe, pc = ne * (ne - 1), nc * (nc - 1)
+    ent_fwd = pe * H * 5                      # z=u+v+a*d (2), relu, row acc, col acc
+    ent_bwd = pe * H * 9                      # z (2), cmp, rho_i+rho_j, select, 2 acc, y*dz fma (2)
+    mid_pairs = pc * H * 5 + pc * (H * 3 + 2 * H * 2 + 12 + H * 2) + pc * H * 7 + pc * H * 9
+    #           H1 sums   | classifier fwd+CE+dU2 per pair         | H2 bwd sums | H3 sums
+    mid_nodes = 2 * (ne * H * H * 2 + ne * 21 * H + ne * H          # E_bar, E3 fwd
+                     + nc * 8 * H + 2 * nc * H * H * 2              # alpha/beta, S,T, sigma/tau
+                     + 5 * nc * H * H * 2                           # dU1e,dS/dT,dV2,dG/dH,S/T again
+                     + ne * 21 * H * 2 + ne * H * H * 3)            # E3 bwd, dW5, rho
+    mid_x1 = 2 * 4 * pe                                             # cross-graph fwd + bwd gathers
+    return {"k_entity_fwd": ent_fwd, "k_commit_mid": mid_pairs + mid_nodes + mid_x1,
+            "k_entity_bwd": ent_bwd}
+
+
+def hbm_bytes_per_commit(ne, nc):
+    """Algorithmic HBM bytes per commit of each kernel (inputs read once, outputs written once)."""
+    H = 20
+    pc = nc * (nc - 1)
+    we, wc = (ne + 31) // 32, (nc + 31) // 32
+    inp = 4 * ne + 4 * ne * we
+    return {"k_entity_fwd": inp + 4 * ne * H,
+            "k_commit_mid": 4 * ne * H * 2 + 4 * ne + 4 * ne * we + 4 * nc * wc + 2 * 4 * 2 * pc,
+            "k_entity_bwd": inp + 4 * ne * H}
+
+
+def cpu_baseline(cb, steps, threads):
+    """oracle/literal.py (same dense op sequence and FLOPs as the TF1 CPU graph) on the
+    GPU box's host cores: fwd + autograd bwd + TF-Adam on the same synthetic batch."""
+    from oracle import layout as olayout
+    from oracle import literal, model_ref
+    torch.set_num_threads(threads)
+    B, ne, nc = cb.B, cb.Ne, cb.Nc
+    params = model_ref.init_params(0)
+    P = model_ref.to_torch_params(params, dtype=torch.float32)
+    D = literal.build_dense(cb.x, cb.a, cb.y, cb.hid, cb.nlen, dtype=torch.float32)
+    keys = [k for k, _, _ in olayout.keyed_specs(2)]
+    theta = np.concatenate([params[k].reshape(-1) for k in keys]).astype(np.float64)
+    opt = model_ref.AdamTF(theta.size)
+
+    def one():
+        for p in P.values():
+            p.grad = None
+        out = literal.forward(P, D, B, ne, nc)
+        out["total"].backward()
+        g = np.concatenate([P[k].grad.numpy().reshape(-1) for k in keys]).astype(np.float64)
+        th = opt.step(theta, g)
+        with torch.no_grad():
+            o = 0
+            for k in keys:
+                n = P[k].numel()
+                P[k].copy_(torch.from_numpy(th[o:o + n].reshape(P[k].shape)))
+                o += n
+
+    one()                                     # warm-up (allocator, thread pool)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * steps / dt, 3), "unit": "commits/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d train steps (fwd+bwd+TF-Adam) of oracle/literal.py, fp32 torch-CPU, "
+                      "B=%d Ne=%d Nc=%d, %.1f s timed after 1 warm-up step" % (steps, B, ne, nc, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=100, help="commits per GPU")
+    ap.add_argument("--ne", type=int, default=200)
+    ap.add_argument("--nc", type=int, default=74)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from hdgnn.engine import Engine
+    from hdgnn import layout
+    from hdgnn.synth import seed_for, synth_commits
+    from hdgnn import _lib
+
+    B, ne, nc = args.batch, args.ne, args.nc
+    cb = synth_commits(B, ne, nc, seed_for(1, rank))
+    db = cb.to_device(dev)
+    eng = Engine(ne, nc, B, device=dev, batch_global=B * world)
+    eng.set_params(layout.init_flat(0))
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    for _ in range(args.warmup):
+        eng.train_step(db)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step(db)
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    value = world * B * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # per-kernel durations (HIP events on the launch stream), separate instrumented pass
+    ev = _lib.HipEvents(5)
+    names = ["k_entity_fwd", "k_commit_mid", "k_entity_bwd", "k_grad_reduce"]
+    acc = dict.fromkeys(names, 0.0)
+    nev = max(10, min(args.steps, 50))
+    import ctypes
+    for _ in range(nev):
+        bstruct = db.struct()
+        _lib.check(eng.lib.hdg_fwd_bwd_events(ctypes.byref(eng.shape), ctypes.byref(bstruct),
+                                              ctypes.c_void_p(eng.params.data_ptr()),
+                                              ctypes.c_void_p(eng.grad.data_ptr()),
+                                              ctypes.byref(eng._out),
+                                              ctypes.c_void_p(eng.workspace.data_ptr()),
+                                              eng._stream(), ev.ev))
+        for i, n in enumerate(names):
+            acc[n] += ev.elapsed_ms(i, i + 1)
+        eng.allreduce()
+        eng.adam()
+    torch.cuda.synchronize(dev)
+    kern_ms = {n: acc[n] / nev for n in names}
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    fl = flops_per_commit(ne, nc)
+    dom = max(fl, key=lambda n: kern_ms[n])
+    achieved = fl[dom] * B / (kern_ms[dom] * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne:
+            traffic = tj.get("bytes_per_launch")
+    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "traffic": traffic, "kernel": dom,
+                "flops_per_launch": fl[dom] * B, "avg_launch_ms": round(kern_ms[dom], 5),
+                "note": "fp32 VALU-bound (fp32 MFMA peak = fp32 vector peak = 157.3 TF)"}
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(cb, args.cpu_steps, threads)
+    line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)",
+            "config": {"workload": "model_2 (HD-GNN/S) train step: fwd+bwd+TF-Adam, glide step=2",
+                       "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": "dp%d" % world},
+            "roofline": roofline, "cpu_baseline": cpu,
+            "kernels_ms": {k: round(v, 5) for k, v in kern_ms.items()}}
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

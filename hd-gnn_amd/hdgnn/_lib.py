@@ -1,0 +1,112 @@
+"""ctypes binding of libhdgnn.so (include/hdgnn.h).
+
+The library is built in-tree (hd-gnn_amd/csrc/libhdgnn.so, see build.py).  There
+is deliberately no fallback: if the shared object is missing or fails to load,
+every entry point raises.  torch is imported first so that the process uses
+torch's HIP runtime (same SONAME libamdhip64.so.7) for both.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's libamdhip64 before ours)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libhdgnn.so")
+
+
+class Shape(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("ne", ctypes.c_int32), ("nc", ctypes.c_int32),
+                ("variant", ctypes.c_int32), ("batch_global", ctypes.c_int32)]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("abits", ctypes.c_void_p), ("ybits", ctypes.c_void_p),
+                ("hid", ctypes.c_void_p), ("nlen", ctypes.c_void_p)]
+
+
+class State(ctypes.Structure):
+    _fields_ = [("params", ctypes.c_void_p), ("adam_m", ctypes.c_void_p),
+                ("adam_v", ctypes.c_void_p), ("beta_pow", ctypes.c_void_p)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("probs", ctypes.c_void_p), ("logits", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p)]
+
+
+EXPORTS = ["hdg_version", "hdg_last_error", "hdg_param_count", "hdg_grad_len",
+           "hdg_workspace_bytes", "hdg_fwd_bwd", "hdg_fwd_bwd_events", "hdg_adam_tf",
+           "hdg_train_step", "hdg_forward", "hdg_debug_mid_stamps"]
+
+_lib = None
+
+
+def load(path=None):
+    """Load (once) and type the library.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise RuntimeError("libhdgnn.so is not built (%s); run __graft_entry__.build() or "
+                           "python hd-gnn_amd/hdgnn/build.py" % path)
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    vp, f32, i32 = ctypes.c_void_p, ctypes.c_float, ctypes.c_int32
+    lib.hdg_version.restype = ctypes.c_int
+    lib.hdg_last_error.restype = ctypes.c_char_p
+    lib.hdg_param_count.argtypes = [i32]
+    lib.hdg_grad_len.argtypes = [i32]
+    lib.hdg_workspace_bytes.argtypes = [P(Shape)]
+    lib.hdg_workspace_bytes.restype = ctypes.c_size_t
+    lib.hdg_fwd_bwd.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp]
+    lib.hdg_fwd_bwd_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp, vp]
+    lib.hdg_debug_mid_stamps.argtypes = [P(Shape), P(Batch), vp, vp, vp, vp]
+    lib.hdg_adam_tf.argtypes = [P(Shape), P(State), vp, f32, vp, vp]
+    lib.hdg_train_step.argtypes = [P(Shape), P(Batch), P(State), f32, P(Outputs), vp, vp, vp]
+    lib.hdg_forward.argtypes = [P(Shape), P(Batch), vp, P(Outputs), vp, vp, vp]
+    for name in EXPORTS:
+        getattr(lib, name)
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().hdg_last_error().decode(errors="replace")
+        raise RuntimeError("libhdgnn error %d: %s" % (rc, msg))
+    return rc
+
+
+class HipEvents:
+    """hipEvent_t handles from the HIP runtime torch already loaded (for per-kernel timing
+    on the stream the kernels run on; torch.cuda.Event only sees torch's own stream API)."""
+
+    def __init__(self, n):
+        self.rt = ctypes.CDLL("libamdhip64.so.7")
+        self.rt.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                                ctypes.c_void_p]
+        self.rt.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+        self.rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.ev = (ctypes.c_void_p * n)()
+        for i in range(n):
+            h = ctypes.c_void_p()
+            if self.rt.hipEventCreate(ctypes.byref(h)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+            self.ev[i] = h
+        self.n = n
+
+    def elapsed_ms(self, a, b):
+        self.rt.hipEventSynchronize(self.ev[b])
+        out = ctypes.c_float()
+        if self.rt.hipEventElapsedTime(ctypes.byref(out), self.ev[a], self.ev[b]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return out.value
+
+    def __del__(self):
+        try:
+            for i in range(self.n):
+                self.rt.hipEventDestroy(self.ev[i])
+        except Exception:
+            pass

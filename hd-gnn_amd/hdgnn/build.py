@@ -1,0 +1,33 @@
+"""Build libhdgnn.so in-tree for gfx950 (hipcc, no torch extension machinery).
+
+    python hd-gnn_amd/hdgnn/build.py
+"""
+import os
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(_HERE)
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+
+def build(verbose=False):
+    src = os.path.join(CSRC, "hdgnn.hip")
+    out = os.path.join(CSRC, "libhdgnn.so")
+    deps = [src, os.path.join(ROOT, "include", "hdgnn.h")]
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp", src]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

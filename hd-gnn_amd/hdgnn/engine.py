@@ -1,0 +1,111 @@
+"""Device-side step runner over libhdgnn.so.
+
+Owns the fp32 parameter vector, TF-Adam state, gradient buffer, workspace and
+per-step outputs on one GPU.  One training step = hdg_fwd_bwd -> (all-reduce of
+the flat gradient + CE-sum trailer when world > 1) -> hdg_adam_tf, all enqueued
+on torch's current stream (so a torch.cuda.CUDAGraph can capture it).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .layout import n_params
+
+
+class Engine:
+    def __init__(self, ne, nc, batch, variant=2, device="cuda", batch_global=None, lr=3e-4,
+                 process_group=None):
+        if variant != 2:
+            raise NotImplementedError("the HIP engine implements model_2 (HD-GNN/S)")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("Engine needs a HIP device (got %s)" % self.device)
+        self.ne, self.nc, self.batch, self.variant = ne, nc, batch, variant
+        self.batch_global = batch_global or batch
+        self.lr = lr
+        self.pg = process_group
+        self.shape = _lib.Shape(batch, ne, nc, variant, self.batch_global)
+        self.np = self.lib.hdg_param_count(variant)
+        assert self.np == n_params(variant)
+        self.glen = self.lib.hdg_grad_len(variant)
+        wsb = self.lib.hdg_workspace_bytes(ctypes.byref(self.shape))
+        if wsb == 0:
+            raise RuntimeError(self.lib.hdg_last_error().decode())
+        dev = self.device
+        f32 = torch.float32
+        self.workspace = torch.empty(wsb // 4, dtype=f32, device=dev)
+        self.params = torch.zeros(self.np, dtype=f32, device=dev)
+        self.m = torch.zeros(self.np, dtype=f32, device=dev)
+        self.v = torch.zeros(self.np, dtype=f32, device=dev)
+        self.beta_pow = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
+        self.grad = torch.zeros(self.glen, dtype=f32, device=dev)
+        self.stats = torch.zeros(4, dtype=f32, device=dev)
+        self.ce_sum = torch.zeros(1, dtype=f32, device=dev)
+        pc = nc * (nc - 1)
+        self.probs = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
+        self.logits = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
+        self._state = _lib.State(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                 self.beta_pow.data_ptr())
+        self._out = _lib.Outputs(self.probs.data_ptr(), self.logits.data_ptr(),
+                                 self.stats.data_ptr())
+
+    # ---- parameters ---------------------------------------------------------
+    def set_params(self, flat):
+        flat = np.asarray(flat, np.float32).reshape(-1)
+        assert flat.size == self.np
+        self.params.copy_(torch.from_numpy(flat))
+        self.m.zero_()
+        self.v.zero_()
+        self.beta_pow.copy_(torch.tensor([0.9, 0.999]))
+
+    def get_params(self):
+        return self.params.detach().cpu().numpy().copy()
+
+    # ---- steps --------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def fwd_bwd(self, dbatch, outputs=True):
+        assert dbatch.B == self.batch and dbatch.Ne == self.ne and dbatch.Nc == self.nc
+        b = dbatch.struct()
+        out = self._out if outputs else None
+        _lib.check(self.lib.hdg_fwd_bwd(ctypes.byref(self.shape), ctypes.byref(b),
+                                        ctypes.c_void_p(self.params.data_ptr()),
+                                        ctypes.c_void_p(self.grad.data_ptr()),
+                                        ctypes.byref(out) if out is not None else None,
+                                        ctypes.c_void_p(self.workspace.data_ptr()),
+                                        self._stream()))
+
+    def allreduce(self):
+        if self.pg is not None or (torch.distributed.is_available()
+                                   and torch.distributed.is_initialized()
+                                   and torch.distributed.get_world_size() > 1):
+            torch.distributed.all_reduce(self.grad, group=self.pg)
+
+    def adam(self):
+        _lib.check(self.lib.hdg_adam_tf(ctypes.byref(self.shape), ctypes.byref(self._state),
+                                        ctypes.c_void_p(self.grad.data_ptr()),
+                                        ctypes.c_float(self.lr),
+                                        ctypes.c_void_p(self.stats.data_ptr()), self._stream()))
+
+    def train_step(self, dbatch, outputs=True):
+        """sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer]) equivalent:
+        outputs land in self.probs / self.stats (pre-update), params updated in place."""
+        self.fwd_bwd(dbatch, outputs)
+        self.allreduce()
+        self.adam()
+
+    def forward(self, dbatch):
+        """sess.run([loss_Hedge_mse, loss_map, C_edge_output2]) equivalent (test path)."""
+        assert dbatch.B == self.batch
+        b = dbatch.struct()
+        _lib.check(self.lib.hdg_forward(ctypes.byref(self.shape), ctypes.byref(b),
+                                        ctypes.c_void_p(self.params.data_ptr()),
+                                        ctypes.byref(self._out),
+                                        ctypes.c_void_p(self.ce_sum.data_ptr()),
+                                        ctypes.c_void_p(self.workspace.data_ptr()),
+                                        self._stream()))
+        return self.probs, self.logits, self.ce_sum

@@ -1,0 +1,113 @@
+/*
+ * hdgnn.h -- C ABI of the MI355X-native HD-GNN training-step engine (libhdgnn.so).
+ *
+ * The reference has no FFI: its only boundary is Python -> TF1 C++ runtime at
+ * sess.run().  These entry points are what that boundary would bind for the
+ * north-star path, one per sess.run() the reference issues:
+ *
+ *   hdg_train_step   sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer],
+ *                             feed_dict)                      model_2.py:369-383
+ *                    = hdg_fwd_bwd + hdg_adam_tf (single process)
+ *   hdg_fwd_bwd      forward + backward of train_loss (model_2.py:336) -> flat gradient
+ *                    of the data term + CE sum; the DP all-reduce sits between this
+ *                    and hdg_adam_tf
+ *   hdg_adam_tf      AdamOptimizer(0.0003).minimize(train_loss) (model_2.py:337-338):
+ *                    adds the loss_para / loss_map gradients, applies TF1 ApplyAdam
+ *   hdg_forward      sess.run([loss_Hedge_mse, loss_map, C_edge_output2], feed_dict)
+ *                    model_2.py:486-502 (test path, forward only)
+ *
+ * Conventions
+ *   - every pointer is a caller-owned DEVICE pointer (the library never allocates);
+ *     `stream` is a hipStream_t passed as void*; all work is enqueued on it, no host
+ *     synchronisation happens inside any call (graph-capturable).
+ *   - return 0 on success, HDG_EINVAL for a shape/argument error, or the hipError_t
+ *     of a failed launch; hdg_last_error() gives a thread-local message.
+ *   - parameters are one flat fp32 vector in tf.global_variables() order with TF
+ *     (in,out) row-major weights (hdg_param_count()).
+ *   - the library keeps no global mutable state apart from the thread-local error.
+ */
+#ifndef HDGNN_H
+#define HDGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDG_ABI_VERSION 1
+#define HDG_EINVAL 1000
+
+/* Per-launch problem shape (one rank's share of the commit batch). */
+typedef struct hdg_shape {
+    int32_t batch;      /* commits in this call (Mini_batch per rank)            */
+    int32_t ne;         /* entity nodes per commit   (main.py --Ne, 2 <= ne <= 256) */
+    int32_t nc;         /* hunk nodes per commit     (main.py --Nc, 2 <= nc <= 160) */
+    int32_t variant;    /* model_<variant>.py; this build implements 2            */
+    int32_t batch_global; /* commits summed by the CE mean across all ranks       */
+} hdg_shape;
+
+/* One batch of commits in compact device form (replaces the 12-tuple feed of
+ * utils2.read_data, utils2.py:248-253, bit-exactly).       */
+typedef struct hdg_batch {
+    const float*    x;      /* [B][ne]     node attribute = diag(CAdjs)  (E_node_train)   */
+    const uint32_t* abits;  /* [B][ne][ceil(ne/32)] entity class bits: bit j of row i =
+                               (E_edge class of relation (i,j) == 1); diagonal bits 0     */
+    const uint32_t* ybits;  /* [B][nc][ceil(nc/32)] hunk class bits (C_edge), diag 0      */
+    const int32_t*  hid;    /* [B][ne] Esc/Etc hunk row of index line i' (-1 = none)      */
+    const int32_t*  nlen;   /* [B] n = len(readlines()[:Ne]) of the commit's index file   */
+} hdg_batch;
+
+/* Adam / parameter state (all device, fp32). */
+typedef struct hdg_state {
+    float* params;       /* [P] */
+    float* adam_m;       /* [P] */
+    float* adam_v;       /* [P] */
+    float* beta_pow;     /* [2] beta1^t, beta2^t (TF beta1_power/beta2_power vars) */
+} hdg_state;
+
+/* Per-step outputs (device). Any pointer may be NULL to skip that output. */
+typedef struct hdg_outputs {
+    float* probs;        /* [B][2][nc(nc-1)]  C_edge_output2        */
+    float* logits;       /* [B][2][nc(nc-1)]  C_edge_output2_logits */
+    float* stats;        /* [4] ce (loss_Hedge_mse), loss_map, loss_para, train_loss
+                            (pre-update values, as sess.run returns them)              */
+} hdg_outputs;
+
+int         hdg_version(void);
+const char* hdg_last_error(void);
+int         hdg_param_count(int32_t variant);
+/* length of the gradient buffer hdg_fwd_bwd fills: param_count + 4 trailer slots
+ * (slot P = CE sum over this call's relations); all-reduce the whole buffer.      */
+int         hdg_grad_len(int32_t variant);
+size_t      hdg_workspace_bytes(const hdg_shape* shape);
+
+int hdg_fwd_bwd(const hdg_shape* shape, const hdg_batch* batch, const float* params,
+                float* grad, hdg_outputs* out, void* workspace, void* stream);
+
+/* hdg_fwd_bwd with hipEvent_t events[5] recorded on `stream` before k_entity_fwd,
+ * k_commit_mid, k_entity_bwd, k_grad_reduce and after the last launch (per-kernel
+ * timing for bench.py; events may be NULL).                                       */
+int hdg_fwd_bwd_events(const hdg_shape* shape, const hdg_batch* batch, const float* params,
+                       float* grad, hdg_outputs* out, void* workspace, void* stream,
+                       void* const* events);
+
+/* Diagnostic: run k_commit_mid alone with s_memrealtime (100 MHz) stamps at every phase
+ * barrier, stamps[B][32] (device); needs a preceding hdg_fwd_bwd on the same workspace. */
+int hdg_debug_mid_stamps(const hdg_shape* shape, const hdg_batch* batch, const float* params,
+                         void* workspace, unsigned long long* stamps, void* stream);
+
+int hdg_adam_tf(const hdg_shape* shape, hdg_state* state, const float* grad,
+                float lr, float* stats, void* stream);
+
+int hdg_train_step(const hdg_shape* shape, const hdg_batch* batch, hdg_state* state,
+                   float lr, hdg_outputs* out, float* grad, void* workspace, void* stream);
+
+int hdg_forward(const hdg_shape* shape, const hdg_batch* batch, const float* params,
+                hdg_outputs* out, float* ce_sum, void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDGNN_H */

@@ -1,0 +1,48 @@
+"""The C-ABI library loads on CPU and exports every symbol include/hdgnn.h declares
+(no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+from conftest import ROOT
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "hdgnn.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(hdg_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for want in ("hdg_fwd_bwd", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
+                 "hdg_workspace_bytes", "hdg_last_error", "hdg_version"):
+        assert want in names
+
+
+def test_library_exports_every_declared_symbol():
+    from hdgnn import _lib
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (hdg_\w+)", out))
+    assert set(_declared()) <= exported
+
+
+def test_host_only_entry_points():
+    from hdgnn import _lib
+    lib = _lib.load()
+    assert lib.hdg_version() == 1
+    assert lib.hdg_param_count(2) == 2127
+    assert lib.hdg_grad_len(2) == 2131
+    ok = _lib.Shape(100, 200, 74, 2, 100)
+    assert lib.hdg_workspace_bytes(ctypes.byref(ok)) > 0
+    bad = _lib.Shape(100, 300, 74, 2, 100)
+    assert lib.hdg_workspace_bytes(ctypes.byref(bad)) == 0
+    assert b"ne must be" in lib.hdg_last_error()
+    bad_v = _lib.Shape(4, 20, 10, 4, 4)
+    assert lib.hdg_workspace_bytes(ctypes.byref(bad_v)) == 0
+    assert b"variant" in lib.hdg_last_error()

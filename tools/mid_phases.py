@@ -1,0 +1,34 @@
+"""Diagnostic: per-phase wall time of k_commit_mid from s_memrealtime stamps (100 MHz)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "hd-gnn_amd"))
+from hdgnn import _lib, layout  # noqa: E402
+from hdgnn.engine import Engine  # noqa: E402
+from hdgnn.synth import synth_commits  # noqa: E402
+
+B, ne, nc = 100, 200, 74
+cb = synth_commits(B, ne, nc, 1)
+db = cb.to_device()
+eng = Engine(ne, nc, B)
+eng.set_params(layout.init_flat(0))
+for _ in range(3):
+    eng.train_step(db)
+st = torch.zeros(B * 32, dtype=torch.int64, device="cuda")
+for _ in range(3):
+    _lib.check(eng.lib.hdg_debug_mid_stamps(ctypes.byref(eng.shape), ctypes.byref(db.struct()),
+                                            ctypes.c_void_p(eng.params.data_ptr()),
+                                            ctypes.c_void_p(eng.workspace.data_ptr()),
+                                            ctypes.c_void_p(st.data_ptr()), eng._stream()))
+torch.cuda.synchronize()
+s = st.view(B, 32).cpu().numpy().astype(np.int64)
+n = int((s[0] > 0).sum())
+d = np.diff(s[:, :n], axis=1) * 10e-3   # us
+med = np.median(d, axis=0)
+for i, v in enumerate(med):
+    print("phase %2d->%2d  %8.2f us" % (i, i + 1, v))
+print("total (median block) %.1f us; block span max %.1f us" % (np.median(d.sum(1)), d.sum(1).max()))
