@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--nc", type=int, default=74)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     args = ap.parse_args()
 
@@ -133,14 +134,19 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
+    if args.no_graph:
+        step = lambda: eng.train_step(db)
+    else:
+        eng.capture(db)                          # one HIP graph per training step
+        step = eng.replay
     for _ in range(args.warmup):
-        eng.train_step(db)
+        step()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.train_step(db)
+        step()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -199,6 +205,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)",
             "config": {"workload": "model_2 (HD-GNN/S) train step: fwd+bwd+TF-Adam, glide step=2",
+                       "launch": "eager" if args.no_graph else "hipGraph replay per step",
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -31,7 +31,7 @@
 namespace {
 
 constexpr int HS = 20;              // h_size = De_e = De_er (model_2.py:163, 192, 247, 306)
-constexpr int NT_MID = 512;         // k_commit_mid block
+constexpr int NT_MID = 1024;        // k_commit_mid block
 constexpr int KK_MID = 5;           // hidden units per pair-tile chunk in k_commit_mid
 constexpr int KK_E = 4;             // hidden units per block in the entity kernels
 constexpr int NCHUNK_E = HS / KK_E;
@@ -65,12 +65,20 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-  v = row16_sum(v);
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+// Sum over the 4 DPP rows of a wave for every lane column: lane l gets
+// v[l] + v[l^16] + v[l^32] + v[l^48].  v_permlane{32,16}_swap in the VALU (no LDS);
+// inline asm because the ROCm 7.2 builtins mis-assign the two results, with the two
+// wait states the swap needs after a VALU write of its operands inside the string.
+__device__ __forceinline__ float xrow_sum4(float v) {
+  float x = v, y = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  const float s = x + y;
+  float p = s, q = s;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(p), "+v"(q));
+  return p + q;
 }
+
+__device__ __forceinline__ float wave_sum(float v) { return xrow_sum4(row16_sum(v)); }
 
 __device__ __forceinline__ float reluf(float v) { return fmaxf(v, 0.f); }
 
@@ -78,12 +86,14 @@ __device__ __forceinline__ uint32_t getbit(const uint32_t* rowbits, int j) {
   return (rowbits[j >> 5] >> (j & 31)) & 1u;
 }
 
-// q = r / d, rem = r % d for 0 <= r < 2^20, 1 <= d < 2^12 (exact via float + fix-up)
-__device__ __forceinline__ void divmod_small(int r, int d, float inv, int& q, int& rem) {
-  q = (int)((float)r * inv);
-  rem = r - q * d;
-  if (rem < 0) { --q; rem += d; }
-  else if (rem >= d) { ++q; rem -= d; }
+// q = r / d, rem = r % d for 0 <= r < 2^22, 1 <= d < 2^12: float estimate + one select
+// correction, 24-bit multiplies, no branches (keeps unrolled loads in flight)
+__device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& rem) {
+  int q0 = (int)((float)r * inv);
+  int r0 = r - __mul24(q0, d);
+  const bool lo = r0 < 0, hi = r0 >= d;
+  q = lo ? q0 - 1 : (hi ? q0 + 1 : q0);
+  rem = lo ? r0 + d : (hi ? r0 - d : r0);
 }
 
 // ------------------------------------------------------------------------------
@@ -94,18 +104,24 @@ __device__ __forceinline__ void divmod_small(int r, int d, float inv, int& q, in
 //   z_ij  = A[i] + B[j] + y_ij * dl          (y_ij = bit j of row i)
 //   MODE 0  e = relu(z)                                       (forward sums)
 //   MODE 1  e = [z > 0] * (wr[i] + wc[j])  , ysum += y*e      (backward, node weights)
-//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e      (backward, pair weights)
-//   Rout[i] = sum_j e_ij   Cout[j] = sum_i e_ij   (diagonal INCLUDED; callers subtract)
+//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e,  zsum += z*e   (pair weights)
+//   Rout[i] = sum_j e_ij   Cout[j] = sum_i e_ij   (diagonal INCLUDED for MODE 0/1:
+//   callers subtract it; MODE 2 masks it)
 // A, B, wr, wc, Rout, Cout: LDS [node][LD] (rows/cols >= N padded with -inf in A/B).
+// Rout may alias A and Cout may alias B (rows are consumed before they are written,
+// columns are written after the closing barrier).  cred: 4*16*SMAX*KK + 8*KK words.
 // Every thread of the BLOCK must call this the same number of times (barriers).
 // ------------------------------------------------------------------------------
+template <int SMAX, int KK>
+constexpr int tile_cred_words() { return 4 * 16 * SMAX * KK + 8 * KK; }
+
 template <int KK, int SMAX, int MODE, int LD>
 __device__ __forceinline__ void pair_tile(
-    const int N, const int t, const float* __restrict__ A, const float* __restrict__ Bv,
-    const int k0, const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
+    const int N, const int t, const float* A, const float* Bv, const int k0,
+    const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
     const float* __restrict__ wr, const float* __restrict__ wc,
-    const float* __restrict__ gam, const int gld, float* __restrict__ Rout,
-    float* __restrict__ Cout, float* __restrict__ ysum, float* __restrict__ cred) {
+    const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
+    float* __restrict__ ysum, float* __restrict__ zsum, float* __restrict__ cred) {
   constexpr int NP16 = 16 * SMAX;
   constexpr int NW = (SMAX + 1) / 2;
   const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
@@ -116,9 +132,9 @@ __device__ __forceinline__ void pair_tile(
   for (int c = 0; c < SMAX; ++c)
 #pragma unroll
     for (int k = 0; k < KK; ++k) cacc[c][k] = 0.f;
-  float yacc[KK], dk[KK];
+  float yacc[KK], zacc[KK], dk[KK];
 #pragma unroll
-  for (int k = 0; k < KK; ++k) { yacc[k] = 0.f; dk[k] = dl[k0 + k]; }
+  for (int k = 0; k < KK; ++k) { yacc[k] = 0.f; zacc[k] = 0.f; dk[k] = dl[k0 + k]; }
 
   for (int s = 0; s < S; ++s) {
     const int i = ti + 16 * s;
@@ -131,14 +147,21 @@ __device__ __forceinline__ void pair_tile(
       racc[k] = 0.f;
     }
     uint32_t wrow[NW];
+    const int ib = iv ? i : 0;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) wrow[q] = (iv && q < W) ? bits[i * W + q] : 0u;
+    for (int q = 0; q < NW; ++q) {      // branch-free: clamped load, masked value
+      const uint32_t w = bits[ib * W + (q < W ? q : 0)];
+      wrow[q] = (iv && q < W) ? w : 0u;
+    }
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
       const float af = (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
       float g = 0.f;
-      if constexpr (MODE == 2) g = (iv && j < N && j != i) ? gam[i * gld + j] : 0.f;
+      if constexpr (MODE == 2) {   // branch-free: clamped load, masked value
+        const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;
+        g = gam[ic * gld + jc] * ((iv && j < N && j != i) ? 1.f : 0.f);
+      }
 #pragma unroll
       for (int k = 0; k < KK; ++k) {
         const float z = a[k] + fmaf(af, dk[k], Bv[j * LD + k0 + k]);
@@ -149,6 +172,7 @@ __device__ __forceinline__ void pair_tile(
           const float w = (MODE == 1) ? (rw[k] + wc[j * LD + k0 + k]) : g;
           e = (z > 0.f) ? w : 0.f;
           yacc[k] = fmaf(af, e, yacc[k]);
+          if constexpr (MODE == 2) zacc[k] = fmaf(reluf(z), e, zacc[k]);   // z may be -inf
         }
         racc[k] += e;
         cacc[c][k] += e;
@@ -162,13 +186,12 @@ __device__ __forceinline__ void pair_tile(
   }
   // close the column partials: 4 ti per wave by shuffles, then 4 waves via LDS
   float* credy = cred + 4 * NP16 * KK;
+  float* credz = credy + 4 * KK;
 #pragma unroll
   for (int c = 0; c < SMAX; ++c)
 #pragma unroll
     for (int k = 0; k < KK; ++k) {
-      float v = cacc[c][k];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
+      const float v = xrow_sum4(cacc[c][k]);
       if (lane < 16) cred[(wv * NP16 + tj + 16 * c) * KK + k] = v;
     }
   if constexpr (MODE != 0) {
@@ -176,6 +199,10 @@ __device__ __forceinline__ void pair_tile(
     for (int k = 0; k < KK; ++k) {
       const float v = wave_sum(yacc[k]);
       if (lane == 0) credy[wv * KK + k] = v;
+      if constexpr (MODE == 2) {
+        const float vz = wave_sum(zacc[k]);
+        if (lane == 0) credz[wv * KK + k] = vz;
+      }
     }
   }
   __syncthreads();
@@ -186,66 +213,85 @@ __device__ __forceinline__ void pair_tile(
   }
   if constexpr (MODE != 0) {
     if (t < KK) ysum[k0 + t] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
+    if constexpr (MODE == 2) {
+      if (t < KK) zsum[k0 + t] = credz[t] + credz[KK + t] + credz[2 * KK + t] + credz[3 * KK + t];
+    }
   }
   __syncthreads();
 }
 
 // ------------------------------------------------------------------------------
-// Generic row/column sweep over an N x N relation grid by NG 256-thread groups:
+// Row/column sweep over an N x N relation grid by NG 256-thread groups, columns
+// split across groups (group g owns column blocks c = g, g+NG, ...):
 //   Rout[i][w] = sum_j f(i,j)[w],  Cout[j][w] = sum_i f(i,j)[w]
-// f returns VW floats (zero for i == j or no relation).  Group g takes rows
-// s = g, g+NG, ...; rows close by 16-lane DPP, columns by registers + LDS.
+// f(i,j,v) must be branch-free and safe on any i,j in [0,N) (it is called on clamped
+// indices and masked: i == j and out-of-range slots contribute 0).
+// scratch: sweep_scratch_words(SMAX, VW, NG) words.
 // ------------------------------------------------------------------------------
+__host__ __device__ constexpr int sweep_scratch_words(int smax, int vw, int ng) {
+  return (ng + 4) * 16 * smax * vw;
+}
+
 template <int VW, int SMAX, int NG, class F>
 __device__ __forceinline__ void grid_sweep(const int N, const int t, F f, float* __restrict__ Rout,
-                                           float* __restrict__ Cout, float* __restrict__ cred) {
+                                           float* __restrict__ Cout, float* __restrict__ scratch) {
   constexpr int NP16 = 16 * SMAX;
+  constexpr int CPG = SMAX / NG;       // column blocks per group
+  static_assert(SMAX % NG == 0, "SMAX must be a multiple of NG");
   const int g = t >> 8, tg = t & 255;
-  const int tj = tg & 15, ti = tg >> 4, lane = t & 63, wv = t >> 6;
+  const int tj = tg & 15, ti = tg >> 4, lane = t & 63, wg = tg >> 6;
   const int S = (N + 15) >> 4;
-  float cacc[SMAX][VW];
+  float* Rpart = scratch;                          // [NG][NP16][VW]
+  float* Cpart = scratch + NG * NP16 * VW;         // [NG][4][16*CPG][VW]
+  float cacc[CPG][VW];
 #pragma unroll
-  for (int c = 0; c < SMAX; ++c)
+  for (int c = 0; c < CPG; ++c)
 #pragma unroll
     for (int w = 0; w < VW; ++w) cacc[c][w] = 0.f;
-  for (int s = g; s < S; s += NG) {
+  for (int s = 0; s < S; ++s) {
     const int i = ti + 16 * s;
+    const int ic = i < N ? i : N - 1;
     float racc[VW];
 #pragma unroll
     for (int w = 0; w < VW; ++w) racc[w] = 0.f;
 #pragma unroll
-    for (int c = 0; c < SMAX; ++c) {
-      const int j = tj + 16 * c;
+    for (int cc = 0; cc < CPG; ++cc) {
+      const int j = tj + 16 * (g + NG * cc);
+      const int jc = j < N ? j : N - 1;
+      const float m = (i < N && j < N && i != j) ? 1.f : 0.f;
       float v[VW];
-#pragma unroll
-      for (int w = 0; w < VW; ++w) v[w] = 0.f;
-      if (i < N && j < N && i != j) f(i, j, v);
+      f(ic, jc, v);
 #pragma unroll
       for (int w = 0; w < VW; ++w) {
-        racc[w] += v[w];
-        cacc[c][w] += v[w];
+        racc[w] = fmaf(m, v[w], racc[w]);
+        cacc[cc][w] = fmaf(m, v[w], cacc[cc][w]);
       }
     }
 #pragma unroll
     for (int w = 0; w < VW; ++w) {
       const float r = row16_sum(racc[w]);
-      if (tj == 0 && i < N) Rout[i * VW + w] = r;
+      if (tj == 0) Rpart[(g * NP16 + i) * VW + w] = r;
     }
   }
 #pragma unroll
-  for (int c = 0; c < SMAX; ++c)
+  for (int cc = 0; cc < CPG; ++cc)
 #pragma unroll
     for (int w = 0; w < VW; ++w) {
-      float v = cacc[c][w];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lane < 16) cred[(wv * NP16 + tj + 16 * c) * VW + w] = v;
+      const float v = xrow_sum4(cacc[cc][w]);
+      if (lane < 16) Cpart[((g * 4 + wg) * 16 * CPG + tj + 16 * cc) * VW + w] = v;
     }
   __syncthreads();
-  for (int e = t; e < NP16 * VW; e += 256 * NG) {
-    float acc = 0.f;
-    for (int q = 0; q < 4 * NG; ++q) acc += cred[q * NP16 * VW + e];
-    if (e / VW < N) Cout[e] = acc;
+  for (int e = t; e < N * VW; e += 256 * NG) {
+    const int i = e / VW, w = e - i * VW;
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) r += Rpart[(q * NP16 + i) * VW + w];
+    Rout[e] = r;
+    const int jb = i >> 4, gq = jb % NG, cc = jb / NG, tq = i & 15;
+    float c = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c += Cpart[((gq * 4 + q) * 16 * CPG + tq + 16 * cc) * VW + w];
+    Cout[e] = c;
   }
   __syncthreads();
 }
@@ -263,7 +309,7 @@ struct EntSmem {
   alignas(16) float R[NP16 * KK_E];
   alignas(16) float C[NP16 * KK_E];
   alignas(16) float rho[NP16 * KK_E];
-  alignas(16) float cred[4 * NP16 * KK_E + 4 * KK_E];
+  alignas(16) float cred[tile_cred_words<SMAX, KK_E>()];
   alignas(16) float xs[NP16];
   float dl[KK_E];
   float ysum[KK_E];
@@ -307,7 +353,7 @@ __global__ __launch_bounds__(256) void k_entity_fwd(const float* __restrict__ x,
   entity_setup<SMAX>(sm, x, abits, Wp, Ne, b, k0, t);
   __syncthreads();
   pair_tile<KK_E, SMAX, 0, KK_E>(Ne, t, sm.u, sm.v, 0, sm.dl, sm.bits, (Ne + 31) >> 5, nullptr,
-                                 nullptr, nullptr, 0, sm.R, sm.C, nullptr, sm.cred);
+                                 nullptr, nullptr, 0, sm.R, sm.C, nullptr, nullptr, sm.cred);
   float* Pb = Pout + (size_t)b * Ne * HS;
   for (int e = t; e < Ne * KK_E; e += 256) {
     const int i = e / KK_E, k = e - i * KK_E;
@@ -335,7 +381,7 @@ __global__ __launch_bounds__(256) void k_entity_bwd(const float* __restrict__ x,
   }
   __syncthreads();
   pair_tile<KK_E, SMAX, 1, KK_E>(Ne, t, sm.u, sm.v, 0, sm.dl, sm.bits, (Ne + 31) >> 5, sm.rho,
-                                 sm.rho, nullptr, 0, sm.R, sm.C, sm.ysum, sm.cred);
+                                 sm.rho, nullptr, 0, sm.R, sm.C, sm.ysum, nullptr, sm.cred);
   // remove the diagonal term the tile included (a_ii = 0)
   for (int e = t; e < Ne * KK_E; e += 256) {
     const float z = sm.u[e] + sm.v[e];
@@ -371,14 +417,18 @@ __global__ __launch_bounds__(256) void k_entity_bwd(const float* __restrict__ x,
 }
 
 // ------------------------------------------------------------------------------
-// k_commit_mid: everything between the two entity pair sweeps, one block/commit.
-// All per-commit node arrays live in LDS; phase-local buffers alias one region.
+// k_commit_mid: everything between the two entity pair sweeps, one 1024-thread
+// block per commit.  Node arrays live in LDS; one union region U is re-carved per
+// phase (entity staging -> X1 sweep -> hunk buffers -> X1 backward -> E3 backward).
+// E_bar and the E3 hidden layer are parked in the workspace across the hunk phases.
+// Node matvecs use a (k, slice) thread map with the weight column held in registers.
 // ------------------------------------------------------------------------------
-constexpr int NBUF_H = 6;           // hunk node buffers [NC16][HS]
+constexpr int NG_MID = NT_MID / 256;            // 4 pair-tile groups, one k-chunk each
+constexpr int NBUF_H = 6;                       // hunk node buffers [NC16][HS]
+constexpr int NSL = NT_MID / HS;                // 51 node slices for (k, slice) matvecs
 
 struct MidLayout {   // offsets in 4-byte words into the dynamic LDS arena
-  int W, xs, xps, os, dxr, dxc, hid, ab, yb, nb, dnb, misc, Mm, Xm, E0, E1, hreg, hreg_words,
-      cred, red, total;
+  int W, xs, xps, os, dxr, dxc, hid, ab, yb, nb, dnb, misc, Mm, Xm, red, U, Uwords, total;
 };
 
 __host__ __device__ inline MidLayout mid_layout(int Ne, int Nc, int smaxc) {
@@ -386,6 +436,7 @@ __host__ __device__ inline MidLayout mid_layout(int Ne, int Nc, int smaxc) {
   const int NC16 = 16 * smaxc;
   const int NE4 = (Ne + 3) & ~3;
   const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
+  const int cred = 4 * 16 * smaxc * KK_MID + 8 * KK_MID;
   int o = 0;
   L.W = o;    o += (m2::NP + 3) & ~3;
   L.xs = o;   o += NE4;
@@ -398,19 +449,36 @@ __host__ __device__ inline MidLayout mid_layout(int Ne, int Nc, int smaxc) {
   L.yb = o;   o += (Nc * WC + 3) & ~3;
   L.nb = o;   o += 4 * NC16;
   L.dnb = o;  o += 4 * NC16;
-  L.misc = o; o += 8 * HS;            // dlt eps cvec ysumv s0 t0 sumD spare
+  L.misc = o; o += 8 * HS;            // dlt eps cvec ysumv s0 t0 sumD zsumv
   L.Mm = o;   o += HS * HS;           // V2 . U1e
   L.Xm = o;   o += HS * HS;           // sum_p G_p (x) Dsig_p + H_p (x) Dtau_p
-  L.E0 = o;   o += NE4 * HS;          // E_bar
-  L.E1 = o;   o += NE4 * HS;          // E3 hidden h
-  int h = NBUF_H * NC16 * HS;         // hunk buffers, or (P | dq | dE) staging, or segments
-  if (3 * NE4 * HS > h) h = 3 * NE4 * HS;
-  if (8 * NE4 + 8 * 256 * 4 > h) h = 8 * NE4 + 8 * 256 * 4;   // X1 sweeps
-  L.hreg = o; L.hreg_words = h; o += h;
-  L.cred = o; o += 2 * (4 * NC16 * KK_MID + 4 * KK_MID);
   L.red = o;  o += (NT_MID / 64) * 32;
+  int u = 3 * NE4 * HS;                                            // P | E_bar | h
+  const int ux1 = 8 * NE4 + sweep_scratch_words(16, 4, NG_MID);    // X1 forward
+  const int uh = NBUF_H * NC16 * HS + NG_MID * cred;               // hunk phases
+  const int ux2 = 6 * NE4 + sweep_scratch_words(16, 2, NG_MID);    // X1 backward
+  const int ueb = 5 * NE4 * HS;                                    // E3 backward
+  if (ux1 > u) u = ux1;
+  if (uh > u) u = uh;
+  if (ux2 > u) u = ux2;
+  if (ueb > u) u = ueb;
+  L.U = o; L.Uwords = u; o += u;
   L.total = o;
   return L;
+}
+
+// dot of a 20-float LDS row (16-B aligned) with 20 register weights
+__device__ __forceinline__ float dot20(const float* row, const float (&w)[HS], float acc) {
+  const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll
+  for (int v = 0; v < HS / 4; ++v) {
+    const float4 q = r4[v];
+    acc = fmaf(q.x, w[4 * v], acc);
+    acc = fmaf(q.y, w[4 * v + 1], acc);
+    acc = fmaf(q.z, w[4 * v + 2], acc);
+    acc = fmaf(q.w, w[4 * v + 3], acc);
+  }
+  return acc;
 }
 
 template <int SMAXC, bool TRAIN, bool STAMPS = false>
@@ -418,27 +486,30 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
     const float* __restrict__ x, const uint32_t* __restrict__ abits,
     const uint32_t* __restrict__ ybits, const int32_t* __restrict__ hidg,
     const int32_t* __restrict__ nleng, const float* __restrict__ Wg,
-    const float* __restrict__ Pg, float* __restrict__ rhog, float* __restrict__ gamg,
-    float* __restrict__ part, float* __restrict__ probs, float* __restrict__ logits, int Ne,
-    int Nc, float ce_scale, unsigned long long* __restrict__ stamps) {
+    const float* __restrict__ Pg, float* __restrict__ Esave, float* __restrict__ rhog,
+    float* __restrict__ gamg, float* __restrict__ part, float* __restrict__ probs,
+    float* __restrict__ logits, int Ne, int Nc, float ce_scale,
+    unsigned long long* __restrict__ stamps) {
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
-  int nstamp = 0;
-#define MID_STAMP()                                                                    \
-  do {                                                                                 \
-    if constexpr (STAMPS) {                                                            \
-      if (threadIdx.x == 0) stamps[blockIdx.x * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
-      ++nstamp;                                                                        \
-    }                                                                                  \
-  } while (0)
-  MID_STAMP();
+  constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const MidLayout L = mid_layout(Ne, Nc, SMAXC);
   const int b = blockIdx.x, t = threadIdx.x;
-  const int lane = t & 63, wv = t >> 6;
+  const int lane = t & 63, wv = t >> 6, g = t >> 8, tg = t & 255;
+  const int mk = t % HS, msl = t / HS;            // (k, slice) map; msl == NSL idles
   const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
   const int NE4 = (Ne + 3) & ~3;
   const int Pc = Nc * (Nc - 1);
+  int nstamp = 0;
+#define MID_STAMP()                                                                     \
+  do {                                                                                  \
+    if constexpr (STAMPS) {                                                             \
+      if (threadIdx.x == 0) stamps[blockIdx.x * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
+      ++nstamp;                                                                         \
+    }                                                                                   \
+  } while (0)
+  MID_STAMP();
   float* Ws = lds + L.W;
   float* xs = lds + L.xs;
   float* xps = lds + L.xps;
@@ -457,18 +528,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* s0v = ysumv + HS;          // sigma offset
   float* t0v = s0v + HS;            // tau offset
   float* sumD = t0v + HS;
+  float* zsumv = sumD + HS;
   float* Mm = lds + L.Mm;
   float* Xm = lds + L.Xm;
-  float* Ebar = lds + L.E0;
-  float* hE = lds + L.E1;
-  float* hreg = lds + L.hreg;
-  float* Bf[NBUF_H];
-#pragma unroll
-  for (int q = 0; q < NBUF_H; ++q) Bf[q] = hreg + q * NC16 * HS;
-  float* credg = lds + L.cred + (t >> 8) * (4 * NC16 * KK_MID + 4 * KK_MID);
   float* red = lds + L.red;
+  float* U = lds + L.U;
 
   const float* Pb = Pg + (size_t)b * Ne * HS;
+  float* EbG = Esave + (size_t)b * 2 * Ne * HS;
+  float* hEG = EbG + Ne * HS;
   float* pb = part + (size_t)b * NPART;
   float* gam = gamg + (size_t)b * NC16 * NC16;
   int n = nleng[b];
@@ -478,6 +546,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   const float twoNe1 = 2.f * (float)(Ne - 1);
 
   // ---- M0: stage weights, commit inputs and P (k_entity_fwd output) -----------------
+  float* Ps = U;
+  float* Eb = U + NE4 * HS;
+  float* hE = U + 2 * NE4 * HS;
   for (int i = t; i < NP; i += NT_MID) Ws[i] = Wg[i];
   for (int i = t; i < Ne; i += NT_MID) {
     xs[i] = x[(size_t)b * Ne + i];
@@ -486,7 +557,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   for (int w = t; w < Ne * WE; w += NT_MID) ab[w] = abits[(size_t)b * Ne * WE + w];
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   {
-    float* Ps = hreg;                                 // P staged in the hunk region
     const float4* src = reinterpret_cast<const float4*>(Pb);
     float4* dst = reinterpret_cast<float4*>(Ps);
     for (int e = t; e < Ne * HS / 4; e += NT_MID) dst[e] = src[e];
@@ -495,58 +565,66 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   MID_STAMP();
 
   // ---- M1: E_bar = P W5 + 2(Ne-1) b5   (agg_entity_B1, model_2.py:181-188) ----------
-  for (int e = t; e < Ne * HS; e += NT_MID) {
-    const int i = e / HS, k = e - i * HS;
-    const float* Pi = hreg + i * HS;
-    float acc = 0.f;
+  if (msl < NSL) {
+    float w[HS];
 #pragma unroll
-    for (int m = 0; m < HS; ++m) acc = fmaf(Pi[m], Ws[E1_W5 + m * HS + k], acc);
-    Ebar[e] = fmaf(twoNe1, Ws[E1_B5 + k], acc);
+    for (int m = 0; m < HS; ++m) w[m] = Ws[E1_W5 + m * HS + mk];
+    const float bias = twoNe1 * Ws[E1_B5 + mk];
+    for (int i = msl; i < Ne; i += NSL) {
+      const float v = dot20(Ps + i * HS, w, 0.f) + bias;
+      Eb[i * HS + mk] = v;
+      EbG[i * HS + mk] = v;
+    }
   }
   __syncthreads();
   MID_STAMP();
   // ---- M2: mlp2_entity_B1 (model_2.py:190-205) --------------------------------------
-  for (int e = t; e < Ne * HS; e += NT_MID) {
-    const int i = e / HS, k = e - i * HS;
-    const float* Ei = Ebar + i * HS;
-    float acc = fmaf(xs[i], Ws[E3_W1 + k], Ws[E3_B1 + k]);
+  if (msl < NSL) {
+    float w[HS];
 #pragma unroll
-    for (int m = 0; m < HS; ++m) acc = fmaf(Ei[m], Ws[E3_W1 + (1 + m) * HS + k], acc);
-    hE[e] = reluf(acc);
+    for (int m = 0; m < HS; ++m) w[m] = Ws[E3_W1 + (1 + m) * HS + mk];
+    const float w0 = Ws[E3_W1 + mk], bb = Ws[E3_B1 + mk];
+    for (int i = msl; i < Ne; i += NSL) {
+      const float v = reluf(dot20(Eb + i * HS, w, fmaf(xs[i], w0, bb)));
+      hE[i * HS + mk] = v;
+      hEG[i * HS + mk] = v;
+    }
   }
   __syncthreads();
   MID_STAMP();
-  for (int i = t; i < Ne; i += NT_MID) {
-    const float* hi = hE + i * HS;
-    float acc = Ws[E3_B2];
+  {
+    float w[HS];
 #pragma unroll
-    for (int k = 0; k < HS; ++k) acc = fmaf(hi[k], Ws[E3_W2 + k], acc);
-    os[i] = acc;
-    xps[i] = reluf(acc);
+    for (int k = 0; k < HS; ++k) w[k] = Ws[E3_W2 + k];
+    for (int i = t; i < Ne; i += NT_MID) {
+      const float o = dot20(hE + i * HS, w, Ws[E3_B2]);
+      os[i] = o;
+      xps[i] = reluf(o);
+    }
   }
   __syncthreads();
   MID_STAMP();
 
   // ---- M3: marshalling_B2 cross-graph sum (model_2.py:146-150, utils2.py:111-137) -----
   // n_c = sum_r ([s_r=c]+[t_r=c]) B2_r,  B2_r = [x'_I, x'_J, [a=0], [a=1]] on the Ne-grid,
-  // s_r = hid[i'(r)], t_r = hid[j'(r)] on the n-grid (stride n-1).
-  float* segS = hreg;                 // [n][4] sum of B2 over n-grid row i'
-  float* segT = hreg + 4 * NE4;       // [n][4] ... over n-grid column j'
-  float* xcred = hreg + 8 * NE4;      // [8 waves][256][4]
+  // s_r = hid[i'(r)], t_r = hid[j'(r)] on the n-grid (stride n-1): row sums (segS) and
+  // column sums (segT) of the n x n grid of B2 values, then binned by hid.
+  float* segS = U;
+  float* segT = U + 4 * NE4;
   if (n >= 2) {
     const int Ne1 = Ne - 1, n1 = n - 1;
     const float invNe1 = 1.f / (float)Ne1;
-    grid_sweep<4, 16, 2>(n, t, [&](int ip, int jp, float* v) {
-      const int r = ip * n1 + jp - (jp > ip ? 1 : 0);
+    grid_sweep<4, 16, NG_MID>(n, t, [&](int ip, int jp, float* v) {
+      const int r = __mul24(ip, n1) + jp - (jp > ip ? 1 : 0);
       int I, jj;
-      divmod_small(r, Ne1, invNe1, I, jj);
-      const int J = jj + (jj >= I);
-      const float a = (float)getbit(ab + I * WE, J);
+      divmod_bf(r < 0 ? 0 : r, Ne1, invNe1, I, jj);
+      const int J = jj + (jj >= I ? 1 : 0);
+      const float a = (float)((ab[__mul24(I, WE) + (J >> 5)] >> (J & 31)) & 1u);
       v[0] = xps[I];
       v[1] = xps[J];
       v[2] = 1.f - a;
       v[3] = a;
-    }, segS, segT, xcred);
+    }, segS, segT, U + 8 * NE4);
   }
   for (int e = t; e < NC16 * 4; e += NT_MID) {
     const int c = e >> 2, m = e & 3;
@@ -588,22 +666,30 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
 
   // ---- M4: first layer of mlp_hunk_B2 split per node (model_2.py:257-260) ----------
   //   alpha_p = n_p V1[0:4] + V1[8] + c1,   beta_q = n_q V1[4:8],   delta = V1[9]-V1[8]
+  float* Bf[NBUF_H];
+#pragma unroll
+  for (int q = 0; q < NBUF_H; ++q) Bf[q] = U + q * NC16 * HS;
+  float* credg = U + NBUF_H * NC16 * HS + g * CRED;
   float* alpha = Bf[0];
   float* beta = Bf[1];
-  for (int e = t; e < NC16 * HS; e += NT_MID) {
-    const int p = e / HS, k = e - p * HS;
-    float al = -INFINITY, be = -INFINITY;
-    if (p < Nc) {
-      al = Ws[H1_W1 + 8 * HS + k] + Ws[H1_B1 + k];
-      be = 0.f;
+  if (msl < NSL) {
+    float wa[4], wb[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        al = fmaf(nb[4 * p + m], Ws[H1_W1 + m * HS + k], al);
-        be = fmaf(nb[4 * p + m], Ws[H1_W1 + (4 + m) * HS + k], be);
-      }
+    for (int m = 0; m < 4; ++m) {
+      wa[m] = Ws[H1_W1 + m * HS + mk];
+      wb[m] = Ws[H1_W1 + (4 + m) * HS + mk];
     }
-    alpha[e] = al;
-    beta[e] = be;
+    const float a0 = Ws[H1_W1 + 8 * HS + mk] + Ws[H1_B1 + mk];
+    for (int p = msl; p < NC16; p += NSL) {
+      float al = -INFINITY, be = -INFINITY;
+      if (p < Nc) {
+        const float4 nv = reinterpret_cast<const float4*>(nb)[p];
+        al = fmaf(nv.w, wa[3], fmaf(nv.z, wa[2], fmaf(nv.y, wa[1], fmaf(nv.x, wa[0], a0))));
+        be = fmaf(nv.w, wb[3], fmaf(nv.z, wb[2], fmaf(nv.y, wb[1], nv.x * wb[0])));
+      }
+      alpha[p * HS + mk] = al;
+      beta[p * HS + mk] = be;
+    }
   }
   __syncthreads();
   MID_STAMP();
@@ -611,11 +697,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   // ---- M5: hunk pair sums G_p = sum_q g1_pq, H_q = sum_p g1_pq (model_2.py:260-275) ---
   float* G = Bf[2];
   float* Hh = Bf[3];
-  const int tg = t & 255;
-  for (int ch = (t >> 8); ch < HS / KK_MID; ch += NT_MID / 256)
-    pair_tile<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, ch * KK_MID, dlt, yb, WC, nullptr,
-                                    nullptr, nullptr, 0, G, Hh, nullptr, credg);
-  MID_STAMP();
+  pair_tile<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
+                                  nullptr, 0, G, Hh, nullptr, nullptr, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const float dg = reluf(alpha[e] + beta[e]);
     G[e] -= dg;
@@ -628,21 +711,20 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   //   sigma_p = G_p M + (Nc-1) c2 U1e + U1[0] + d1,  tau_q = H_q M + (Nc-1) c2 U1e
   float* sig = Bf[4];
   float* tau = Bf[5];
-  for (int e = t; e < NC16 * HS; e += NT_MID) {
-    const int p = e / HS, k = e - p * HS;
-    float as = -INFINITY, at = -INFINITY;
-    if (p < Nc) {
-      as = s0v[k];
-      at = t0v[k];
+  if (msl < NSL) {
+    float w[HS];
 #pragma unroll
-      for (int l = 0; l < HS; ++l) {
-        const float w = Mm[l * HS + k];
-        as = fmaf(G[p * HS + l], w, as);
-        at = fmaf(Hh[p * HS + l], w, at);
+    for (int l = 0; l < HS; ++l) w[l] = Mm[l * HS + mk];
+    const float s0 = s0v[mk], t0 = t0v[mk];
+    for (int p = msl; p < NC16; p += NSL) {
+      float as = -INFINITY, at = -INFINITY;
+      if (p < Nc) {
+        as = dot20(G + p * HS, w, s0);
+        at = dot20(Hh + p * HS, w, t0);
       }
+      sig[p * HS + mk] = as;
+      tau[p * HS + mk] = at;
     }
-    sig[e] = as;
-    tau[e] = at;
   }
   __syncthreads();
   MID_STAMP();
@@ -651,41 +733,34 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
   float ce_acc = 0.f, gsum = 0.f;
-  float du2[HS];
-#pragma unroll
-  for (int k = 0; k < HS; ++k) du2[k] = 0.f;
   {
     const int Nc1i = Nc - 1;
     const float invNc1 = 1.f / (float)Nc1i;
-    float w0[HS], w1[HS], ep[HS];
+    float w0[HS], w1[HS];
 #pragma unroll
     for (int k = 0; k < HS; ++k) {
       w0[k] = Ws[H2_W2 + 2 * k];
       w1[k] = Ws[H2_W2 + 2 * k + 1];
-      ep[k] = eps[k];
     }
     const float b0 = Ws[H2_B2], b1 = Ws[H2_B2 + 1];
+    const float4* ep4 = reinterpret_cast<const float4*>(eps);
     for (int e = t; e < Pc; e += NT_MID) {
       int p, qq;
-      divmod_small(e, Nc1i, invNc1, p, qq);
-      const int q = qq + (qq >= p);
-      const float yf = (float)getbit(yb + p * WC, q);
+      divmod_bf(e, Nc1i, invNc1, p, qq);
+      const int q = qq + (qq >= p ? 1 : 0);
+      const float yf = (float)((yb[__mul24(p, WC) + (q >> 5)] >> (q & 31)) & 1u);
       const float4* sp = reinterpret_cast<const float4*>(sig + p * HS);
       const float4* tq = reinterpret_cast<const float4*>(tau + q * HS);
-      float kk[HS];
-#pragma unroll
-      for (int v = 0; v < HS / 4; ++v) {
-        const float4 a = sp[v], c = tq[v];
-        kk[4 * v + 0] = reluf(a.x + fmaf(yf, ep[4 * v + 0], c.x));
-        kk[4 * v + 1] = reluf(a.y + fmaf(yf, ep[4 * v + 1], c.y));
-        kk[4 * v + 2] = reluf(a.z + fmaf(yf, ep[4 * v + 2], c.z));
-        kk[4 * v + 3] = reluf(a.w + fmaf(yf, ep[4 * v + 3], c.w));
-      }
       float z0 = b0, z1 = b1;
 #pragma unroll
-      for (int k = 0; k < HS; ++k) {
-        z0 = fmaf(kk[k], w0[k], z0);
-        z1 = fmaf(kk[k], w1[k], z1);
+      for (int v = 0; v < HS / 4; ++v) {
+        const float4 a = sp[v], c = tq[v], ee = ep4[v];
+        const float k0 = reluf(a.x + fmaf(yf, ee.x, c.x));
+        const float k1 = reluf(a.y + fmaf(yf, ee.y, c.y));
+        const float k2 = reluf(a.z + fmaf(yf, ee.z, c.z));
+        const float k3 = reluf(a.w + fmaf(yf, ee.w, c.w));
+        z0 = fmaf(k3, w0[4 * v + 3], fmaf(k2, w0[4 * v + 2], fmaf(k1, w0[4 * v + 1], fmaf(k0, w0[4 * v], z0))));
+        z1 = fmaf(k3, w1[4 * v + 3], fmaf(k2, w1[4 * v + 2], fmaf(k1, w1[4 * v + 1], fmaf(k0, w1[4 * v], z1))));
       }
       const float mx = fmaxf(z0, z1);
       const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
@@ -696,61 +771,57 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
       if (prb) { prb[e] = p0; prb[Pc + e] = p1; }
       if (lgb) { lgb[e] = z0; lgb[Pc + e] = z1; }
       if constexpr (TRAIN) {
+        if (qq == p) gam[p * NC16 + p] = 0.f;     // defined diagonal (read masked in M8)
         const float gmm = ce_scale * (p1 - yf);   // dL/dz1 = -dL/dz0
         gam[p * NC16 + q] = gmm;
         gsum += gmm;
-#pragma unroll
-        for (int k = 0; k < HS; ++k) du2[k] = fmaf(kk[k], gmm, du2[k]);
       }
     }
   }
   {
-    float vals[HS + 2];
-    vals[0] = ce_acc;
-    vals[1] = gsum;
-#pragma unroll
-    for (int k = 0; k < HS; ++k) vals[2 + k] = du2[k];
-#pragma unroll
-    for (int v = 0; v < HS + 2; ++v) {
-      const float s = wave_sum(vals[v]);
-      if (lane == 0) red[wv * 32 + v] = s;
-    }
+    const float s0 = wave_sum(ce_acc), s1 = wave_sum(gsum);
+    if (lane == 0) { red[wv * 32] = s0; red[wv * 32 + 1] = s1; }
   }
   __syncthreads();
   MID_STAMP();
-  if (t < HS + 2) {
+  if (t < 2) {
     float s = 0.f;
     for (int w = 0; w < NT_MID / 64; ++w) s += red[w * 32 + t];
     if (t == 0) pb[NP] = s;
     if constexpr (TRAIN) {
       if (t == 1) { pb[H2_B2] = -s; pb[H2_B2 + 1] = s; }
-      if (t >= 2) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
     }
   }
   if constexpr (!TRAIN) return;   // uniform exit: forward-only launch
 
   // ---- M8: classifier backward: dkappa_pq = c (.) [kappa_pq > 0] gamma_pq,
-  //          row sums Dsig (in place over sigma), column sums Dtau (over tau) ---------
+  //          row sums Dsig (in place over sigma), column sums Dtau (over tau);
+  //          zsum_k = sum relu(kappa_k) gamma -> dU2 ---------------------------------
   float* Dsig = sig;
   float* Dtau = tau;
-  for (int ch = (t >> 8); ch < HS / KK_MID; ch += NT_MID / 256)
-    pair_tile<KK_MID, SMAXC, 2, HS>(Nc, tg, sig, tau, ch * KK_MID, eps, yb, WC, nullptr,
-                                    nullptr, gam, NC16, Dsig, Dtau, ysumv, credg);
+  pair_tile<KK_MID, SMAXC, 2, HS>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr,
+                                  gam, NC16, Dsig, Dtau, ysumv, zsumv, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const int k = e % HS;
     Dsig[e] *= cvec[k];
     Dtau[e] *= cvec[k];
   }
+  if (t < HS) { pb[H2_W2 + 2 * t] = -zsumv[t]; pb[H2_W2 + 2 * t + 1] = zsumv[t]; }
   __syncthreads();
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
   for (int e = t; e < HS * HS + HS; e += NT_MID) {
     const int l = e / HS, k = e - l * HS;
-    float acc = 0.f;
     if (l < HS) {
-      for (int p = 0; p < Nc; ++p)
-        acc = fmaf(G[p * HS + l], Dsig[p * HS + k], fmaf(Hh[p * HS + l], Dtau[p * HS + k], acc));
-      Xm[e] = acc;
+      float a0 = 0.f, a1 = 0.f;
+      int p = 0;
+      for (; p + 1 < Nc; p += 2) {
+        a0 = fmaf(G[p * HS + l], Dsig[p * HS + k], fmaf(Hh[p * HS + l], Dtau[p * HS + k], a0));
+        a1 = fmaf(G[(p + 1) * HS + l], Dsig[(p + 1) * HS + k],
+                  fmaf(Hh[(p + 1) * HS + l], Dtau[(p + 1) * HS + k], a1));
+      }
+      if (p < Nc) a0 = fmaf(G[p * HS + l], Dsig[p * HS + k], fmaf(Hh[p * HS + l], Dtau[p * HS + k], a0));
+      Xm[e] = a0 + a1;
     } else {
       float dd1 = 0.f, dt = 0.f;
       for (int p = 0; p < Nc; ++p) { dd1 += Dsig[p * HS + k]; dt += Dtau[p * HS + k]; }
@@ -786,19 +857,19 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   }
   float* dG = G;       // G, H dead once X is formed
   float* dH = Hh;
-  for (int e = t; e < NC16 * HS; e += NT_MID) {     // dG_p[l] = sum_k M[l][k] Dsig_p[k]
-    const int p = e / HS, l = e - p * HS;
-    float ag = 0.f, ah = 0.f;
-    if (p < Nc) {
+  if (msl < NSL) {     // dG_p[l] = sum_k M[l][k] Dsig_p[k]
+    float w[HS];
 #pragma unroll
-      for (int k = 0; k < HS; ++k) {
-        const float w = Mm[l * HS + k];
-        ag = fmaf(w, Dsig[p * HS + k], ag);
-        ah = fmaf(w, Dtau[p * HS + k], ah);
+    for (int k = 0; k < HS; ++k) w[k] = Mm[mk * HS + k];
+    for (int p = msl; p < NC16; p += NSL) {
+      float ag = 0.f, ah = 0.f;
+      if (p < Nc) {
+        ag = dot20(Dsig + p * HS, w, 0.f);
+        ah = dot20(Dtau + p * HS, w, 0.f);
       }
+      dG[p * HS + mk] = ag;
+      dH[p * HS + mk] = ah;
     }
-    dG[e] = ag;
-    dH[e] = ah;
   }
   __syncthreads();
   MID_STAMP();
@@ -806,9 +877,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   // ---- M10: hunk pair backward: dgamma = [g1 > 0](dG_p + dH_q) -----------------------
   float* Dal = Bf[4];   // Dsig/Dtau dead after dG/dH
   float* Dbe = Bf[5];
-  for (int ch = (t >> 8); ch < HS / KK_MID; ch += NT_MID / 256)
-    pair_tile<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, ch * KK_MID, dlt, yb, WC, dG, dH,
-                                    nullptr, 0, Dal, Dbe, ysumv, credg);
+  pair_tile<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
+                                  Dal, Dbe, ysumv, nullptr, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const float dz = (alpha[e] + beta[e] > 0.f) ? (dG[e] + dH[e]) : 0.f;
     Dal[e] -= dz;
@@ -848,10 +918,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   // ---- M11: cross-graph backward: dx'_I += D_r[0], dx'_J += D_r[1], D_r = dn_s + dn_t --
   //   one sweep over the Ne-grid: row sums of D[0] -> dxr, column sums of D[1] -> dxc
   {
-    float* gv = hreg;                   // [Ne][2] dn of the index line's hunk (0 if none)
-    float* R2 = hreg + 2 * NE4;         // [Ne][2]
-    float* C2 = hreg + 4 * NE4;         // [Ne][2]
-    float* xcred2 = hreg + 6 * NE4;     // [8][256][2]
+    float* gv = U;                      // [Ne][2] dn of the index line's hunk (0 if none)
+    float* R2 = U + 2 * NE4;            // [Ne][2]
+    float* C2 = U + 4 * NE4;            // [Ne][2]
     for (int e = t; e < 2 * Ne; e += NT_MID) {
       const int ip = e >> 1, m = e & 1;
       const int h = (ip < n) ? hid[ip] : -1;
@@ -861,18 +930,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
     if (nrel > 0) {
       const int Ne1 = Ne - 1, n1 = n - 1;
       const float invn1 = 1.f / (float)n1;
-      grid_sweep<2, 16, 2>(Ne, t, [&](int i, int j, float* v) {
-        const int r = i * Ne1 + j - (j > i ? 1 : 0);
-        if (r < nrel) {
-          int Ip, jj;
-          divmod_small(r, n1, invn1, Ip, jj);
-          const int Jp = jj + (jj >= Ip);
-          const float2 gs = reinterpret_cast<const float2*>(gv)[Ip];
-          const float2 gt = reinterpret_cast<const float2*>(gv)[Jp];
-          v[0] = gs.x + gt.x;
-          v[1] = gs.y + gt.y;
-        }
-      }, R2, C2, xcred2);
+      grid_sweep<2, 16, NG_MID>(Ne, t, [&](int i, int j, float* v) {
+        const int r = __mul24(i, Ne1) + j - (j > i ? 1 : 0);
+        const float live = r < nrel ? 1.f : 0.f;
+        const int rc = r < nrel ? (r < 0 ? 0 : r) : nrel - 1;
+        int Ip, jj;
+        divmod_bf(rc, n1, invn1, Ip, jj);
+        const int Jp = jj + (jj >= Ip ? 1 : 0);
+        const float2 gs = reinterpret_cast<const float2*>(gv)[Ip];
+        const float2 gt = reinterpret_cast<const float2*>(gv)[Jp];
+        v[0] = live * (gs.x + gt.x);
+        v[1] = live * (gs.y + gt.y);
+      }, R2, C2, U + 6 * NE4);
       for (int i = t; i < Ne; i += NT_MID) {
         dxr[i] = R2[2 * i];
         dxc[i] = C2[2 * i + 1];
@@ -882,19 +951,23 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
     }
   }
   __syncthreads();
+  MID_STAMP();
 
-  // ---- M12: mlp2_entity_B1 backward (hunk buffers are dead: reuse as dq | dE | P) ----
-  float* dq = hreg;
-  float* dE = hreg + NE4 * HS;
-  float* Ps = hreg + 2 * NE4 * HS;
+  // ---- M12: mlp2_entity_B1 backward (U re-carved: P | E_bar | h | dq | dE) ------------
+  float* dq = U + 3 * NE4 * HS;
+  float* dE = U + 4 * NE4 * HS;
   for (int i = t; i < Ne; i += NT_MID) {
     const float dxp = dxr[i] + dxc[i];
     dxr[i] = (os[i] > 0.f) ? dxp : 0.f;             // d o_i
   }
   {
-    const float4* src = reinterpret_cast<const float4*>(Pb);
-    float4* dst = reinterpret_cast<float4*>(Ps);
-    for (int e = t; e < Ne * HS / 4; e += NT_MID) dst[e] = src[e];
+    const float4* s0 = reinterpret_cast<const float4*>(Pb);
+    const float4* s1 = reinterpret_cast<const float4*>(EbG);
+    const float4* s2 = reinterpret_cast<const float4*>(hEG);
+    float4* d0 = reinterpret_cast<float4*>(Ps);
+    float4* d1 = reinterpret_cast<float4*>(Eb);
+    float4* d2 = reinterpret_cast<float4*>(hE);
+    for (int e = t; e < Ne * HS / 4; e += NT_MID) { d0[e] = s0[e]; d1[e] = s1[e]; d2[e] = s2[e]; }
   }
   __syncthreads();
   MID_STAMP();
@@ -919,48 +992,53 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   MID_STAMP();
   for (int e = t; e < 22 * HS; e += NT_MID) {       // dW1' (21 rows) + db1'
     const int r = e / HS, k = e - r * HS;
-    float acc = 0.f;
-    if (r == 0) {
-      for (int i = 0; i < Ne; ++i) acc = fmaf(xs[i], dq[i * HS + k], acc);
-      pb[E3_W1 + k] = acc;
-    } else if (r <= HS) {
-      for (int i = 0; i < Ne; ++i) acc = fmaf(Ebar[i * HS + r - 1], dq[i * HS + k], acc);
-      pb[E3_W1 + r * HS + k] = acc;
+    float a0 = 0.f, a1 = 0.f;
+    const float* src = (r == 0) ? xs : Eb + (r - 1);
+    const int sst = (r == 0) ? 1 : HS;
+    if (r <= HS) {
+      int i = 0;
+      for (; i + 1 < Ne; i += 2) {
+        a0 = fmaf(src[i * sst], dq[i * HS + k], a0);
+        a1 = fmaf(src[(i + 1) * sst], dq[(i + 1) * HS + k], a1);
+      }
+      if (i < Ne) a0 = fmaf(src[i * sst], dq[i * HS + k], a0);
+      pb[E3_W1 + r * HS + k] = a0 + a1;
     } else {
-      for (int i = 0; i < Ne; ++i) acc += dq[i * HS + k];
-      pb[E3_B1 + k] = acc;
+      for (int i = 0; i < Ne; ++i) a0 += dq[i * HS + k];
+      pb[E3_B1 + k] = a0;
     }
   }
-  for (int e = t; e < Ne * HS; e += NT_MID) {       // dE_i[m] = sum_k W1'[1+m][k] dq_i[k]
-    const int i = e / HS, m = e - i * HS;
-    const float* dqi = dq + i * HS;
-    float acc = 0.f;
+  if (msl < NSL) {      // dE_i[m] = sum_k W1'[1+m][k] dq_i[k]
+    float w[HS];
 #pragma unroll
-    for (int k = 0; k < HS; ++k) acc = fmaf(Ws[E3_W1 + (1 + m) * HS + k], dqi[k], acc);
-    dE[e] = acc;
+    for (int k = 0; k < HS; ++k) w[k] = Ws[E3_W1 + (1 + mk) * HS + k];
+    for (int i = msl; i < Ne; i += NSL) dE[i * HS + mk] = dot20(dq + i * HS, w, 0.f);
   }
   __syncthreads();
   MID_STAMP();
   // ---- M13: agg_entity_B1 / mlp_entity_B1 second layer backward ----------------------
   for (int e = t; e < HS * HS + HS; e += NT_MID) {
     const int m = e / HS, k = e - m * HS;
-    float acc = 0.f;
+    float a0 = 0.f, a1 = 0.f;
     if (m < HS) {
-      for (int i = 0; i < Ne; ++i) acc = fmaf(Ps[i * HS + m], dE[i * HS + k], acc);
-      pb[E1_W5 + e] = acc;
+      int i = 0;
+      for (; i + 1 < Ne; i += 2) {
+        a0 = fmaf(Ps[i * HS + m], dE[i * HS + k], a0);
+        a1 = fmaf(Ps[(i + 1) * HS + m], dE[(i + 1) * HS + k], a1);
+      }
+      if (i < Ne) a0 = fmaf(Ps[i * HS + m], dE[i * HS + k], a0);
+      pb[E1_W5 + e] = a0 + a1;
     } else {
-      for (int i = 0; i < Ne; ++i) acc += dE[i * HS + k];
-      pb[E1_B5 + k] = twoNe1 * acc;
+      for (int i = 0; i < Ne; ++i) a0 += dE[i * HS + k];
+      pb[E1_B5 + k] = twoNe1 * a0;
     }
   }
   float* rb = rhog + (size_t)b * Ne * HS;
-  for (int e = t; e < Ne * HS; e += NT_MID) {       // rho_i[m] = sum_k W5[m][k] dE_i[k]
-    const int i = e / HS, m = e - i * HS;
-    const float* dEi = dE + i * HS;
-    float acc = 0.f;
+  if (msl < NSL) {      // rho_i[m] = sum_k W5[m][k] dE_i[k]
+    float w[HS];
 #pragma unroll
-    for (int k = 0; k < HS; ++k) acc = fmaf(Ws[E1_W5 + m * HS + k], dEi[k], acc);
-    rb[e] = acc;
+    for (int k = 0; k < HS; ++k) w[k] = Ws[E1_W5 + mk * HS + k];
+    for (int i = msl; i < Ne; i += NSL) rb[i * HS + mk] = dot20(dE + i * HS, w, 0.f);
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 4) pb[NP + 1 + t] = 0.f;                  // trailer / pad
@@ -1079,7 +1157,7 @@ int smax_e(int ne) { return ne <= 128 ? 8 : 16; }
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
 
 struct Work {   // workspace carve (floats)
-  size_t P, rho, gam, part, total;
+  size_t P, rho, Esave, gam, part, total;
 };
 
 Work work_layout(const hdg_shape* s) {
@@ -1090,6 +1168,7 @@ Work work_layout(const hdg_shape* s) {
   auto take = [&](size_t n) { size_t r = o; o += (n + 63) & ~(size_t)63; return r; };
   w.P = take(B * Ne * HS);
   w.rho = take(B * Ne * HS);
+  w.Esave = take(2 * B * Ne * HS);
   w.gam = take(B * NC16 * NC16);
   w.part = take(B * (size_t)NPART);
   w.total = o;
@@ -1136,8 +1215,9 @@ hipError_t launch_mid(const hdg_shape* s, const hdg_batch* bt, const float* para
     attr_set = true;
   }
   hipLaunchKernelGGL((k_commit_mid<SMAXC, TRAIN>), dim3(s->batch), dim3(NT_MID), lds, st, bt->x,
-                     bt->abits, bt->ybits, bt->hid, bt->nlen, params, ws + w.P, ws + w.rho,
-                     ws + w.gam, ws + w.part, probs, logits, s->ne, s->nc, ce_scale, nullptr);
+                     bt->abits, bt->ybits, bt->hid, bt->nlen, params, ws + w.P, ws + w.Esave,
+                     ws + w.rho, ws + w.gam, ws + w.part, probs, logits, s->ne, s->nc, ce_scale,
+                     nullptr);
   return hipGetLastError();
 }
 
@@ -1226,8 +1306,8 @@ int hdg_debug_mid_stamps(const hdg_shape* s, const hdg_batch* bt, const float* p
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipLaunchKernelGGL((k_commit_mid<5, true, true>), dim3(s->batch), dim3(NT_MID),
                      (size_t)L.total * 4, st, bt->x, bt->abits, bt->ybits, bt->hid, bt->nlen,
-                     params, ws + w.P, ws + w.rho, ws + w.gam, ws + w.part, nullptr, nullptr,
-                     s->ne, s->nc, 1.f, stamps);
+                     params, ws + w.P, ws + w.Esave, ws + w.rho, ws + w.gam, ws + w.part, nullptr,
+                     nullptr, s->ne, s->nc, 1.f, stamps);
   HIP_TRY(hipGetLastError());
   return 0;
 }

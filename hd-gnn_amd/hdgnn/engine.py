@@ -98,6 +98,26 @@ class Engine:
         self.allreduce()
         self.adam()
 
+    # ---- HIP graph of one training step ----------------------------------------
+    def capture(self, dbatch, outputs=True):
+        """Capture train_step(dbatch) (fwd_bwd [+ RCCL all-reduce] + Adam) into a HIP graph;
+        replay() then runs one step with a single launch.  dbatch must stay alive."""
+        saved = [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
+        self.train_step(dbatch, outputs)          # warm: attributes set, RCCL comm built
+        for t, v in zip((self.params, self.m, self.v, self.beta_pow), saved):
+            t.copy_(v)                            # the warm-up step leaves no trace
+        torch.cuda.synchronize(self.device)
+        self._graph_batch = dbatch
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.train_step(dbatch, outputs)
+        torch.cuda.synchronize(self.device)
+        self._graph = g
+        return g
+
+    def replay(self):
+        self._graph.replay()
+
     def forward(self, dbatch):
         """sess.run([loss_Hedge_mse, loss_map, C_edge_output2]) equivalent (test path)."""
         assert dbatch.B == self.batch
