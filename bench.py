@@ -28,33 +28,25 @@ HBM_PEAK_GBS = 8000.0
 
 
 def flops_per_commit(ne, nc):
-    """Algorithmic FLOPs per commit of each kernel (DESIGN.md section 5 derives them).
-    One add / max / compare / select = 1 FLOP, one FMA = 2.  Diagonal and padding
-    work the kernels do is NOT counted."""
-    H = 20
+    """Algorithmic training FLOPs per commit, SURVEY 8(d) / BASELINE.md:
+    3 * F_fwd(model_2), F_fwd = 1008 Pe + 880 Ne + 2200 Pc (the dense TF graph's pair
+    MLPs, sums, node MLPs and classifier; padding / recompute not counted).  The engine
+    executes far fewer operations (sorted-x entity sums), so this is
+    work-equivalent throughput; k_commit_step carries all of it (fwd + bwd)."""
     pe, pc = ne * (ne - 1), nc * (nc - 1)
-    ent_fwd = pe * H * 5                      # z=u+v+a*d (2), relu, row acc, col acc
-    ent_bwd = pe * H * 9                      # z (2), cmp, rho_i+rho_j, select, 2 acc, y*dz fma (2)
-    mid_pairs = pc * H * 5 + pc * (H * 3 + 2 * H * 2 + 12 + H * 2) + pc * H * 7 + pc * H * 9
-    #           H1 sums   | classifier fwd+CE+dU2 per pair         | H2 bwd sums | H3 sums
-    mid_nodes = 2 * (ne * H * H * 2 + ne * 21 * H + ne * H          # E_bar, E3 fwd
-                     + nc * 8 * H + 2 * nc * H * H * 2              # alpha/beta, S,T, sigma/tau
-                     + 5 * nc * H * H * 2                           # dU1e,dS/dT,dV2,dG/dH,S/T again
-                     + ne * 21 * H * 2 + ne * H * H * 3)            # E3 bwd, dW5, rho
-    mid_x1 = 2 * 4 * pe                                             # cross-graph fwd + bwd gathers
-    return {"k_entity_fwd": ent_fwd, "k_commit_mid": mid_pairs + mid_nodes + mid_x1,
-            "k_entity_bwd": ent_bwd}
+    return 3 * (1008 * pe + 880 * ne + 2200 * pc)
 
 
 def hbm_bytes_per_commit(ne, nc):
-    """Algorithmic HBM bytes per commit of each kernel (inputs read once, outputs written once)."""
+    """Bytes one step moves per commit in the engine's compact form: inputs (x, a bits,
+    y bits, prepared tables incl. the two u16 count matrices read twice), the parked
+    P/E_bar/h (written + read back), row boundaries, per-commit gradient row."""
     H = 20
-    pc = nc * (nc - 1)
     we, wc = (ne + 31) // 32, (nc + 31) // 32
-    inp = 4 * ne + 4 * ne * we
-    return {"k_entity_fwd": inp + 4 * ne * H,
-            "k_commit_mid": 4 * ne * H * 2 + 4 * ne + 4 * ne * we + 4 * nc * wc + 2 * 4 * 2 * pc,
-            "k_entity_bwd": inp + 4 * ne * H}
+    inp = 4 * ne + 2 * 4 * ne * we + 4 * nc * wc + 16 * ne
+    kmat = 2 * 2 * (2 * nc * ne)
+    park = 2 * 3 * 4 * ne * H + 2 * 2 * ne * H
+    return inp + kmat + park + 4 * 2132
 
 
 def cpu_baseline(cb, steps, threads):
@@ -158,8 +150,8 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
 
     # per-kernel durations (HIP events on the launch stream), separate instrumented pass
-    ev = _lib.HipEvents(5)
-    names = ["k_entity_fwd", "k_commit_mid", "k_entity_bwd", "k_grad_reduce"]
+    ev = _lib.HipEvents(3)
+    names = ["k_commit_step", "k_grad_reduce"]
     acc = dict.fromkeys(names, 0.0)
     nev = max(10, min(args.steps, 50))
     import ctypes
@@ -182,9 +174,9 @@ def main():
         if world > 1:
             torch.distributed.destroy_process_group()
         return
-    fl = flops_per_commit(ne, nc)
-    dom = max(fl, key=lambda n: kern_ms[n])
-    achieved = fl[dom] * B / (kern_ms[dom] * 1e-3) / 1e12
+    dom = "k_commit_step"
+    flops_launch = flops_per_commit(ne, nc) * B
+    achieved = flops_launch / (kern_ms[dom] * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
@@ -194,8 +186,10 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic, "kernel": dom,
-                "flops_per_launch": fl[dom] * B, "avg_launch_ms": round(kern_ms[dom], 5),
-                "note": "fp32 VALU-bound (fp32 MFMA peak = fp32 vector peak = 157.3 TF)"}
+                "flops_per_launch": flops_launch, "avg_launch_ms": round(kern_ms[dom], 5),
+                "algorithmic_bytes_per_launch": hbm_bytes_per_commit(ne, nc) * B,
+                "note": "SURVEY 8(d) dense-graph FLOPs (3 F_fwd per commit) over the measured "
+                        "k_commit_step time; the engine executes fewer ops (DESIGN.md 3)"}
     cpu = None
     if world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)

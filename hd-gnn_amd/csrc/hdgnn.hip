@@ -1,23 +1,26 @@
 // hdgnn.hip -- MI355X (gfx950, CDNA4) engine for the HD-GNN/S training step.
 //
 // One training step of model_2.graph2graph (model_2.py:86-130 forward, 336-338
-// loss + Adam) runs as five launches on the caller's stream:
+// loss + Adam) runs as three launches on the caller's stream:
 //
-//   k_entity_fwd  [5 x B]   entity pair grid, relu(u_i + v_j + a_ij d) row+col sums
-//                           (mlp_entity_B1 + agg_entity_B1 with W5 hoisted out of the
-//                           pair sum: model_2.py:161-188)
-//   k_commit_mid  [B]       per-commit: E3 node MLP, entity->hunk cross-graph sum,
-//                           hunk pair MLP sums, edge classifier + softmax-CE (fwd+bwd),
-//                           all node-level backward, rho = dL/dP  (model_2.py:94-130)
-//   k_entity_bwd  [5 x B]   entity pair grid backward -> dW1 / db1 partials
-//   k_grad_reduce [P/256]   deterministic per-commit partial sum (fixed commit order)
+//   k_commit_step [B]       one 1024-thread block per commit: entity pair stage,
+//                           E3 node MLP, entity->hunk cross-graph sum, hunk pair MLP
+//                           sums, edge classifier + softmax-CE (fwd+bwd), the whole
+//                           backward down to dW1 of the entity pair MLP
+//                           (model_2.py:94-130, 161-324)
+//   k_grad_reduce [P/64]    deterministic per-commit partial sum (fixed commit order)
 //   k_adam_tf     [1]       loss_para / loss_map gradients + TF1 ApplyAdam
 //
+// plus, once per uploaded batch, k_prep_sort / k_prep_maps (hdg_prepare): the
+// parameter-independent tables of a commit (x sort order, transposed class bits,
+// cross-graph count matrices).
+//
 // Algebra used (exact up to fp32 re-association; derivation in DESIGN.md section 3):
-//   first-layer pre-activation of a pair MLP on [x_i, x_j, 1-a, a] = u_i + v_j + a*d,
-//   so a pair costs ~5 VALU ops per hidden unit; second layers are linear and commute
-//   with the row/column sums, so they run once per NODE.  The diagonal (i == j) is
-//   summed with the tile and subtracted once per node.
+//   first-layer pre-activation of a pair MLP on [x_i, x_j, 1-a, a] = u_i + v_j + a*d;
+//   second layers are linear and commute with the row/column sums, so they run once
+//   per NODE.  Entity pairs: u, v are affine in the scalar x, so the a = 0 relu sums
+//   are prefix/suffix sums over the x-sorted order (O(Ne log nd) per hidden unit)
+//   plus sparse corrections for a = 1.  Hunk pairs run as dense register tiles.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -31,10 +34,8 @@
 namespace {
 
 constexpr int HS = 20;              // h_size = De_e = De_er (model_2.py:163, 192, 247, 306)
-constexpr int NT_MID = 1024;        // k_commit_mid block
-constexpr int KK_MID = 5;           // hidden units per pair-tile chunk in k_commit_mid
-constexpr int KK_E = 4;             // hidden units per block in the entity kernels
-constexpr int NCHUNK_E = HS / KK_E;
+constexpr int NT_MID = 1024;        // k_commit_step block
+constexpr int KK_MID = 5;           // hidden units per pair-tile chunk in k_commit_step
 
 // model_2 flat parameter offsets (tf.global_variables order)
 namespace m2 {
@@ -104,7 +105,7 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 //   z_ij  = A[i] + B[j] + y_ij * dl          (y_ij = bit j of row i)
 //   MODE 0  e = relu(z)                                       (forward sums)
 //   MODE 1  e = [z > 0] * (wr[i] + wc[j])  , ysum += y*e      (backward, node weights)
-//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e,  zsum += z*e   (pair weights)
+//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e                 (pair weights)
 //   Rout[i] = sum_j e_ij   Cout[j] = sum_i e_ij   (diagonal INCLUDED for MODE 0/1:
 //   callers subtract it; MODE 2 masks it)
 // A, B, wr, wc, Rout, Cout: LDS [node][LD] (rows/cols >= N padded with -inf in A/B).
@@ -121,7 +122,7 @@ __device__ __forceinline__ void pair_tile(
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
-    float* __restrict__ ysum, float* __restrict__ zsum, float* __restrict__ cred) {
+    float* __restrict__ ysum, float* __restrict__ cred) {
   constexpr int NP16 = 16 * SMAX;
   constexpr int NW = (SMAX + 1) / 2;
   const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
@@ -132,9 +133,9 @@ __device__ __forceinline__ void pair_tile(
   for (int c = 0; c < SMAX; ++c)
 #pragma unroll
     for (int k = 0; k < KK; ++k) cacc[c][k] = 0.f;
-  float yacc[KK], zacc[KK], dk[KK];
+  float yacc[KK], dk[KK];
 #pragma unroll
-  for (int k = 0; k < KK; ++k) { yacc[k] = 0.f; zacc[k] = 0.f; dk[k] = dl[k0 + k]; }
+  for (int k = 0; k < KK; ++k) { yacc[k] = 0.f; dk[k] = dl[k0 + k]; }
 
   for (int s = 0; s < S; ++s) {
     const int i = ti + 16 * s;
@@ -172,36 +173,38 @@ __device__ __forceinline__ void pair_tile(
           const float w = (MODE == 1) ? (rw[k] + wc[j * LD + k0 + k]) : g;
           e = (z > 0.f) ? w : 0.f;
           yacc[k] = fmaf(af, e, yacc[k]);
-          if constexpr (MODE == 2) zacc[k] = fmaf(reluf(z), e, zacc[k]);   // z may be -inf
         }
         racc[k] += e;
         cacc[c][k] += e;
       }
     }
 #pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      const float r = row16_sum(racc[k]);
-      if (tj == 0 && iv) Rout[i * LD + k0 + k] = r;
+    for (int k = 0; k < KK; ++k) racc[k] = row16_sum(racc[k]);
+    if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
+#pragma unroll
+      for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = racc[k];
     }
   }
   // close the column partials: 4 ti per wave by shuffles, then 4 waves via LDS
   float* credy = cred + 4 * NP16 * KK;
-  float* credz = credy + 4 * KK;
 #pragma unroll
   for (int c = 0; c < SMAX; ++c)
 #pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      const float v = xrow_sum4(cacc[c][k]);
-      if (lane < 16) cred[(wv * NP16 + tj + 16 * c) * KK + k] = v;
-    }
+    for (int k = 0; k < KK; ++k) cacc[c][k] = xrow_sum4(cacc[c][k]);
   if constexpr (MODE != 0) {
 #pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      const float v = wave_sum(yacc[k]);
-      if (lane == 0) credy[wv * KK + k] = v;
-      if constexpr (MODE == 2) {
-        const float vz = wave_sum(zacc[k]);
-        if (lane == 0) credz[wv * KK + k] = vz;
+    for (int k = 0; k < KK; ++k) yacc[k] = wave_sum(yacc[k]);
+  }
+  if (lane < 16) {           // one predicated block of stores
+    float* cw = cred + (wv * NP16 + tj) * KK;
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c)
+#pragma unroll
+      for (int k = 0; k < KK; ++k) cw[16 * c * KK + k] = cacc[c][k];
+    if constexpr (MODE != 0) {
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < KK; ++k) credy[wv * KK + k] = yacc[k];
       }
     }
   }
@@ -213,226 +216,260 @@ __device__ __forceinline__ void pair_tile(
   }
   if constexpr (MODE != 0) {
     if (t < KK) ysum[k0 + t] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
-    if constexpr (MODE == 2) {
-      if (t < KK) zsum[k0 + t] = credz[t] + credz[KK + t] + credz[2 * KK + t] + credz[3 * KK + t];
-    }
   }
   __syncthreads();
 }
 
 // ------------------------------------------------------------------------------
-// Row/column sweep over an N x N relation grid by NG 256-thread groups, columns
-// split across groups (group g owns column blocks c = g, g+NG, ...):
-//   Rout[i][w] = sum_j f(i,j)[w],  Cout[j][w] = sum_i f(i,j)[w]
-// f(i,j,v) must be branch-free and safe on any i,j in [0,N) (it is called on clamped
-// indices and masked: i == j and out-of-range slots contribute 0).
-// scratch: sweep_scratch_words(SMAX, VW, NG) words.
+// scans / searches
 // ------------------------------------------------------------------------------
-__host__ __device__ constexpr int sweep_scratch_words(int smax, int vw, int ng) {
-  return (ng + 4) * 16 * smax * vw;
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T n = __shfl_up(v, o);
+    if (lane >= o) v += n;
+  }
+  return v;
 }
 
-template <int VW, int SMAX, int NG, class F>
-__device__ __forceinline__ void grid_sweep(const int N, const int t, F f, float* __restrict__ Rout,
-                                           float* __restrict__ Cout, float* __restrict__ scratch) {
-  constexpr int NP16 = 16 * SMAX;
-  constexpr int CPG = SMAX / NG;       // column blocks per group
-  static_assert(SMAX % NG == 0, "SMAX must be a multiple of NG");
-  const int g = t >> 8, tg = t & 255;
-  const int tj = tg & 15, ti = tg >> 4, lane = t & 63, wg = tg >> 6;
-  const int S = (N + 15) >> 4;
-  float* Rpart = scratch;                          // [NG][NP16][VW]
-  float* Cpart = scratch + NG * NP16 * VW;         // [NG][4][16*CPG][VW]
-  float cacc[CPG][VW];
+// A bit row of nw <= 8 words in registers with prefix popcounts, for rank-select:
+// the lanes of a node group each pick a DIFFERENT set bit (lane r -> r-th neighbour),
+// so neighbour extraction costs O(1) per neighbour instead of per (neighbour, lane).
+struct BitRow {
+  uint32_t rw[8];
+  int pre[9];          // pre[q] = set bits in words < q; pre[8] = degree
+  __device__ __forceinline__ void init(const uint32_t* row, int nw) {
+    pre[0] = 0;
 #pragma unroll
-  for (int c = 0; c < CPG; ++c)
-#pragma unroll
-    for (int w = 0; w < VW; ++w) cacc[c][w] = 0.f;
-  for (int s = 0; s < S; ++s) {
-    const int i = ti + 16 * s;
-    const int ic = i < N ? i : N - 1;
-    float racc[VW];
-#pragma unroll
-    for (int w = 0; w < VW; ++w) racc[w] = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < CPG; ++cc) {
-      const int j = tj + 16 * (g + NG * cc);
-      const int jc = j < N ? j : N - 1;
-      const float m = (i < N && j < N && i != j) ? 1.f : 0.f;
-      float v[VW];
-      f(ic, jc, v);
-#pragma unroll
-      for (int w = 0; w < VW; ++w) {
-        racc[w] = fmaf(m, v[w], racc[w]);
-        cacc[cc][w] = fmaf(m, v[w], cacc[cc][w]);
-      }
-    }
-#pragma unroll
-    for (int w = 0; w < VW; ++w) {
-      const float r = row16_sum(racc[w]);
-      if (tj == 0) Rpart[(g * NP16 + i) * VW + w] = r;
+    for (int q = 0; q < 8; ++q) {
+      rw[q] = q < nw ? row[q] : 0u;
+      pre[q + 1] = pre[q] + __builtin_popcount(rw[q]);
     }
   }
+  __device__ __forceinline__ int degree() const { return pre[8]; }
+  // column index of the r-th set bit (0 <= r < degree())
+  __device__ __forceinline__ int select(int r) const {
+    int w = 0;
 #pragma unroll
-  for (int cc = 0; cc < CPG; ++cc)
+    for (int q = 1; q < 8; ++q) w += (pre[q] <= r) ? 1 : 0;
+    uint32_t m = 0u;
+    int base = 0;
 #pragma unroll
-    for (int w = 0; w < VW; ++w) {
-      const float v = xrow_sum4(cacc[cc][w]);
-      if (lane < 16) Cpart[((g * 4 + wg) * 16 * CPG + tj + 16 * cc) * VW + w] = v;
+    for (int q = 0; q < 8; ++q) {
+      m = (w == q) ? rw[q] : m;
+      base = (w == q) ? pre[q] : base;
     }
-  __syncthreads();
-  for (int e = t; e < N * VW; e += 256 * NG) {
-    const int i = e / VW, w = e - i * VW;
-    float r = 0.f;
+    int rr = r - base, pos = 0;
 #pragma unroll
-    for (int q = 0; q < NG; ++q) r += Rpart[(q * NP16 + i) * VW + w];
-    Rout[e] = r;
-    const int jb = i >> 4, gq = jb % NG, cc = jb / NG, tq = i & 15;
-    float c = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c += Cpart[((gq * 4 + q) * 16 * CPG + tq + 16 * cc) * VW + w];
-    Cout[e] = c;
+    for (int width = 16; width > 0; width >>= 1) {
+      const int c = __builtin_popcount(m & ((1u << width) - 1u));
+      const bool up = rr >= c;
+      rr = up ? rr - c : rr;
+      m = up ? m >> width : m;
+      pos = up ? pos + width : pos;
+    }
+    return 32 * w + pos;
   }
-  __syncthreads();
-}
-
-// ------------------------------------------------------------------------------
-// Entity stage (shared set-up of the forward and backward entity kernels)
-//   u_i = x_i W1[0] + W1[2] + b1      v_j = x_j W1[1]      d = W1[3] - W1[2]
-// so W1^T [x_i, x_j, [a=0], [a=1]] + b1 = u_i + v_j + a_ij d   (model_2.py:165-170)
-// ------------------------------------------------------------------------------
-template <int SMAX>
-struct EntSmem {
-  static constexpr int NP16 = 16 * SMAX;
-  alignas(16) float u[NP16 * KK_E];
-  alignas(16) float v[NP16 * KK_E];
-  alignas(16) float R[NP16 * KK_E];
-  alignas(16) float C[NP16 * KK_E];
-  alignas(16) float rho[NP16 * KK_E];
-  alignas(16) float cred[tile_cred_words<SMAX, KK_E>()];
-  alignas(16) float xs[NP16];
-  float dl[KK_E];
-  float ysum[KK_E];
-  uint32_t bits[NP16 * ((NP16 + 31) / 32)];
 };
 
-template <int SMAX>
-__device__ __forceinline__ void entity_setup(EntSmem<SMAX>& sm, const float* __restrict__ x,
-                                             const uint32_t* __restrict__ abits,
-                                             const float* __restrict__ Wp, int Ne, int b,
-                                             int k0, int t) {
-  constexpr int NP16 = 16 * SMAX;
-  using namespace m2;
-  const int WE = (Ne + 31) >> 5;
-  const float* xb = x + (size_t)b * Ne;
-  for (int i = t; i < NP16; i += 256) {
-    const float xi = (i < Ne) ? xb[i] : 0.f;
-    sm.xs[i] = xi;
-#pragma unroll
-    for (int k = 0; k < KK_E; ++k) {
-      const int kk = k0 + k;
-      sm.u[i * KK_E + k] = (i < Ne) ? fmaf(xi, Wp[E1_W1 + kk], Wp[E1_W1 + 40 + kk] + Wp[E1_B1 + kk])
-                                    : -INFINITY;
-      sm.v[i * KK_E + k] = (i < Ne) ? xi * Wp[E1_W1 + 20 + kk] : -INFINITY;
-    }
-  }
-  if (t < KK_E) sm.dl[t] = Wp[E1_W1 + 60 + k0 + t] - Wp[E1_W1 + 40 + k0 + t];
-  const uint32_t* ab = abits + (size_t)b * Ne * WE;
-  for (int w = t; w < Ne * WE; w += 256) sm.bits[w] = ab[w];
-}
-
-// P[b][i][k] = sum_{j!=i} relu(z_ij) + sum_{j!=i} relu(z_ji)   (so that
-// E_bar_i = P_i W5 + 2(Ne-1) b5, model_2.py:175 + 186)
-template <int SMAX>
-__global__ __launch_bounds__(256) void k_entity_fwd(const float* __restrict__ x,
-                                                    const uint32_t* __restrict__ abits,
-                                                    const float* __restrict__ Wp,
-                                                    float* __restrict__ Pout, int Ne) {
-  __shared__ EntSmem<SMAX> sm;
-  const int kc = blockIdx.x, b = blockIdx.y, t = threadIdx.x, k0 = kc * KK_E;
-  entity_setup<SMAX>(sm, x, abits, Wp, Ne, b, k0, t);
-  __syncthreads();
-  pair_tile<KK_E, SMAX, 0, KK_E>(Ne, t, sm.u, sm.v, 0, sm.dl, sm.bits, (Ne + 31) >> 5, nullptr,
-                                 nullptr, nullptr, 0, sm.R, sm.C, nullptr, nullptr, sm.cred);
-  float* Pb = Pout + (size_t)b * Ne * HS;
-  for (int e = t; e < Ne * KK_E; e += 256) {
-    const int i = e / KK_E, k = e - i * KK_E;
-    const float diag = reluf(sm.u[i * KK_E + k] + sm.v[i * KK_E + k]);
-    Pb[i * HS + k0 + k] = (sm.R[e] + sm.C[e]) - 2.f * diag;
+// For every neighbour j of the node owned by this lane's group (GL lanes starting at
+// lane gbase) call f(j, x_j).  Lane r of the group rank-selects neighbour c0+r and
+// loads its x once; the group reads (j, x_j) back with ds_bpermute (LDS pipe, not
+// VALU).  All lanes of a group share the trip count, so bpermute sources are active.
+template <int GL, class F>
+__device__ __forceinline__ void for_each_nbr(const BitRow& row, const int gbase, const int r,
+                                             const float* xs, F f) {
+  const int d = row.degree();
+  for (int c0 = 0; c0 < d; c0 += GL) {
+    const int jl = (c0 + r < d) ? row.select(c0 + r) : 0;
+    const float xl = xs[jl];
+    const int nn = (d - c0 < GL) ? d - c0 : GL;
+#pragma unroll 2
+    for (int n = 0; n < nn; ++n) f(__shfl(jl, gbase + n), __shfl(xl, gbase + n));
   }
 }
 
-// dz_ij = [z_ij > 0] (rho_i + rho_j)  (rho = dL/dP from k_commit_mid)
-// dW1[0] = sum x_i dz, dW1[1] = sum x_j dz, dW1[3] = sum a dz, dW1[2] = sum (1-a) dz, db1 = sum dz
-template <int SMAX>
-__global__ __launch_bounds__(256) void k_entity_bwd(const float* __restrict__ x,
-                                                    const uint32_t* __restrict__ abits,
-                                                    const float* __restrict__ Wp,
-                                                    const float* __restrict__ rho,
-                                                    float* __restrict__ part, int Ne) {
-  constexpr int NP16 = 16 * SMAX;
-  __shared__ EntSmem<SMAX> sm;
-  const int kc = blockIdx.x, b = blockIdx.y, t = threadIdx.x, k0 = kc * KK_E;
-  entity_setup<SMAX>(sm, x, abits, Wp, Ne, b, k0, t);
-  const float* rb = rho + (size_t)b * Ne * HS;
-  for (int e = t; e < NP16 * KK_E; e += 256) {
-    const int i = e / KK_E, k = e - i * KK_E;
-    sm.rho[e] = (i < Ne) ? rb[i * HS + k0 + k] : 0.f;
-  }
-  __syncthreads();
-  pair_tile<KK_E, SMAX, 1, KK_E>(Ne, t, sm.u, sm.v, 0, sm.dl, sm.bits, (Ne + 31) >> 5, sm.rho,
-                                 sm.rho, nullptr, 0, sm.R, sm.C, sm.ysum, nullptr, sm.cred);
-  // remove the diagonal term the tile included (a_ii = 0)
-  for (int e = t; e < Ne * KK_E; e += 256) {
-    const float z = sm.u[e] + sm.v[e];
-    const float dz = (z > 0.f) ? (sm.rho[e] + sm.rho[e]) : 0.f;
-    sm.R[e] -= dz;
-    sm.C[e] -= dz;
-  }
-  __syncthreads();
-  // 12 sums over nodes: (k, which) -> one 16-lane row each
-  const int row = t >> 4, tj = t & 15;
-  if (row < 3 * KK_E) {
-    const int k = row % KK_E, which = row / KK_E;
-    float acc = 0.f;
-    for (int i = tj; i < Ne; i += 16) {
-      const float du = sm.R[i * KK_E + k], dv = sm.C[i * KK_E + k], xi = sm.xs[i];
-      acc += (which == 0) ? xi * du : (which == 1) ? xi * dv : du;
-    }
-    acc = row16_sum(acc);
-    if (tj == 0) {
-      using namespace m2;
-      float* pb = part + (size_t)b * NPART;
-      const int kk = k0 + k;
-      if (which == 0) pb[E1_W1 + kk] = acc;
-      if (which == 1) pb[E1_W1 + 20 + kk] = acc;
-      if (which == 2) {
-        const float ya = sm.ysum[k];
-        pb[E1_W1 + 60 + kk] = ya;
-        pb[E1_W1 + 40 + kk] = acc - ya;
-        pb[E1_B1 + kk] = acc;
-      }
-    }
-  }
+typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
+
+__device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+
+__device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n (n >= 1)
+  return 1 << (31 - __builtin_clz((unsigned)n));
 }
 
 // ------------------------------------------------------------------------------
-// k_commit_mid: everything between the two entity pair sweeps, one 1024-thread
-// block per commit.  Node arrays live in LDS; one union region U is re-carved per
-// phase (entity staging -> X1 sweep -> hunk buffers -> X1 backward -> E3 backward).
-// E_bar and the E3 hidden layer are parked in the workspace across the hunk phases.
-// Node matvecs use a (k, slice) thread map with the weight column held in registers.
+// Prepared batch (hdg_prepare: once per uploaded batch, independent of the parameters).
+// Per commit, in 4-byte words:
+//   xsrt[NE4]    x sorted ascending            perm[NE4]  node at sorted slot m
+//   xu[NE4]      the nd distinct x values      cum[NE4+4] cum[q] = #nodes with x < xu[q]
+//   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
+//   atb[Ne*WE]   transposed entity class bits (bit i of row j = a_ij)
+//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
+//   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
+// ------------------------------------------------------------------------------
+struct PrepLayout {
+  int xsrt, perm, xu, cum, pxd, meta, atb, ks, kt, ncst, words;
+};
+
+__host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
+  PrepLayout L;
+  const int NE4 = (Ne + 3) & ~3, WE = (Ne + 31) >> 5;
+  const int kw = ((Nc * Ne + 1) / 2 + 3) & ~3;
+  int o = 0;
+  L.xsrt = o; o += NE4;
+  L.perm = o; o += NE4;
+  L.xu = o;   o += NE4;
+  L.cum = o;  o += NE4 + 4;
+  L.pxd = o;  o += 2 * (NE4 + 4);     // even word offset: 8-byte aligned
+  L.meta = o; o += 4;
+  L.atb = o;  o += (Ne * WE + 3) & ~3;
+  L.ks = o;   o += kw;
+  L.kt = o;   o += kw;
+  L.ncst = o; o += (2 * Nc + 3) & ~3;
+  L.words = (o + 63) & ~63;
+  return L;
+}
+
+// sort x (stable rank count), distinct values + f64 prefix sums, transposed class bits
+__global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
+                                                   const uint32_t* __restrict__ abits,
+                                                   uint32_t* __restrict__ prep, int Ne, int Nc) {
+  const PrepLayout L = prep_layout(Ne, Nc);
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int WE = (Ne + 31) >> 5;
+  __shared__ float xl[256], xsl[256];
+  __shared__ uint32_t al[256 * 8];
+  uint32_t* pb = prep + (size_t)b * L.words;
+  float* xsrt = (float*)(pb + L.xsrt);
+  int* perm = (int*)(pb + L.perm);
+  float* xu = (float*)(pb + L.xu);
+  int* cum = (int*)(pb + L.cum);
+  double* pxd = (double*)(pb + L.pxd);
+  if (t < Ne) xl[t] = x[(size_t)b * Ne + t];
+  for (int w = t; w < Ne * WE; w += 256) al[w] = abits[(size_t)b * Ne * WE + w];
+  __syncthreads();
+  if (t < Ne) {
+    const float xi = xl[t];
+    int r = 0;
+    for (int j = 0; j < Ne; ++j) {
+      const float xj = xl[j];
+      r += (xj < xi || (xj == xi && j < t)) ? 1 : 0;
+    }
+    xsl[r] = xi;
+    xsrt[r] = xi;
+    perm[r] = t;
+  }
+  for (int e = t; e < Ne * WE; e += 256) {
+    const int j = e / WE, w = e - j * WE;
+    uint32_t bits = 0;
+    for (int l = 0; l < 32; ++l) {
+      const int i = 32 * w + l;
+      if (i < Ne) bits |= ((al[i * WE + (j >> 5)] >> (j & 31)) & 1u) << l;
+    }
+    pb[L.atb + e] = bits;
+  }
+  __syncthreads();
+  if (t == 0) {   // serial over <= 256 sorted values, once per batch
+    int nd = 0;
+    double s = 0.0;
+    for (int m = 0; m < Ne; ++m) {
+      const float v = xsl[m];
+      if (m == 0 || v != xsl[m - 1]) {
+        xu[nd] = v;
+        cum[nd] = m;
+        pxd[nd] = s;
+        ++nd;
+      }
+      s += (double)v;
+    }
+    cum[nd] = Ne;
+    pxd[nd] = s;
+    pb[L.meta] = (uint32_t)nd;
+  }
+}
+
+// Cross-graph aggregation counts.  marshalling_B2 (model_2.py:146-150, dense maps of
+// utils2.py:111-137) is n_c = sum_r ([s_r = c] + [t_r = c]) B2_r with
+// B2_r = [x'_I, x'_J, [a_IJ = 0], [a_IJ = 1]], (I, J) = relation r on the Ne-grid and
+// s_r = hid[i'], t_r = hid[j'] with (i', j') = relation r on the n-grid (r < n(n-1)).
+// Only x' changes between steps, so
+//   n_c[0] = sum_I ks[c][I] x'_I,  n_c[1] = sum_J kt[c][J] x'_J,  n_c[2:4] = ncst[c]
+// ks[c][I] = #{r in Ne-row I : s_r = c} + #{r in Ne-row I : t_r = c}, kt over Ne-columns.
+// Integer LDS atomics (order-independent) over chunks of CH hunks.
+__global__ __launch_bounds__(1024) void k_prep_maps(const uint32_t* __restrict__ abits,
+                                                    const int32_t* __restrict__ hidg,
+                                                    const int32_t* __restrict__ nleng,
+                                                    uint32_t* __restrict__ prep, int Ne, int Nc,
+                                                    int CH) {
+  extern __shared__ uint32_t cnt[];   // [2][CH][Ne], then [Nc][2]
+  const PrepLayout L = prep_layout(Ne, Nc);
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int WE = (Ne + 31) >> 5;
+  uint32_t* pb = prep + (size_t)b * L.words;
+  uint16_t* ks = (uint16_t*)(pb + L.ks);
+  uint16_t* kt = (uint16_t*)(pb + L.kt);
+  float* ncst = (float*)(pb + L.ncst);
+  uint32_t* ncl = cnt + 2 * CH * Ne;
+  const int32_t* hid = hidg + (size_t)b * Ne;
+  const uint32_t* ab = abits + (size_t)b * Ne * WE;
+  int n = nleng[b];
+  n = n < 0 ? 0 : (n > Ne ? Ne : n);
+  const int nrel = n >= 2 ? n * (n - 1) : 0;
+  for (int c0 = 0; c0 < Nc; c0 += CH) {
+    for (int e = t; e < 2 * CH * Ne; e += 1024) cnt[e] = 0;
+    if (c0 == 0)
+      for (int e = t; e < 2 * Nc; e += 1024) ncl[e] = 0;
+    __syncthreads();
+    for (int r = t; r < nrel; r += 1024) {
+      const int ip = r / (n - 1), jjp = r - ip * (n - 1);
+      const int jp = jjp + (jjp >= ip ? 1 : 0);
+      const int I = r / (Ne - 1), jj = r - I * (Ne - 1);
+      const int J = jj + (jj >= I ? 1 : 0);
+      const uint32_t a = (ab[I * WE + (J >> 5)] >> (J & 31)) & 1u;
+      const int hs[2] = {hid[ip], hid[jp]};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int h = hs[q];
+        if (h < 0 || h >= Nc) continue;
+        if (h >= c0 && h < c0 + CH) {
+          atomicAdd(&cnt[(h - c0) * Ne + I], 1u);
+          atomicAdd(&cnt[(CH + h - c0) * Ne + J], 1u);
+        }
+        if (c0 == 0) atomicAdd(&ncl[2 * h + a], 1u);
+      }
+    }
+    __syncthreads();
+    for (int e = t; e < CH * Ne; e += 1024) {
+      if (c0 + e / Ne < Nc) {
+        ks[(size_t)c0 * Ne + e] = (uint16_t)cnt[e];
+        kt[(size_t)c0 * Ne + e] = (uint16_t)cnt[CH * Ne + e];
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < 2 * Nc; e += 1024) ncst[e] = (float)ncl[e];
+}
+
+// ------------------------------------------------------------------------------
+// k_commit_step: the whole per-commit forward + backward, one 1024-thread block per
+// commit.  Node arrays live in LDS; one union region U is re-carved per phase
+// (entity stage -> hunk buffers -> E3 backward -> entity backward).  P, E_bar and the
+// E3 hidden layer are parked in the workspace across the hunk phases.  Node matvecs
+// use a (k, slice) thread map with the weight column held in registers.
 // ------------------------------------------------------------------------------
 constexpr int NG_MID = NT_MID / 256;            // 4 pair-tile groups, one k-chunk each
-constexpr int NBUF_H = 6;                       // hunk node buffers [NC16][HS]
+// hunk node buffers [NC16][HS]: alpha beta G H sigma tau (+ tau+eps when it fits)
+__host__ __device__ constexpr int nbuf_h(int smaxc) { return smaxc <= 8 ? 7 : 6; }
 constexpr int NSL = NT_MID / HS;                // 51 node slices for (k, slice) matvecs
 
-struct MidLayout {   // offsets in 4-byte words into the dynamic LDS arena
-  int W, xs, xps, os, dxr, dxc, hid, ab, yb, nb, dnb, misc, Mm, Xm, red, U, Uwords, total;
+struct StepLayout {   // offsets in 4-byte words into the dynamic LDS arena
+  int W, xs, xps, os, dxp, xsrt, perm, xu, cum, pxd, yb, nb, dnb, misc, u2, Mm, Xm, red, U,
+      Uwords, total;
 };
 
-__host__ __device__ inline MidLayout mid_layout(int Ne, int Nc, int smaxc) {
-  MidLayout L;
+__host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
+  StepLayout L;
   const int NC16 = 16 * smaxc;
   const int NE4 = (Ne + 3) & ~3;
   const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
@@ -442,25 +479,27 @@ __host__ __device__ inline MidLayout mid_layout(int Ne, int Nc, int smaxc) {
   L.xs = o;   o += NE4;
   L.xps = o;  o += NE4;
   L.os = o;   o += NE4;
-  L.dxr = o;  o += NE4;
-  L.dxc = o;  o += NE4;
-  L.hid = o;  o += NE4;
-  L.ab = o;   o += (Ne * WE + 3) & ~3;
+  L.dxp = o;  o += NE4;
+  L.xsrt = o; o += NE4;
+  L.perm = o; o += NE4;
+  L.xu = o;   o += NE4;
+  L.cum = o;  o += NE4 + 4;
+  L.pxd = o;  o += 2 * (NE4 + 4);     // f64 (offset is a multiple of 4 words)
   L.yb = o;   o += (Nc * WC + 3) & ~3;
   L.nb = o;   o += 4 * NC16;
-  L.dnb = o;  o += 4 * NC16;
-  L.misc = o; o += 8 * HS;            // dlt eps cvec ysumv s0 t0 sumD zsumv
+  L.dnb = o;  o += 2 * NC16;
+  L.misc = o; o += 8 * HS;            // dlt eps cvec ysumv s0 t0 sumD (spare)
+  L.u2 = o;   o += 2 * HS;            // U2 (classifier output layer), 16-B aligned copy
   L.Mm = o;   o += HS * HS;           // V2 . U1e
   L.Xm = o;   o += HS * HS;           // sum_p G_p (x) Dsig_p + H_p (x) Dtau_p
   L.red = o;  o += (NT_MID / 64) * 32;
-  int u = 3 * NE4 * HS;                                            // P | E_bar | h
-  const int ux1 = 8 * NE4 + sweep_scratch_words(16, 4, NG_MID);    // X1 forward
-  const int uh = NBUF_H * NC16 * HS + NG_MID * cred;               // hunk phases
-  const int ux2 = 6 * NE4 + sweep_scratch_words(16, 2, NG_MID);    // X1 backward
-  const int ueb = 5 * NE4 * HS;                                    // E3 backward
-  if (ux1 > u) u = ux1;
+  const int bw = (Ne * WE + 3) & ~3;
+  int u = 3 * NE4 * HS + 2 * bw;                                   // entity fwd
+  const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred;        // hunk phases
+  int ueb = 5 * NE4 * HS;                                          // E3 bwd
+  const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2
+  if (ue2 > ueb) ueb = ue2;
   if (uh > u) u = uh;
-  if (ux2 > u) u = ux2;
   if (ueb > u) u = ueb;
   L.U = o; L.Uwords = u; o += u;
   L.total = o;
@@ -481,12 +520,192 @@ __device__ __forceinline__ float dot20(const float* row, const float (&w)[HS], f
   return acc;
 }
 
+// first layer of mlp_entity_B1 for hidden unit kk (model_2.py:165-170):
+//   W1^T [x_i, x_j, [a=0], [a=1]] + b1 = u_i + v_j + a_ij d,
+//   u = fma(x, W1[0], W1[2] + b1), v = x * W1[1], d = W1[3] - W1[2]
+// z_ij = u_i + v_j (a = 0) or u_i + (v_j + d) (a = 1), each op rounded (no contraction),
+// so the forward sets, the sparse corrections and the backward masks agree exactly.
+struct EntUnit {
+  float w0, w1, c0, d;
+};
+__device__ __forceinline__ EntUnit ent_unit(const float* Ws, int kk) {
+  using namespace m2;
+  EntUnit e;
+  e.w0 = Ws[E1_W1 + kk];
+  e.w1 = Ws[E1_W1 + HS + kk];
+  const float w2 = Ws[E1_W1 + 2 * HS + kk];
+  e.c0 = w2 + Ws[E1_B1 + kk];
+  e.d = Ws[E1_W1 + 3 * HS + kk] - w2;
+  return e;
+}
+
+// Entity-stage lane map: a wave takes EG_N = 6 nodes, a node group is EG_L = 10 lanes,
+// lane kp of a group owns hidden units (2kp, 2kp+1) as one packed fp32 pair.
+constexpr int EG_L = HS / 2, EG_N = 6;
+
+// E1 body (phase comment in k_commit_step).  Rounding contract (no fma contraction):
+//   z0_ij = fl(u_i + fl(x_j w1)),  u = fma(x, w0, c0);   z1_ij = fl(z0_ij + d)
+// shared by the dense sets, the sparse corrections and the backward masks.
+// ABL: ablation bits for the microbenchmark (1 = skip search, 2 = skip dense sums,
+// 4 = skip row bits, 8 = skip column bits); 0 in the engine.
+template <int ABL = 0>
+__device__ __forceinline__ void entity_fwd(const int lane, const int wv, const float* Ws,
+                                           const float* xs, const float* xu, const int* cum,
+                                           const double* pxd, const int nd,
+                                           const uint32_t* abL, const uint32_t* atL,
+                                           const int WE, const int Ne, float* Ps,
+                                           float* __restrict__ EG, uint16_t* __restrict__ rq) {
+#pragma clang fp contract(off)
+  const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
+  const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
+  const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
+  const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f}, ca[2] = {ea.w0 >= 0.f, eb.w0 >= 0.f};
+  for (int base = EG_N * wv; base < Ne; base += EG_N * (NT_MID / 64)) {     // wave-uniform
+    const int i = base + sub;
+    const bool live = sub < EG_N && i < Ne;
+    const int ic = live ? i : 0;
+    const float xi = xs[ic];
+    const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
+    const f2 v = xi * w1;
+    int br[2] = {0, 0}, bc[2] = {0, 0};
+    for (int s = (ABL & 1) ? 0 : top_pow2(nd); s > 0; s >>= 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int mr = br[h] + s - 1, mc = bc[h] + s - 1;
+        const float xr = xu[mr < nd ? mr : nd - 1], xc = xu[mc < nd ? mc : nd - 1];
+        const bool fr = (u[h] + xr * w1[h]) > 0.f;
+        const bool fc = (fmaf(xc, w0[h], c0[h]) + v[h]) > 0.f;
+        br[h] = ((mr < nd) && (fr != ra[h])) ? br[h] + s : br[h];
+        bc[h] = ((mc < nd) && (fc != ca[h])) ? bc[h] + s : bc[h];
+      }
+    }
+    double tot[2] = {0.0, 0.0};
+    if constexpr (!(ABL & 2)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rlo = ra[h] ? br[h] : 0, rhi = ra[h] ? nd : br[h];
+        const int clo = ca[h] ? bc[h] : 0, chi = ca[h] ? nd : bc[h];
+        double acc = (double)(cum[rhi] - cum[rlo]) * (double)u[h] +
+                     (double)w1[h] * (pxd[rhi] - pxd[rlo]);
+        acc += (double)(cum[chi] - cum[clo]) * ((double)v[h] + (double)c0[h]) +
+               (double)w0[h] * (pxd[chi] - pxd[clo]);
+        acc -= 2.0 * (double)reluf(u[h] + v[h]);
+        tot[h] = acc;
+      }
+    }
+    f2 sp = {0.f, 0.f};
+    const int wl = live ? WE : 0;
+    {
+      BitRow row;
+      row.init(abL + ic * WE, (ABL & 4) ? 0 : wl);
+      for_each_nbr<EG_L>(row, sub * EG_L, kp, xs, [&](int, float xj) {
+        const f2 z0 = u + xj * w1;
+        sp += relu2(z0 + dd) - relu2(z0);
+      });
+    }
+    {
+      BitRow col;
+      col.init(atL + ic * WE, (ABL & 8) ? 0 : wl);
+      for_each_nbr<EG_L>(col, sub * EG_L, kp, xs, [&](int, float xj) {
+        const f2 z0 = __builtin_elementwise_fma((f2){xj, xj}, w0, c0) + v;
+        sp += relu2(z0 + dd) - relu2(z0);
+      });
+    }
+    if (live && kp < EG_L) {
+      const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
+      *reinterpret_cast<float2*>(Ps + i * HS + k0) = P;
+      *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
+      rq[i * HS + k0] = (uint16_t)br[0];
+      rq[i * HS + k0 + 1] = (uint16_t)br[1];
+    }
+  }
+}
+
+// E2 body: per-wave partial sums S0..S3 (dW1 rows, model_2.py:165-170 backward) for
+// the wave's nodes -> red2[wv][4][HS].  Same lane map and rounding contract as E1.
+__device__ __forceinline__ void entity_bwd(const int lane, const int wv, const float* Ws,
+                                           const float* xs, const int* cum, const double* pxd,
+                                           const int nd, const uint16_t* __restrict__ rq,
+                                           const float* rho, const float* Tr, const float* Tx,
+                                           const int TL, const uint32_t* abE, const int WE,
+                                           const int Ne, float* red2) {
+#pragma clang fp contract(off)
+  const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
+  const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
+  const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
+  const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f};
+  f2 S0 = {0.f, 0.f}, S1 = S0, S2 = S0, S3 = S0;
+  for (int base = EG_N * wv; base < Ne; base += EG_N * (NT_MID / 64)) {     // wave-uniform
+    const int i = base + sub;
+    const bool live = sub < EG_N && i < Ne;
+    const int ic = live ? i : 0;
+    const float xi = xs[ic];
+    const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
+    const f2 vi = xi * w1;
+    const f2 ri = *reinterpret_cast<const f2*>(rho + ic * HS + (k0 < HS ? k0 : 0));
+    f2 s0, s1, s2, s3 = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = (k0 < HS ? k0 : 0) + h;
+      const int q = rq[ic * HS + k];
+      const int lo = ra[h] ? q : 0, hi = ra[h] ? nd : q;
+      const float cnt = (float)(cum[hi] - cum[lo]);
+      const float sx = (float)(pxd[hi] - pxd[lo]);
+      const int bm = cum[q];
+      float rs = fmaf(cnt, ri[h], Tr[k * TL + bm]);            // sum_{j in set} rho_i + rho_j
+      float a0 = xi * rs, a1 = fmaf(ri[h], sx, Tx[k * TL + bm]);
+      if ((u[h] + vi[h]) > 0.f) {                                // remove j == i
+        const float r2 = 2.f * ri[h];
+        rs -= r2;
+        a0 -= xi * r2;
+        a1 -= xi * r2;
+      }
+      s0[h] = a0;
+      s1[h] = a1;
+      s2[h] = rs;
+    }
+    BitRow row;
+    row.init(abE + ic * WE, live ? WE : 0);
+    for_each_nbr<EG_L>(row, sub * EG_L, kp, xs, [&](int j, float xj) {
+      const f2 rj = *reinterpret_cast<const f2*>(rho + j * HS + k0);
+      const f2 z0 = u + xj * w1;
+      const f2 z1 = z0 + dd;
+      const f2 gs = ri + rj;
+      const f2 m1g = {z1.x > 0.f ? gs.x : 0.f, z1.y > 0.f ? gs.y : 0.f};
+      const f2 m0g = {z0.x > 0.f ? gs.x : 0.f, z0.y > 0.f ? gs.y : 0.f};
+      const f2 dm = m1g - m0g;
+      s0 = __builtin_elementwise_fma((f2){xi, xi}, dm, s0);
+      s1 = __builtin_elementwise_fma((f2){xj, xj}, dm, s1);
+      s2 += dm;
+      s3 += m1g;
+    });
+    if (live) { S0 += s0; S1 += s1; S2 += s2; S3 += s3; }
+  }
+  // fold the 6 node groups (lanes kp + 10 s), then lanes 0..9 write the wave's sums
+  f2 sv[4] = {S0, S1, S2, S3};
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float a = sv[w][h];
+      a += __shfl_down(a, 3 * EG_L);
+      a += __shfl_down(a, EG_L) + __shfl_down(a, 2 * EG_L);
+      sv[w][h] = a;
+    }
+  if (lane < EG_L) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      red2[(wv * 4 + w) * HS + k0] = sv[w].x;
+      red2[(wv * 4 + w) * HS + k0 + 1] = sv[w].y;
+    }
+  }
+}
+
 template <int SMAXC, bool TRAIN, bool STAMPS = false>
-__global__ __launch_bounds__(NT_MID) void k_commit_mid(
+__global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float* __restrict__ x, const uint32_t* __restrict__ abits,
-    const uint32_t* __restrict__ ybits, const int32_t* __restrict__ hidg,
-    const int32_t* __restrict__ nleng, const float* __restrict__ Wg,
-    const float* __restrict__ Pg, float* __restrict__ Esave, float* __restrict__ rhog,
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ prep,
+    const float* __restrict__ Wg, float* __restrict__ Esave, uint16_t* __restrict__ rowq,
     float* __restrict__ gamg, float* __restrict__ part, float* __restrict__ probs,
     float* __restrict__ logits, int Ne, int Nc, float ce_scale,
     unsigned long long* __restrict__ stamps) {
@@ -494,10 +713,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const MidLayout L = mid_layout(Ne, Nc, SMAXC);
-  const int b = blockIdx.x, t = threadIdx.x;
-  const int lane = t & 63, wv = t >> 6, g = t >> 8, tg = t & 255;
-  const int mk = t % HS, msl = t / HS;            // (k, slice) map; msl == NSL idles
+  const StepLayout L = step_layout(Ne, Nc, SMAXC);
+  const PrepLayout PL = prep_layout(Ne, Nc);
+  const int b = blockIdx.x;
+  // Thread ids are re-derived from an opaque copy of threadIdx.x at every phase
+  // boundary (PHASE()), so the compiler cannot keep addresses derived from them live
+  // across phases: this kernel runs at the 128-VGPR ceiling of 1024-thread blocks.
+  int t = threadIdx.x;
+  int lane = t & 63, wv = t >> 6, g = t >> 8, tg = t & 255;
+  int mk = t % HS, msl = t / HS;                  // (k, slice) map; msl == NSL idles
   const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
   const int NE4 = (Ne + 3) & ~3;
   const int Pc = Nc * (Nc - 1);
@@ -508,16 +732,25 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
       if (threadIdx.x == 0) stamps[blockIdx.x * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
       ++nstamp;                                                                         \
     }                                                                                   \
+    asm volatile("" : "+v"(t));                                                         \
+    lane = t & 63;                                                                      \
+    wv = __builtin_amdgcn_readfirstlane(t >> 6);                                        \
+    g = __builtin_amdgcn_readfirstlane(t >> 8);                                         \
+    tg = t & 255;                                                                       \
+    mk = t % HS;                                                                        \
+    msl = t / HS;                                                                       \
   } while (0)
   MID_STAMP();
   float* Ws = lds + L.W;
   float* xs = lds + L.xs;
   float* xps = lds + L.xps;
   float* os = lds + L.os;
-  float* dxr = lds + L.dxr;
-  float* dxc = lds + L.dxc;
-  int* hid = (int*)(lds + L.hid);
-  uint32_t* ab = (uint32_t*)(lds + L.ab);
+  float* dxp = lds + L.dxp;
+  float* xsrt = lds + L.xsrt;
+  int* perm = (int*)(lds + L.perm);
+  float* xu = lds + L.xu;
+  int* cum = (int*)(lds + L.cum);
+  double* pxd = (double*)(lds + L.pxd);
   uint32_t* yb = (uint32_t*)(lds + L.yb);
   float* nb = lds + L.nb;
   float* dnb = lds + L.dnb;
@@ -528,39 +761,57 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* s0v = ysumv + HS;          // sigma offset
   float* t0v = s0v + HS;            // tau offset
   float* sumD = t0v + HS;
-  float* zsumv = sumD + HS;
   float* Mm = lds + L.Mm;
   float* Xm = lds + L.Xm;
   float* red = lds + L.red;
   float* U = lds + L.U;
 
-  const float* Pb = Pg + (size_t)b * Ne * HS;
-  float* EbG = Esave + (size_t)b * 2 * Ne * HS;
+  const uint32_t* pp = prep + (size_t)b * PL.words;
+  const int nd = (int)pp[PL.meta];
+  float* EG = Esave + (size_t)b * 3 * Ne * HS;     // P | E_bar | h
+  float* EbG = EG + Ne * HS;
   float* hEG = EbG + Ne * HS;
   float* pb = part + (size_t)b * NPART;
   float* gam = gamg + (size_t)b * NC16 * NC16;
-  int n = nleng[b];
-  n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  const int nrel = n * (n - 1);
+  uint16_t* rq = rowq + (size_t)b * Ne * HS;
   const float Nc1 = (float)(Nc - 1);
   const float twoNe1 = 2.f * (float)(Ne - 1);
 
-  // ---- M0: stage weights, commit inputs and P (k_entity_fwd output) -----------------
+  // ---- M0: stage weights, commit inputs, sorted-x tables and entity class bits --------
   float* Ps = U;
   float* Eb = U + NE4 * HS;
   float* hE = U + 2 * NE4 * HS;
+  uint32_t* abL = (uint32_t*)(U + 3 * NE4 * HS);
+  uint32_t* atL = abL + ((Ne * WE + 3) & ~3);
   for (int i = t; i < NP; i += NT_MID) Ws[i] = Wg[i];
   for (int i = t; i < Ne; i += NT_MID) {
     xs[i] = x[(size_t)b * Ne + i];
-    hid[i] = hidg[(size_t)b * Ne + i];
+    xsrt[i] = reinterpret_cast<const float*>(pp + PL.xsrt)[i];
+    perm[i] = reinterpret_cast<const int*>(pp + PL.perm)[i];
   }
-  for (int w = t; w < Ne * WE; w += NT_MID) ab[w] = abits[(size_t)b * Ne * WE + w];
+  for (int q = t; q <= nd; q += NT_MID) {
+    if (q < nd) xu[q] = reinterpret_cast<const float*>(pp + PL.xu)[q];
+    cum[q] = reinterpret_cast<const int*>(pp + PL.cum)[q];
+    pxd[q] = reinterpret_cast<const double*>(pp + PL.pxd)[q];
+  }
+  for (int w = t; w < Ne * WE; w += NT_MID) {
+    abL[w] = abits[(size_t)b * Ne * WE + w];
+    atL[w] = pp[PL.atb + w];
+  }
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
-  {
-    const float4* src = reinterpret_cast<const float4*>(Pb);
-    float4* dst = reinterpret_cast<float4*>(Ps);
-    for (int e = t; e < Ne * HS / 4; e += NT_MID) dst[e] = src[e];
-  }
+  __syncthreads();
+  MID_STAMP();
+
+  // ---- E1: mlp_entity_B1 pair sums (model_2.py:161-175, agg model_2.py:181-188) -----
+  //   P_i[k] = sum_{j!=i} relu(z_ij) + sum_{j!=i} relu(z_ji)  (E_bar = P W5 + 2(Ne-1) b5)
+  //   a = 0 part over ALL j: {j : u_i + v_j > 0} is a prefix or suffix of the x-sorted
+  //   order (v_j monotone in x_j), found by binary search over the nd distinct x values;
+  //   its sum is cnt*u_i + w1*sum(x_j) from f64 prefix sums.  Likewise the column side
+  //   {j : u_j + v_i > 0}.  a_ij = 1 entries add relu(z + d) - relu(z) (set bits of row
+  //   i of a and of a^T); the diagonal is removed once.  Lane map: a wave takes 3 nodes,
+  //   lane = (node sub, hidden unit k), so the 20 lanes of a node walk its bits together.
+  //   The row-set boundaries are kept for the backward.
+  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, abL, atL, WE, Ne, Ps, EG, rq);
   __syncthreads();
   MID_STAMP();
 
@@ -605,42 +856,24 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   __syncthreads();
   MID_STAMP();
 
-  // ---- M3: marshalling_B2 cross-graph sum (model_2.py:146-150, utils2.py:111-137) -----
-  // n_c = sum_r ([s_r=c]+[t_r=c]) B2_r,  B2_r = [x'_I, x'_J, [a=0], [a=1]] on the Ne-grid,
-  // s_r = hid[i'(r)], t_r = hid[j'(r)] on the n-grid (stride n-1): row sums (segS) and
-  // column sums (segT) of the n x n grid of B2 values, then binned by hid.
-  float* segS = U;
-  float* segT = U + 4 * NE4;
-  if (n >= 2) {
-    const int Ne1 = Ne - 1, n1 = n - 1;
-    const float invNe1 = 1.f / (float)Ne1;
-    grid_sweep<4, 16, NG_MID>(n, t, [&](int ip, int jp, float* v) {
-      const int r = __mul24(ip, n1) + jp - (jp > ip ? 1 : 0);
-      int I, jj;
-      divmod_bf(r < 0 ? 0 : r, Ne1, invNe1, I, jj);
-      const int J = jj + (jj >= I ? 1 : 0);
-      const float a = (float)((ab[__mul24(I, WE) + (J >> 5)] >> (J & 31)) & 1u);
-      v[0] = xps[I];
-      v[1] = xps[J];
-      v[2] = 1.f - a;
-      v[3] = a;
-    }, segS, segT, U + 8 * NE4);
-  }
-  for (int e = t; e < NC16 * 4; e += NT_MID) {
-    const int c = e >> 2, m = e & 3;
-    float acc = 0.f;
-    if (c < Nc && n >= 2) {
-      const int4* h4 = reinterpret_cast<const int4*>(hid);
-      for (int q = 0; q < (n + 3) >> 2; ++q) {
-        const int4 h = h4[q];
-        const int ip = 4 * q;
-        if (h.x == c) acc += segS[4 * ip + m] + segT[4 * ip + m];
-        if (h.y == c && ip + 1 < n) acc += segS[4 * ip + 4 + m] + segT[4 * ip + 4 + m];
-        if (h.z == c && ip + 2 < n) acc += segS[4 * ip + 8 + m] + segT[4 * ip + 8 + m];
-        if (h.w == c && ip + 3 < n) acc += segS[4 * ip + 12 + m] + segT[4 * ip + 12 + m];
-      }
+  // ---- M3: marshalling_B2 (model_2.py:146-150) as two count-matrix matvecs -----------
+  //   n_c = [sum_I ks[c][I] x'_I, sum_J kt[c][J] x'_J, ncst[c][0], ncst[c][1]]  (k_prep_maps)
+  {
+    const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
+    const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
+    const float* ncst = reinterpret_cast<const float*>(pp + PL.ncst);
+    for (int task = wv; task < 2 * Nc; task += NT_MID / 64) {      // wave-uniform
+      const int c = task >> 1, m = task & 1;
+      const uint16_t* kr = (m ? kt : ks) + (size_t)c * Ne;
+      float acc = 0.f;
+      for (int I = lane; I < Ne; I += 64) acc = fmaf((float)kr[I], xps[I], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) nb[4 * c + m] = acc;
     }
-    nb[e] = acc;
+    for (int c = t; c < Nc; c += NT_MID) {
+      nb[4 * c + 2] = ncst[2 * c];
+      nb[4 * c + 3] = ncst[2 * c + 1];
+    }
   }
   // per-block constants: delta, eps, c, M = V2 U1e, sigma/tau offsets
   if (t < HS) {
@@ -654,6 +887,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
     t0v[t] = cu;
     s0v[t] = cu + (Ws[H2_W1 + t] + Ws[H2_B1 + t]);
   }
+  if (t < 2 * HS) lds[L.u2 + t] = Ws[H2_W2 + t];
   for (int e = t; e < HS * HS; e += NT_MID) {
     const int l = e / HS, k = e - l * HS;
     float acc = 0.f;
@@ -666,7 +900,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
 
   // ---- M4: first layer of mlp_hunk_B2 split per node (model_2.py:257-260) ----------
   //   alpha_p = n_p V1[0:4] + V1[8] + c1,   beta_q = n_q V1[4:8],   delta = V1[9]-V1[8]
-  float* Bf[NBUF_H];
+  constexpr int NBUF_H = nbuf_h(SMAXC);
+  constexpr bool TAUE = NBUF_H == 7;
+  float* Bf[7];
 #pragma unroll
   for (int q = 0; q < NBUF_H; ++q) Bf[q] = U + q * NC16 * HS;
   float* credg = U + NBUF_H * NC16 * HS + g * CRED;
@@ -698,7 +934,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* G = Bf[2];
   float* Hh = Bf[3];
   pair_tile<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
-                                  nullptr, 0, G, Hh, nullptr, nullptr, credg);
+                                  nullptr, 0, G, Hh, nullptr, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const float dg = reluf(alpha[e] + beta[e]);
     G[e] -= dg;
@@ -711,11 +947,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   //   sigma_p = G_p M + (Nc-1) c2 U1e + U1[0] + d1,  tau_q = H_q M + (Nc-1) c2 U1e
   float* sig = Bf[4];
   float* tau = Bf[5];
+  float* tauE = TAUE ? Bf[6] : nullptr;     // tau + eps: the y = 1 column operand of pass A
   if (msl < NSL) {
     float w[HS];
 #pragma unroll
     for (int l = 0; l < HS; ++l) w[l] = Mm[l * HS + mk];
-    const float s0 = s0v[mk], t0 = t0v[mk];
+    const float s0 = s0v[mk], t0 = t0v[mk], ek = eps[mk];
     for (int p = msl; p < NC16; p += NSL) {
       float as = -INFINITY, at = -INFINITY;
       if (p < Nc) {
@@ -724,6 +961,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
       }
       sig[p * HS + mk] = as;
       tau[p * HS + mk] = at;
+      if constexpr (TAUE) tauE[p * HS + mk] = at + ek;
     }
   }
   __syncthreads();
@@ -733,34 +971,50 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
   float ce_acc = 0.f, gsum = 0.f;
+  float zacc[HS];          // sum relu(kappa_k) gamma  (dU2, model_2.py:318-321)
+#pragma unroll
+  for (int k = 0; k < HS; ++k) zacc[k] = 0.f;
   {
     const int Nc1i = Nc - 1;
     const float invNc1 = 1.f / (float)Nc1i;
-    float w0[HS], w1[HS];
-#pragma unroll
-    for (int k = 0; k < HS; ++k) {
-      w0[k] = Ws[H2_W2 + 2 * k];
-      w1[k] = Ws[H2_W2 + 2 * k + 1];
-    }
+    // U2 rows (w0_k, w1_k) read as broadcast LDS float4 pairs: keeps 40 VGPRs free
+    const float4* u2 = reinterpret_cast<const float4*>(lds + L.u2);
     const float b0 = Ws[H2_B2], b1 = Ws[H2_B2 + 1];
-    const float4* ep4 = reinterpret_cast<const float4*>(eps);
     for (int e = t; e < Pc; e += NT_MID) {
       int p, qq;
       divmod_bf(e, Nc1i, invNc1, p, qq);
       const int q = qq + (qq >= p ? 1 : 0);
       const float yf = (float)((yb[__mul24(p, WC) + (q >> 5)] >> (q & 31)) & 1u);
       const float4* sp = reinterpret_cast<const float4*>(sig + p * HS);
-      const float4* tq = reinterpret_cast<const float4*>(tau + q * HS);
+      const float4* tq =
+          reinterpret_cast<const float4*>((TAUE && yf > 0.f ? tauE : tau) + q * HS);
+      const float4* ep4 = reinterpret_cast<const float4*>(eps);
+      const float ey = TAUE ? 0.f : yf;       // without tau+eps: add y*eps here
       float z0 = b0, z1 = b1;
+      float kap[HS];
 #pragma unroll
       for (int v = 0; v < HS / 4; ++v) {
-        const float4 a = sp[v], c = tq[v], ee = ep4[v];
-        const float k0 = reluf(a.x + fmaf(yf, ee.x, c.x));
-        const float k1 = reluf(a.y + fmaf(yf, ee.y, c.y));
-        const float k2 = reluf(a.z + fmaf(yf, ee.z, c.z));
-        const float k3 = reluf(a.w + fmaf(yf, ee.w, c.w));
-        z0 = fmaf(k3, w0[4 * v + 3], fmaf(k2, w0[4 * v + 2], fmaf(k1, w0[4 * v + 1], fmaf(k0, w0[4 * v], z0))));
-        z1 = fmaf(k3, w1[4 * v + 3], fmaf(k2, w1[4 * v + 2], fmaf(k1, w1[4 * v + 1], fmaf(k0, w1[4 * v], z1))));
+        const float4 a = sp[v];
+        float4 c = tq[v];
+        if constexpr (!TAUE) {
+          const float4 ee = ep4[v];
+          c.x = fmaf(ey, ee.x, c.x);
+          c.y = fmaf(ey, ee.y, c.y);
+          c.z = fmaf(ey, ee.z, c.z);
+          c.w = fmaf(ey, ee.w, c.w);
+        }
+        kap[4 * v] = reluf(a.x + c.x);
+        kap[4 * v + 1] = reluf(a.y + c.y);
+        kap[4 * v + 2] = reluf(a.z + c.z);
+        kap[4 * v + 3] = reluf(a.w + c.w);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 w = u2[2 * v + h];           // w0_k, w1_k, w0_k+1, w1_k+1
+          z0 = fmaf(kap[4 * v + 2 * h], w.x, z0);
+          z1 = fmaf(kap[4 * v + 2 * h], w.y, z1);
+          z0 = fmaf(kap[4 * v + 2 * h + 1], w.z, z0);
+          z1 = fmaf(kap[4 * v + 2 * h + 1], w.w, z1);
+        }
       }
       const float mx = fmaxf(z0, z1);
       const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
@@ -775,38 +1029,49 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
         const float gmm = ce_scale * (p1 - yf);   // dL/dz1 = -dL/dz0
         gam[p * NC16 + q] = gmm;
         gsum += gmm;
+#pragma unroll
+        for (int k = 0; k < HS; ++k) zacc[k] = fmaf(kap[k], gmm, zacc[k]);
       }
     }
   }
   {
-    const float s0 = wave_sum(ce_acc), s1 = wave_sum(gsum);
-    if (lane == 0) { red[wv * 32] = s0; red[wv * 32 + 1] = s1; }
+    const float s0 = wave_sum(ce_acc);
+    if (lane == 0) red[wv * 32] = s0;
+    if constexpr (TRAIN) {
+      const float s1 = wave_sum(gsum);
+      if (lane == 0) red[wv * 32 + 1] = s1;
+#pragma unroll
+      for (int k = 0; k < HS; ++k) zacc[k] = wave_sum(zacc[k]);
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < HS; ++k) red[wv * 32 + 2 + k] = zacc[k];
+      }
+    }
   }
   __syncthreads();
   MID_STAMP();
-  if (t < 2) {
+  if (t < 2 + HS) {
     float s = 0.f;
     for (int w = 0; w < NT_MID / 64; ++w) s += red[w * 32 + t];
     if (t == 0) pb[NP] = s;
     if constexpr (TRAIN) {
       if (t == 1) { pb[H2_B2] = -s; pb[H2_B2 + 1] = s; }
+      if (t >= 2) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
     }
   }
   if constexpr (!TRAIN) return;   // uniform exit: forward-only launch
 
   // ---- M8: classifier backward: dkappa_pq = c (.) [kappa_pq > 0] gamma_pq,
-  //          row sums Dsig (in place over sigma), column sums Dtau (over tau);
-  //          zsum_k = sum relu(kappa_k) gamma -> dU2 ---------------------------------
+  //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
   pair_tile<KK_MID, SMAXC, 2, HS>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr,
-                                  gam, NC16, Dsig, Dtau, ysumv, zsumv, credg);
+                                  gam, NC16, Dsig, Dtau, ysumv, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const int k = e % HS;
     Dsig[e] *= cvec[k];
     Dtau[e] *= cvec[k];
   }
-  if (t < HS) { pb[H2_W2 + 2 * t] = -zsumv[t]; pb[H2_W2 + 2 * t + 1] = zsumv[t]; }
   __syncthreads();
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
@@ -878,7 +1143,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* Dal = Bf[4];   // Dsig/Dtau dead after dG/dH
   float* Dbe = Bf[5];
   pair_tile<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
-                                  Dal, Dbe, ysumv, nullptr, credg);
+                                  Dal, Dbe, ysumv, credg);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const float dz = (alpha[e] + beta[e] > 0.f) ? (dG[e] + dH[e]) : 0.f;
     Dal[e] -= dz;
@@ -915,39 +1180,21 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   __syncthreads();
   MID_STAMP();
 
-  // ---- M11: cross-graph backward: dx'_I += D_r[0], dx'_J += D_r[1], D_r = dn_s + dn_t --
-  //   one sweep over the Ne-grid: row sums of D[0] -> dxr, column sums of D[1] -> dxc
+  // ---- M11: cross-graph backward: dx'_I = sum_c dn_c[0] ks[c][I] + dn_c[1] kt[c][I] ----
+  //   4 hunk ranges (one per group) -> partial rows in the dq slot of U
+  float* dxpart = U + 3 * NE4 * HS;
   {
-    float* gv = U;                      // [Ne][2] dn of the index line's hunk (0 if none)
-    float* R2 = U + 2 * NE4;            // [Ne][2]
-    float* C2 = U + 4 * NE4;            // [Ne][2]
-    for (int e = t; e < 2 * Ne; e += NT_MID) {
-      const int ip = e >> 1, m = e & 1;
-      const int h = (ip < n) ? hid[ip] : -1;
-      gv[e] = (h >= 0) ? dnb[2 * h + m] : 0.f;
-    }
-    __syncthreads();
-    if (nrel > 0) {
-      const int Ne1 = Ne - 1, n1 = n - 1;
-      const float invn1 = 1.f / (float)n1;
-      grid_sweep<2, 16, NG_MID>(Ne, t, [&](int i, int j, float* v) {
-        const int r = __mul24(i, Ne1) + j - (j > i ? 1 : 0);
-        const float live = r < nrel ? 1.f : 0.f;
-        const int rc = r < nrel ? (r < 0 ? 0 : r) : nrel - 1;
-        int Ip, jj;
-        divmod_bf(rc, n1, invn1, Ip, jj);
-        const int Jp = jj + (jj >= Ip ? 1 : 0);
-        const float2 gs = reinterpret_cast<const float2*>(gv)[Ip];
-        const float2 gt = reinterpret_cast<const float2*>(gv)[Jp];
-        v[0] = live * (gs.x + gt.x);
-        v[1] = live * (gs.y + gt.y);
-      }, R2, C2, U + 6 * NE4);
-      for (int i = t; i < Ne; i += NT_MID) {
-        dxr[i] = R2[2 * i];
-        dxc[i] = C2[2 * i + 1];
+    const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
+    const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
+    const int cq = (Nc + NG_MID - 1) / NG_MID;
+    const int cb0 = g * cq, cb1 = (cb0 + cq < Nc) ? cb0 + cq : Nc;
+    for (int I = tg; I < Ne; I += 256) {
+      float a0 = 0.f, a1 = 0.f;
+      for (int c = cb0; c < cb1; ++c) {
+        a0 = fmaf(dnb[2 * c], (float)ks[(size_t)c * Ne + I], a0);
+        a1 = fmaf(dnb[2 * c + 1], (float)kt[(size_t)c * Ne + I], a1);
       }
-    } else {
-      for (int i = t; i < Ne; i += NT_MID) { dxr[i] = 0.f; dxc[i] = 0.f; }
+      dxpart[g * NE4 + I] = a0 + a1;
     }
   }
   __syncthreads();
@@ -957,11 +1204,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   float* dq = U + 3 * NE4 * HS;
   float* dE = U + 4 * NE4 * HS;
   for (int i = t; i < Ne; i += NT_MID) {
-    const float dxp = dxr[i] + dxc[i];
-    dxr[i] = (os[i] > 0.f) ? dxp : 0.f;             // d o_i
+    const float d = (dxpart[i] + dxpart[NE4 + i]) + (dxpart[2 * NE4 + i] + dxpart[3 * NE4 + i]);
+    dxp[i] = (os[i] > 0.f) ? d : 0.f;               // d o_i (x' = relu(o))
   }
   {
-    const float4* s0 = reinterpret_cast<const float4*>(Pb);
+    const float4* s0 = reinterpret_cast<const float4*>(EG);
     const float4* s1 = reinterpret_cast<const float4*>(EbG);
     const float4* s2 = reinterpret_cast<const float4*>(hEG);
     float4* d0 = reinterpret_cast<float4*>(Ps);
@@ -973,17 +1220,17 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   MID_STAMP();
   for (int e = t; e < Ne * HS; e += NT_MID) {
     const int i = e / HS, k = e - i * HS;
-    dq[e] = (hE[e] > 0.f) ? Ws[E3_W2 + k] * dxr[i] : 0.f;
+    dq[e] = (hE[e] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
   }
   if (t >= NT_MID - 64) {                           // one wave: dw2' (20), db2' (1)
     const int k = t - (NT_MID - 64);
     if (k <= HS) {
       float acc = 0.f;
       if (k < HS) {
-        for (int i = 0; i < Ne; ++i) acc = fmaf(hE[i * HS + k], dxr[i], acc);
+        for (int i = 0; i < Ne; ++i) acc = fmaf(hE[i * HS + k], dxp[i], acc);
         pb[E3_W2 + k] = acc;
       } else {
-        for (int i = 0; i < Ne; ++i) acc += dxr[i];
+        for (int i = 0; i < Ne; ++i) acc += dxp[i];
         pb[E3_B2] = acc;
       }
     }
@@ -1016,7 +1263,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
   }
   __syncthreads();
   MID_STAMP();
-  // ---- M13: agg_entity_B1 / mlp_entity_B1 second layer backward ----------------------
+  // ---- M13: agg_entity_B1 / mlp_entity_B1 second layer backward; rho = dL/dP ----------
+  float* rho = Eb;      // E_bar dead after dW1'
   for (int e = t; e < HS * HS + HS; e += NT_MID) {
     const int m = e / HS, k = e - m * HS;
     float a0 = 0.f, a1 = 0.f;
@@ -1033,16 +1281,79 @@ __global__ __launch_bounds__(NT_MID) void k_commit_mid(
       pb[E1_B5 + k] = twoNe1 * a0;
     }
   }
-  float* rb = rhog + (size_t)b * Ne * HS;
   if (msl < NSL) {      // rho_i[m] = sum_k W5[m][k] dE_i[k]
     float w[HS];
 #pragma unroll
     for (int k = 0; k < HS; ++k) w[k] = Ws[E1_W5 + mk * HS + k];
-    for (int i = msl; i < Ne; i += NSL) rb[i * HS + mk] = dot20(dE + i * HS, w, 0.f);
+    for (int i = msl; i < Ne; i += NSL) rho[i * HS + mk] = dot20(dE + i * HS, w, 0.f);
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 4) pb[NP + 1 + t] = 0.f;                  // trailer / pad
   __syncthreads();
+  MID_STAMP();
+
+  // ---- E2: mlp_entity_B1 first-layer backward -----------------------------------------
+  //   dz_ij = [z_ij > 0] (rho_i + rho_j)  (P_i holds row i AND column i of the grid)
+  //   S0 = sum x_i dz, S1 = sum x_j dz, S2 = sum dz, S3 = sum a dz  ->
+  //   dW1[0] = S0, dW1[1] = S1, dW1[2] = S2 - S3, dW1[3] = S3, db1 = S2.
+  //   The a = 0 part reuses the forward's row sets: per k, sums of rho and of x*rho over
+  //   every suffix (w1 >= 0) or prefix (w1 < 0) of the x-sorted order, one wave per scan,
+  //   so each set sum is one table read.  a = 1 corrections over the set bits of row i,
+  //   same (node, k) lane map as E1.
+  const int TL = NE4 + 4;
+  float* Tr = hE;                          // [HS][TL]
+  float* Tx = hE + HS * TL;                // [HS][TL]
+  float* red2 = hE + 2 * HS * TL;          // [16 waves][4][HS]
+  uint32_t* abE = (uint32_t*)Ps;           // P dead after dW5
+  for (int w = t; w < Ne * WE; w += NT_MID) abE[w] = abits[(size_t)b * Ne * WE + w];
+  for (int task = wv; task < 2 * HS; task += NT_MID / 64) {        // wave-uniform
+    const int k = task >> 1, which = task & 1;
+    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
+    float* T = (which ? Tx : Tr) + k * TL;
+    float run[4];
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = 4 * lane + q;                 // scan position
+      float val = 0.f;
+      if (s < Ne) {
+        const int m = suf ? Ne - 1 - s : s;
+        val = rho[perm[m] * HS + k];
+        if (which) val *= xsrt[m];
+      }
+      r += val;
+      run[q] = r;
+    }
+    const float off = wave_incl_scan(r, lane) - r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = 4 * lane + q;
+      if (s < Ne) {
+        if (suf) T[Ne - 1 - s] = off + run[q];   // sum over sorted slots [m, Ne)
+        else T[s + 1] = off + run[q];            // sum over sorted slots [0, m)
+      }
+    }
+    if (lane == 0) T[suf ? Ne : 0] = 0.f;
+  }
+  __syncthreads();
+  MID_STAMP();
+  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, abE, WE, Ne, red2);
+  __syncthreads();
+  if (t < 4 * HS) {
+    const int w = t / HS, k = t - w * HS;
+    float s = 0.f;
+    for (int q = 0; q < NT_MID / 64; ++q) s += red2[(q * 4 + w) * HS + k];
+    red[w * 32 + k] = s;
+  }
+  __syncthreads();
+  if (t < HS) {
+    const float s0 = red[t], s1 = red[32 + t], s2 = red[64 + t], s3 = red[96 + t];
+    pb[E1_W1 + t] = s0;
+    pb[E1_W1 + HS + t] = s1;
+    pb[E1_W1 + 2 * HS + t] = s2 - s3;
+    pb[E1_W1 + 3 * HS + t] = s3;
+    pb[E1_B1 + t] = s2;
+  }
   MID_STAMP();
 #undef MID_STAMP
 }
@@ -1153,11 +1464,10 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-int smax_e(int ne) { return ne <= 128 ? 8 : 16; }
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
 
 struct Work {   // workspace carve (floats)
-  size_t P, rho, Esave, gam, part, total;
+  size_t Esave, rowq, gam, part, total;
 };
 
 Work work_layout(const hdg_shape* s) {
@@ -1166,13 +1476,19 @@ Work work_layout(const hdg_shape* s) {
   const size_t NC16 = 16 * (size_t)smax_c(s->nc);
   size_t o = 0;
   auto take = [&](size_t n) { size_t r = o; o += (n + 63) & ~(size_t)63; return r; };
-  w.P = take(B * Ne * HS);
-  w.rho = take(B * Ne * HS);
-  w.Esave = take(2 * B * Ne * HS);
+  w.Esave = take(3 * B * Ne * HS);
+  w.rowq = take((B * Ne * HS + 1) / 2);     // u16
   w.gam = take(B * NC16 * NC16);
   w.part = take(B * (size_t)NPART);
   w.total = o;
   return w;
+}
+
+constexpr int PREP_LDS_WORDS = 36 * 1024;   // k_prep_maps count chunk (144 KiB)
+
+int prep_chunk(int ne, int nc) {
+  int ch = (PREP_LDS_WORDS - 2 * nc) / (2 * ne);
+  return ch < nc ? ch : nc;
 }
 
 int check_shape(const hdg_shape* s) {
@@ -1182,15 +1498,15 @@ int check_shape(const hdg_shape* s) {
   if (s->batch < 1) return fail(HDG_EINVAL, "batch must be >= 1 (got %d)", s->batch);
   if (s->ne < 2 || s->ne > 256) return fail(HDG_EINVAL, "ne must be in [2,256] (got %d)", s->ne);
   if (s->nc < 2 || s->nc > 160) return fail(HDG_EINVAL, "nc must be in [2,160] (got %d)", s->nc);
-  const MidLayout L = mid_layout(s->ne, s->nc, smax_c(s->nc));
+  const StepLayout L = step_layout(s->ne, s->nc, smax_c(s->nc));
   if ((size_t)L.total * 4 > 160 * 1024)
-    return fail(HDG_EINVAL, "ne=%d nc=%d needs %zu B of LDS in k_commit_mid (> 160 KiB)", s->ne,
+    return fail(HDG_EINVAL, "ne=%d nc=%d needs %zu B of LDS in k_commit_step (> 160 KiB)", s->ne,
                 s->nc, (size_t)L.total * 4);
   return 0;
 }
 
 int check_batch(const hdg_batch* bt) {
-  if (!bt || !bt->x || !bt->abits || !bt->ybits || !bt->hid || !bt->nlen)
+  if (!bt || !bt->x || !bt->abits || !bt->ybits || !bt->hid || !bt->nlen || !bt->prep)
     return fail(HDG_EINVAL, "batch has a NULL device pointer");
   return 0;
 }
@@ -1201,48 +1517,35 @@ int check_batch(const hdg_batch* bt) {
     if (e_ != hipSuccess) return fail((int)e_, "%s: %s", #expr, hipGetErrorString(e_));   \
   } while (0)
 
-template <int SMAXC, bool TRAIN>
-hipError_t launch_mid(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
-                      const Work& w, float* probs, float* logits, float ce_scale,
-                      hipStream_t st) {
-  const MidLayout L = mid_layout(s->ne, s->nc, SMAXC);
+template <int SMAXC, bool TRAIN, bool STAMPS>
+hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
+                       const Work& w, float* probs, float* logits, float ce_scale,
+                       unsigned long long* stamps, hipStream_t st) {
+  const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
   const size_t lds = (size_t)L.total * 4;
   static bool attr_set = false;   // the attribute is per function; 160 KiB covers every shape
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_commit_mid<SMAXC, TRAIN>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_commit_step<SMAXC, TRAIN, STAMPS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_commit_mid<SMAXC, TRAIN>), dim3(s->batch), dim3(NT_MID), lds, st, bt->x,
-                     bt->abits, bt->ybits, bt->hid, bt->nlen, params, ws + w.P, ws + w.Esave,
-                     ws + w.rho, ws + w.gam, ws + w.part, probs, logits, s->ne, s->nc, ce_scale,
-                     nullptr);
+  hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS>), dim3(s->batch), dim3(NT_MID), lds, st,
+                     bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params, ws + w.Esave,
+                     (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, probs, logits, s->ne,
+                     s->nc, ce_scale, stamps);
   return hipGetLastError();
 }
 
-template <bool TRAIN>
-hipError_t dispatch_mid(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
-                        const Work& w, float* probs, float* logits, float ce_scale,
-                        hipStream_t st) {
+template <bool TRAIN, bool STAMPS = false>
+hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
+                         const Work& w, float* probs, float* logits, float ce_scale,
+                         unsigned long long* stamps, hipStream_t st) {
   switch (smax_c(s->nc)) {
-    case 5: return launch_mid<5, TRAIN>(s, bt, params, ws, w, probs, logits, ce_scale, st);
-    case 8: return launch_mid<8, TRAIN>(s, bt, params, ws, w, probs, logits, ce_scale, st);
-    default: return launch_mid<10, TRAIN>(s, bt, params, ws, w, probs, logits, ce_scale, st);
+    case 5: return launch_step<5, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
+    case 8: return launch_step<8, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
+    default: return launch_step<10, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
   }
-}
-
-hipError_t launch_entity(bool fwd, const hdg_shape* s, const hdg_batch* bt, const float* params,
-                         float* ws, const Work& w, hipStream_t st) {
-  dim3 grid(NCHUNK_E, s->batch);
-  if (smax_e(s->ne) == 8) {
-    if (fwd) hipLaunchKernelGGL(k_entity_fwd<8>, grid, dim3(256), 0, st, bt->x, bt->abits, params, ws + w.P, s->ne);
-    else hipLaunchKernelGGL(k_entity_bwd<8>, grid, dim3(256), 0, st, bt->x, bt->abits, params, ws + w.rho, ws + w.part, s->ne);
-  } else {
-    if (fwd) hipLaunchKernelGGL(k_entity_fwd<16>, grid, dim3(256), 0, st, bt->x, bt->abits, params, ws + w.P, s->ne);
-    else hipLaunchKernelGGL(k_entity_bwd<16>, grid, dim3(256), 0, st, bt->x, bt->abits, params, ws + w.rho, ws + w.part, s->ne);
-  }
-  return hipGetLastError();
 }
 
 }  // namespace
@@ -1257,6 +1560,32 @@ int hdg_grad_len(int32_t variant) { return variant == 2 ? GRAD_LEN : -1; }
 size_t hdg_workspace_bytes(const hdg_shape* shape) {
   if (check_shape(shape)) return 0;
   return work_layout(shape).total * sizeof(float);
+}
+
+size_t hdg_prep_bytes(const hdg_shape* shape) {
+  if (check_shape(shape)) return 0;
+  return (size_t)shape->batch * prep_layout(shape->ne, shape->nc).words * 4;
+}
+
+int hdg_prepare(const hdg_shape* s, const hdg_batch* bt, void* stream) {
+  if (int rc = check_shape(s)) return rc;
+  if (int rc = check_batch(bt)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_prep_sort, dim3(s->batch), dim3(256), 0, st, bt->x, bt->abits,
+                     (uint32_t*)bt->prep, s->ne, s->nc);
+  HIP_TRY(hipGetLastError());
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_TRY(hipFuncSetAttribute((const void*)k_prep_maps,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int ch = prep_chunk(s->ne, s->nc);
+  const size_t lds = (size_t)(2 * ch * s->ne + 2 * s->nc) * 4;
+  hipLaunchKernelGGL(k_prep_maps, dim3(s->batch), dim3(1024), lds, st, bt->abits, bt->hid,
+                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* params,
@@ -1274,17 +1603,13 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
     return events ? hipEventRecord((hipEvent_t)events[k], st) : hipSuccess;
   };
   HIP_TRY(mark(0));
-  HIP_TRY(launch_entity(true, s, bt, params, ws, w, st));
+  HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
+                              out ? out->logits : nullptr, ce_scale, nullptr, st));
   HIP_TRY(mark(1));
-  HIP_TRY(dispatch_mid<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                             out ? out->logits : nullptr, ce_scale, st));
-  HIP_TRY(mark(2));
-  HIP_TRY(launch_entity(false, s, bt, params, ws, w, st));
-  HIP_TRY(mark(3));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(256), 0, st,
                      ws + w.part, s->batch, 0, GRAD_LEN, grad);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(mark(4));
+  HIP_TRY(mark(2));
   return 0;
 }
 
@@ -1293,22 +1618,15 @@ int hdg_fwd_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, fl
   return hdg_fwd_bwd_events(s, bt, params, grad, out, workspace, stream, nullptr);
 }
 
-int hdg_debug_mid_stamps(const hdg_shape* s, const hdg_batch* bt, const float* params,
-                         void* workspace, unsigned long long* stamps, void* stream) {
+int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* params,
+                          void* workspace, unsigned long long* stamps, void* stream) {
   if (int rc = check_shape(s)) return rc;
   if (int rc = check_batch(bt)) return rc;
-  if (smax_c(s->nc) != 5) return fail(HDG_EINVAL, "phase stamps are built for nc <= 80");
-  hipStream_t st = (hipStream_t)stream;
+  if (!stamps || !workspace || !params) return fail(HDG_EINVAL, "NULL stamps/workspace/params");
   const Work w = work_layout(s);
-  float* ws = (float*)workspace;
-  const MidLayout L = mid_layout(s->ne, s->nc, 5);
-  HIP_TRY(hipFuncSetAttribute((const void*)k_commit_mid<5, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  hipLaunchKernelGGL((k_commit_mid<5, true, true>), dim3(s->batch), dim3(NT_MID),
-                     (size_t)L.total * 4, st, bt->x, bt->abits, bt->ybits, bt->hid, bt->nlen,
-                     params, ws + w.P, ws + w.Esave, ws + w.rho, ws + w.gam, ws + w.part, nullptr,
-                     nullptr, s->ne, s->nc, 1.f, stamps);
-  HIP_TRY(hipGetLastError());
+  const hipError_t e = dispatch_step<true, true>(s, bt, params, (float*)workspace, w, nullptr,
+                                                 nullptr, 1.f, stamps, (hipStream_t)stream);
+  HIP_TRY(e);
   return 0;
 }
 
@@ -1341,9 +1659,8 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
   hipStream_t st = (hipStream_t)stream;
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
-  HIP_TRY(launch_entity(true, s, bt, params, ws, w, st));
-  HIP_TRY(dispatch_mid<false>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, 0.f, st));
+  HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, out ? out->probs : nullptr,
+                               out ? out->logits : nullptr, 0.f, nullptr, st));
   if (ce_sum) {
     hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(256), 0, st, ws + w.part, s->batch, m2::NP,
                        m2::NP + 1, ce_sum);

@@ -1,0 +1,75 @@
+// mb_entity.hip -- ablations of the sorted-x entity forward (entity_fwd, phase E1).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include mb_entity.hip -o mb_entity
+// One block per "commit" (100 blocks x 1024 threads), Ne = 200, x in 0..9, a ~ 5 %.
+#include "hdgnn.hip"
+
+namespace {
+
+template <int ABL>
+__global__ __launch_bounds__(1024) void mb_e1(int Ne, int iters, float* out, float* EG,
+                                              uint16_t* rq) {
+  __shared__ float Ws[2128];
+  __shared__ float xs[256], xu[256], Ps[256 * HS];
+  __shared__ int cum[260];
+  __shared__ double pxd[260];
+  __shared__ uint32_t ab[256 * 8], at[256 * 8];
+  const int t = threadIdx.x, b = blockIdx.x;
+  const int WE = (Ne + 31) >> 5;
+  for (int i = t; i < 2128; i += 1024) Ws[i] = 0.01f * (float)((i * 2654435761u) % 200) - 1.f;
+  for (int i = t; i < Ne; i += 1024) xs[i] = (float)((i * 7 + b) % 10);
+  if (t < 10) { xu[t] = (float)t; }
+  if (t <= 10) { cum[t] = t * Ne / 10; pxd[t] = 0.0; }
+  for (int w = t; w < Ne * WE; w += 1024) {
+    const uint32_t h = (uint32_t)(w + 977 * b) * 2654435761u;
+    ab[w] = (h & 0x1111u) | ((h >> 16) & 0x0101u);     // ~2 bits per word
+    at[w] = (h & 0x0111u) | ((h >> 20) & 0x0011u);
+  }
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    entity_fwd<ABL>(t & 63, t >> 6, Ws, xs, xu, cum, pxd, 10, ab, at, WE, Ne, Ps,
+                    EG + (size_t)b * Ne * HS, rq + (size_t)b * Ne * HS);
+    __syncthreads();
+  }
+  if (t == 0) out[b] = Ps[7] + Ps[300];
+}
+
+}  // namespace
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+template <int ABL>
+float run(float* out, float* EG, uint16_t* rq, int blocks, int iters) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL(mb_e1<ABL>, dim3(blocks), dim3(1024), 0, 0, 200, 1, out, EG, rq);
+  hipDeviceSynchronize();
+  hipEventRecord(a);
+  hipLaunchKernelGGL(mb_e1<ABL>, dim3(blocks), dim3(1024), 0, 0, 200, iters, out, EG, rq);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  return ms * 1e3f / iters;
+}
+
+int main() {
+  float *out, *EG;
+  uint16_t* rq;
+  CK(hipMalloc(&out, 4096 * sizeof(float)));
+  CK(hipMalloc(&EG, 100 * 256 * HS * sizeof(float)));
+  CK(hipMalloc(&rq, 100 * 256 * HS * sizeof(uint16_t)));
+  const int B = 100, IT = 20;
+  printf("entity_fwd Ne=200 (us per call, %d blocks x 1024 thr)\n", B);
+  printf("  full              %8.2f\n", run<0>(out, EG, rq, B, IT));
+  printf("  no search         %8.2f\n", run<1>(out, EG, rq, B, IT));
+  printf("  no dense          %8.2f\n", run<2>(out, EG, rq, B, IT));
+  printf("  no row bits       %8.2f\n", run<4>(out, EG, rq, B, IT));
+  printf("  no col bits       %8.2f\n", run<8>(out, EG, rq, B, IT));
+  printf("  no bits           %8.2f\n", run<12>(out, EG, rq, B, IT));
+  printf("  search only       %8.2f\n", run<14>(out, EG, rq, B, IT));
+  printf("  nothing           %8.2f\n", run<15>(out, EG, rq, B, IT));
+  printf("  1 block full      %8.2f\n", run<0>(out, EG, rq, 1, IT));
+  CK(hipDeviceSynchronize());
+  return 0;
+}

@@ -21,7 +21,7 @@ class Shape(ctypes.Structure):
 
 class Batch(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("abits", ctypes.c_void_p), ("ybits", ctypes.c_void_p),
-                ("hid", ctypes.c_void_p), ("nlen", ctypes.c_void_p)]
+                ("hid", ctypes.c_void_p), ("nlen", ctypes.c_void_p), ("prep", ctypes.c_void_p)]
 
 
 class State(ctypes.Structure):
@@ -35,8 +35,9 @@ class Outputs(ctypes.Structure):
 
 
 EXPORTS = ["hdg_version", "hdg_last_error", "hdg_param_count", "hdg_grad_len",
-           "hdg_workspace_bytes", "hdg_fwd_bwd", "hdg_fwd_bwd_events", "hdg_adam_tf",
-           "hdg_train_step", "hdg_forward", "hdg_debug_mid_stamps"]
+           "hdg_workspace_bytes", "hdg_prep_bytes", "hdg_prepare", "hdg_fwd_bwd",
+           "hdg_fwd_bwd_events", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
+           "hdg_debug_step_stamps"]
 
 _lib = None
 
@@ -59,9 +60,12 @@ def load(path=None):
     lib.hdg_grad_len.argtypes = [i32]
     lib.hdg_workspace_bytes.argtypes = [P(Shape)]
     lib.hdg_workspace_bytes.restype = ctypes.c_size_t
+    lib.hdg_prep_bytes.argtypes = [P(Shape)]
+    lib.hdg_prep_bytes.restype = ctypes.c_size_t
+    lib.hdg_prepare.argtypes = [P(Shape), P(Batch), vp]
     lib.hdg_fwd_bwd.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp]
     lib.hdg_fwd_bwd_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp, vp]
-    lib.hdg_debug_mid_stamps.argtypes = [P(Shape), P(Batch), vp, vp, vp, vp]
+    lib.hdg_debug_step_stamps.argtypes = [P(Shape), P(Batch), vp, vp, vp, vp]
     lib.hdg_adam_tf.argtypes = [P(Shape), P(State), vp, f32, vp, vp]
     lib.hdg_train_step.argtypes = [P(Shape), P(Batch), P(State), f32, P(Outputs), vp, vp, vp]
     lib.hdg_forward.argtypes = [P(Shape), P(Batch), vp, P(Outputs), vp, vp, vp]

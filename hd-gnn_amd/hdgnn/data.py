@@ -11,6 +11,7 @@ plus Es/Et/Cs/Ct, which are the canonical complete-digraph incidences for every
 commit.  compact_from_read_data() extracts exactly that and VERIFIES the rest, so
 a feed that is not of this form is rejected instead of silently mis-read.
 """
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -90,11 +91,23 @@ class CommitBatch:
 
 
 class DeviceBatch:
-    """The hdg_batch struct's device arrays (include/hdgnn.h)."""
+    """The hdg_batch struct's device arrays (include/hdgnn.h), prepared on upload:
+    hdg_prepare builds the per-commit sort / transposed-bit / count tables in `prep`."""
 
     def __init__(self, x, abits, ybits, hid, nlen, Ne, Nc):
+        import torch
+        from . import _lib
         self.x, self.abits, self.ybits, self.hid, self.nlen = x, abits, ybits, hid, nlen
         self.B, self.Ne, self.Nc = x.shape[0], Ne, Nc
+        lib = _lib.load()
+        shape = _lib.Shape(self.B, Ne, Nc, 2, self.B)
+        nbytes = lib.hdg_prep_bytes(ctypes.byref(shape))
+        if nbytes == 0:
+            raise ValueError(lib.hdg_last_error().decode())
+        self.prep = torch.empty(nbytes // 4, dtype=torch.int32, device=x.device)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(lib.hdg_prepare(ctypes.byref(shape), ctypes.byref(self.struct()),
+                                   ctypes.c_void_p(stream)))
 
     @classmethod
     def from_host(cls, cb, device="cuda"):
@@ -109,8 +122,10 @@ class DeviceBatch:
 
     def struct(self):
         from ._lib import Batch
+        prep = getattr(self, "prep", None)
         return Batch(self.x.data_ptr(), self.abits.data_ptr(), self.ybits.data_ptr(),
-                     self.hid.data_ptr(), self.nlen.data_ptr())
+                     self.hid.data_ptr(), self.nlen.data_ptr(),
+                     prep.data_ptr() if prep is not None else None)
 
 
 # ----------------------------------------------------------------------------

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 1
+#define HDG_ABI_VERSION 2
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -57,6 +57,9 @@ typedef struct hdg_batch {
     const uint32_t* ybits;  /* [B][nc][ceil(nc/32)] hunk class bits (C_edge), diag 0      */
     const int32_t*  hid;    /* [B][ne] Esc/Etc hunk row of index line i' (-1 = none)      */
     const int32_t*  nlen;   /* [B] n = len(readlines()[:Ne]) of the commit's index file   */
+    void*           prep;   /* hdg_prep_bytes(shape) of device scratch, filled once per
+                               uploaded batch by hdg_prepare (sorted x, transposed bits,
+                               cross-graph count matrices); read by every step after    */
 } hdg_batch;
 
 /* Adam / parameter state (all device, fp32). */
@@ -82,20 +85,27 @@ int         hdg_param_count(int32_t variant);
  * (slot P = CE sum over this call's relations); all-reduce the whole buffer.      */
 int         hdg_grad_len(int32_t variant);
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
+/* bytes of batch->prep for this shape (0 on a shape error) */
+size_t      hdg_prep_bytes(const hdg_shape* shape);
+
+/* Build batch->prep from x / abits / hid / nlen (the parameter-independent per-commit
+ * tables the step kernel reads).  Call once after uploading a batch, before any step;
+ * re-call whenever the batch contents change.  Replaces nothing in the reference: it is
+ * the device-side half of the feed_dict marshalling (utils2.py:111-137, 248-253).    */
+int hdg_prepare(const hdg_shape* shape, const hdg_batch* batch, void* stream);
 
 int hdg_fwd_bwd(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                 float* grad, hdg_outputs* out, void* workspace, void* stream);
 
-/* hdg_fwd_bwd with hipEvent_t events[5] recorded on `stream` before k_entity_fwd,
- * k_commit_mid, k_entity_bwd, k_grad_reduce and after the last launch (per-kernel
- * timing for bench.py; events may be NULL).                                       */
+/* hdg_fwd_bwd with hipEvent_t events[3] recorded on `stream` before k_commit_step,
+ * before k_grad_reduce and after it (per-kernel timing for bench.py; may be NULL). */
 int hdg_fwd_bwd_events(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                        float* grad, hdg_outputs* out, void* workspace, void* stream,
                        void* const* events);
 
-/* Diagnostic: run k_commit_mid alone with s_memrealtime (100 MHz) stamps at every phase
- * barrier, stamps[B][32] (device); needs a preceding hdg_fwd_bwd on the same workspace. */
-int hdg_debug_mid_stamps(const hdg_shape* shape, const hdg_batch* batch, const float* params,
+/* Diagnostic: run k_commit_step alone with s_memrealtime (100 MHz) stamps at every
+ * phase barrier, stamps[B][32] (device).  Overwrites the workspace.                 */
+int hdg_debug_step_stamps(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                          void* workspace, unsigned long long* stamps, void* stream);
 
 int hdg_adam_tf(const hdg_shape* shape, hdg_state* state, const float* grad,

@@ -81,6 +81,8 @@ CASES = [
     (4, 37, 19, 1),
     (2, 200, 74, 2),
     (1, 33, 17, 3),
+    (2, 250, 150, 4),     # s5 shapes (BASELINE config 4), largest hunk tile
+    (1, 256, 160, 5),     # engine limits
 ]
 
 
@@ -144,6 +146,13 @@ EDGE = {
     "one_index_line": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid, cb.nlen * 0 + 1),
     "all_lines_one_hunk": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid * 0, cb.nlen * 0 + cb.Ne),
     "zero_attributes": lambda cb: CommitBatch(cb.x * 0, cb.a, cb.y, cb.hid, cb.nlen),
+    # real-valued, signed, all-distinct attributes (the sorted-x entity sums see nd = Ne)
+    "float_attributes": lambda cb: CommitBatch(
+        (np.random.default_rng(3).standard_normal(cb.x.shape) * 4).astype(np.float32),
+        cb.a, cb.y, cb.hid, cb.nlen),
+    "dense_entity_rows": lambda cb: CommitBatch(
+        cb.x, ((np.random.default_rng(4).random(cb.a.shape) < 0.6)
+               & ~np.eye(cb.Ne, dtype=bool)[None]).astype(np.uint8), cb.y, cb.hid, cb.nlen),
 }
 
 

@@ -35,11 +35,15 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from hdgnn import _lib
     lib = _lib.load()
-    assert lib.hdg_version() == 1
+    assert lib.hdg_version() == 2
     assert lib.hdg_param_count(2) == 2127
     assert lib.hdg_grad_len(2) == 2131
     ok = _lib.Shape(100, 200, 74, 2, 100)
     assert lib.hdg_workspace_bytes(ctypes.byref(ok)) > 0
+    assert lib.hdg_prep_bytes(ctypes.byref(ok)) > 0
+    for ne, nc in ((250, 114), (250, 150), (256, 160), (2, 2)):   # s3, s5, limits
+        sh = _lib.Shape(100, ne, nc, 2, 100)
+        assert lib.hdg_workspace_bytes(ctypes.byref(sh)) > 0, lib.hdg_last_error()
     bad = _lib.Shape(100, 300, 74, 2, 100)
     assert lib.hdg_workspace_bytes(ctypes.byref(bad)) == 0
     assert b"ne must be" in lib.hdg_last_error()

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase wall time of k_commit_mid from s_memrealtime stamps (100 MHz)."""
+"""Diagnostic: per-phase wall time of k_commit_step from s_memrealtime stamps (100 MHz)."""
 import ctypes
 import os
 import sys
@@ -20,7 +20,7 @@ for _ in range(3):
     eng.train_step(db)
 st = torch.zeros(B * 32, dtype=torch.int64, device="cuda")
 for _ in range(3):
-    _lib.check(eng.lib.hdg_debug_mid_stamps(ctypes.byref(eng.shape), ctypes.byref(db.struct()),
+    _lib.check(eng.lib.hdg_debug_step_stamps(ctypes.byref(eng.shape), ctypes.byref(db.struct()),
                                             ctypes.c_void_p(eng.params.data_ptr()),
                                             ctypes.c_void_p(eng.workspace.data_ptr()),
                                             ctypes.c_void_p(st.data_ptr()), eng._stream()))

@@ -18,7 +18,7 @@ def find(pattern):
 
 
 def short(name):
-    for k in ("k_entity_fwd", "k_entity_bwd", "k_commit_mid", "k_grad_reduce", "k_adam_tf"):
+    for k in ("k_commit_step", "k_grad_reduce", "k_adam_tf", "k_prep_sort", "k_prep_maps"):
         if k in name:
             return k
     return name[:60]
