@@ -1,4 +1,7 @@
-"""Summarise a tools/profile.sh run into profiles/<tag>/ (kernel stats + HBM traffic)."""
+"""Summarise a tools/profile.sh run (merged back under gpurun_out/prof_<tag>) into
+profiles/<tag>/ (kernel stats + HBM traffic) and profiles/hbm_traffic.json (bench.py's
+roofline.traffic source).  Run locally after the gpurun call:
+    python tools/prof_summary.py gpurun_out/prof_r01 r01"""
 import csv
 import glob
 import json
@@ -72,3 +75,9 @@ print(txt)
 if traffic:
     with open(os.path.join(dst, "hbm_traffic_all.json"), "w") as f:
         json.dump({"batch": 100, "ne": 200, "nc": 74, "bytes_per_launch": traffic}, f, indent=1)
+    if "k_commit_step" in traffic:
+        with open(os.path.join(root, "profiles", "hbm_traffic.json"), "w") as f:
+            json.dump({"kernel": "k_commit_step", "batch": 100, "ne": 200, "nc": 74,
+                       "bytes_per_launch": traffic["k_commit_step"],
+                       "source": "profiles/%s/summary.txt (2*FETCH_SIZE + WRITE_SIZE)" % tag},
+                      f, indent=1)
