@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100, help="commits per GPU")
     ap.add_argument("--ne", type=int, default=200)
     ap.add_argument("--nc", type=int, default=74)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))

@@ -1,0 +1,287 @@
+"""Drop-in for the reference's model_2.graph2graph (HD-GNN/S), backed by libhdgnn.so.
+
+Same constructor (model_2.py:16-33), same train(args) / test(args) flow, files and
+printed lines (model_2.py:336-407, 434-548); the TF graph + sess.run are replaced by
+the engine (hdgnn.engine.Engine -> C ABI -> k_commit_step on MI355X):
+
+    reference                                         here
+    sess.run([..., trainer], feed_dict) (369-383)     Engine.train_step(DeviceBatch)
+    sess.run([loss, loss_map, C_edge_output2]) (486)  Engine.forward(DeviceBatch)
+    read_data(self, Step) -> 12 dense arrays          reader(self, Step) -> the same tuple,
+                                                      then data.compact_from_read_data
+    saver.save / restore (409-432)                    .npz of the 18 TF-named variables
+
+Reference behaviours kept on purpose: every batch feeds the maps
+of the first Mini_batch commits (B.2, also in test); remainder commits are dropped
+(B.3); test() looks for its checkpoint under checkpoint_dir/Repo/Repo/model_2/Step and
+so normally evaluates freshly initialised weights (B.8).
+
+Data parallel: when torch.distributed is initialised with world W > 1, every batch of
+Mini_batch commits is split into W contiguous shards (Mini_batch % W == 0); the flat
+gradient is all-reduced once per step (Engine.allreduce) and the epoch accuracy is an
+all-reduced correct count.  Outputs written to disk are gathered on rank 0.
+"""
+import os
+import time
+
+import numpy as np
+
+from . import layout, metrics
+from .data import DeviceBatch, compact_from_read_data
+
+HS = 20   # De_e = De_er = h_size compiled into the engine
+
+
+def shard_plan(n_commits, mini_batch, world=1, rank=0):
+    """Per reference batch j (floor division, model_2.py:364): this rank's commit range and
+    the batch positions whose maps it feeds (Esc/Etc/..[:Mini_batch], model_2.py:376-381)
+    -> list of ((commit_lo, commit_hi), (pos_lo, pos_hi))."""
+    if mini_batch % world:
+        raise ValueError("Mini_batch=%d is not divisible by world=%d" % (mini_batch, world))
+    lb = mini_batch // world
+    lo = rank * lb
+    return [((j * mini_batch + lo, j * mini_batch + lo + lb), (lo, lo + lb))
+            for j in range(n_commits // mini_batch)]
+
+
+def _default_reader(model, step):
+    """The reference's own loader (utils2.read_data), imported from the caller's path the
+    way model_2.py does (`from utils2 import read_data`)."""
+    try:
+        from utils2 import read_data
+    except ImportError as e:       # no silent fallback: the dataset loader is the caller's
+        raise ImportError("graph2graph needs a reader: pass reader=... or put the reference's "
+                          "utils2.py on sys.path") from e
+    return read_data(model, step)
+
+
+class graph2graph(object):
+    def __init__(self, sess, Ds, Ne, Nc, Ner, Ncr, Dr, De_e, De_er, Mini_batch, checkpoint_dir,
+                 epoch, Ds_inter, Dr_inter, Step, Repo, *, reader=None, device=None, seed=0,
+                 lr=3e-4, process_group=None):
+        self.sess = sess                       # accepted and ignored (no TF session)
+        self.Ds, self.Ne, self.Nc, self.Ner, self.Ncr, self.Dr = Ds, Ne, Nc, Ner, Ncr, Dr
+        self.Ds_inter, self.Dr_inter = Ds_inter, Dr_inter
+        self.De_e, self.De_er = De_e, De_er
+        self.mini_batch_num = Mini_batch
+        self.epoch = epoch
+        self.checkpoint_dir = checkpoint_dir
+        self.Step, self.Repo = Step, Repo
+        self.reader = reader or _default_reader
+        self.seed, self.lr, self.pg = seed, lr, process_group
+        self.device = device
+        if (Ds, Dr, De_e, De_er) != (1, 2, HS, HS):
+            raise ValueError("the engine is built for Ds=1, Dr=2, De_e=De_er=20 (got %s)"
+                             % ((Ds, Dr, De_e, De_er),))
+        if Ner != Ne * (Ne - 1) or Ncr != Nc * (Nc - 1):
+            raise ValueError("Ner/Ncr must be Ne(Ne-1)/Nc(Nc-1) (complete relation digraphs)")
+        self.build_model()
+
+    # ------------------------------------------------------------------ model
+    def build_model(self):
+        import torch
+        from .engine import Engine
+        dist = torch.distributed
+        self.world = dist.get_world_size(self.pg) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(self.pg) if self.world > 1 else 0
+        if self.mini_batch_num % self.world:
+            raise ValueError("Mini_batch=%d is not divisible by world=%d"
+                             % (self.mini_batch_num, self.world))
+        self.local_batch = self.mini_batch_num // self.world
+        dev = self.device or torch.device("cuda", torch.cuda.current_device())
+        self.engine = Engine(self.Ne, self.Nc, self.local_batch, device=dev,
+                             batch_global=self.mini_batch_num, lr=self.lr,
+                             process_group=self.pg)
+        self._initialize()
+        # fetchable attributes (filled by the last step, like sess.run results)
+        self.C_edge_output2 = None
+        self.C_edge_output2_logits = None
+        self.loss_Hedge_mse = None
+        self.loss_map = None
+        self.loss_para = None
+
+    def _initialize(self):
+        """tf.global_variables_initializer(): truncated_normal(0.1) weights, zero biases,
+        fresh Adam slots and beta powers."""
+        self.engine.set_params(layout.init_flat(self.seed))
+
+    @property
+    def vars(self):
+        return layout.split(self.engine.get_params())
+
+    @property
+    def theta(self):
+        return self.vars["map_conv/map_theta2:0"]
+
+    # ------------------------------------------------------------------ data
+    def _compact(self):
+        tup = self.reader(self, self.Step)
+        train, test, maps = compact_from_read_data(tup, self.Ne, self.Nc, self.mini_batch_num)
+        return tup, train, test, maps
+
+    def _device_batches(self, part, maps):
+        """Per reference batch j: this rank's shard of commits j*mb .. (j+1)*mb with the
+        maps of batch positions (model_2.py:365-381: Esc/Etc/..[:Mini_batch])."""
+        out = []
+        for (c0, c1), (p0, p1) in shard_plan(part.B, self.mini_batch_num, self.world, self.rank):
+            sh = part.slice(c0, c1).with_maps(maps.slice(p0, p1))
+            out.append(DeviceBatch.from_host(sh, self.engine.device))
+        return out
+
+    def _gather(self, arr):
+        """Concatenate a per-rank (lb, ...) array over ranks on every rank."""
+        if self.world == 1:
+            return arr
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr)).to(self.engine.device)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        torch.distributed.all_gather(parts, t, group=self.pg)
+        return torch.cat(parts).cpu().numpy()
+
+    def _allsum(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.engine.device)
+        torch.distributed.all_reduce(t, group=self.pg)
+        return t.item()
+
+    # ------------------------------------------------------------------ train
+    def train(self, args):
+        import torch
+        self._initialize()
+        tup, train, _, maps = self._compact()
+        C_edge_train = np.asarray(tup[4])
+        batches = self._device_batches(train, maps)
+        nb = len(batches)
+        counter = 1
+        start_time1 = time.time()
+        eng = self.engine
+        for i in range(self.epoch):
+            tr_loss_Hedge = 0.0
+            tr_loss_map = 0.0
+            correct = 0
+            for j, db in enumerate(batches):
+                eng.train_step(db)
+                stats = eng.stats.cpu().numpy()            # pre-update, like sess.run
+                probs = eng.probs.cpu().numpy()
+                tr_loss_Hedge += float(stats[0])
+                tr_loss_map += float(stats[1])
+                self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(stats[0]),
+                                                                      float(stats[1]),
+                                                                      float(stats[2]))
+                self.C_edge_output2 = probs
+                self.C_edge_output2_logits = eng.logits.cpu().numpy()
+                lo = j * self.mini_batch_num + self.rank * self.local_batch
+                correct += metrics.top_acc_count(C_edge_train[lo:lo + self.local_batch], probs)
+            torch.cuda.synchronize(eng.device)
+            acc_top = self._allsum(correct) / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
+            theta = self.theta.reshape([2])
+            resultString = "Epoch " + str(i + 1) + \
+                           " acc: " + str(acc_top)[0:6] + \
+                           " Hedge loss: " + str(tr_loss_Hedge / nb if nb else 0.0)[0:6] + \
+                           " map MSE: " + str(tr_loss_map / nb if nb else 0.0)[0:6] + \
+                           " theta: " + str(theta[0]) + ' ' + str(theta[1]) + '\n'
+            if self.rank == 0:
+                filepath = r'outputSelf/{}/model_2/{}/result_{}.npy'.format(args.Repo, self.Step,
+                                                                              self.Step)
+                os.makedirs(os.path.dirname(filepath), exist_ok=True)
+                with open(filepath, "a", encoding='utf-8') as f:
+                    f.write(resultString)
+                print(resultString)
+            counter += 1
+            self.save(args.checkpoint_dir, counter)
+        end_time1 = time.time()
+        if self.rank == 0:
+            print('test time:' + str(end_time1 - start_time1))
+
+    # ------------------------------------------------------------------ checkpoints
+    def _model_dir(self, checkpoint_dir):
+        return os.path.join(checkpoint_dir, "%s" % (self.Repo + '/model_2/' + str(self.Step)))
+
+    def save(self, checkpoint_dir, step):
+        """g2g.model-<step>.npz holding the 18 variables under their TF names, the Adam
+        slots and beta powers (enough to resume), plus a TF-style 'checkpoint' index."""
+        if self.rank != 0:
+            return
+        d = self._model_dir(checkpoint_dir)
+        os.makedirs(d, exist_ok=True)
+        eng = self.engine
+        name = "g2g.model-%d" % step
+        state = dict(self.vars)
+        state["_adam_m"] = eng.m.cpu().numpy()
+        state["_adam_v"] = eng.v.cpu().numpy()
+        state["_beta_pow"] = eng.beta_pow.cpu().numpy()
+        np.savez(os.path.join(d, name + ".npz"), **state)
+        with open(os.path.join(d, "checkpoint"), "w") as f:
+            f.write('model_checkpoint_path: "%s"\n' % name)
+
+    def load(self, checkpoint_dir):
+        print(" [*] Reading checkpoint...")
+        d = self._model_dir(checkpoint_dir)
+        idx = os.path.join(d, "checkpoint")
+        if not os.path.exists(idx):
+            return False
+        with open(idx) as f:
+            name = f.read().split('"')[1]
+        path = os.path.join(d, name + ".npz")
+        if not os.path.exists(path):
+            return False
+        import torch
+        z = np.load(path, allow_pickle=False)
+        flat = np.concatenate([np.asarray(z[n], np.float32).reshape(-1)
+                               for n, _ in layout.specs()])
+        eng = self.engine
+        eng.set_params(flat)
+        if "_adam_m" in z:
+            eng.m.copy_(torch.from_numpy(z["_adam_m"]))
+            eng.v.copy_(torch.from_numpy(z["_adam_v"]))
+            eng.beta_pow.copy_(torch.from_numpy(z["_beta_pow"]))
+        return True
+
+    # ------------------------------------------------------------------ test
+    def test(self, args):
+        tup, _, test, maps = self._compact()
+        C_edge_test = np.asarray(tup[5])
+        self._initialize()
+        checkpoint_dir = os.path.join(self.checkpoint_dir, self.Repo)
+        if self.load(checkpoint_dir):
+            print(" [*] Load SUCCESS")
+        else:
+            print(" [!] Load failed...")
+        te_loss_Hedge = 0.0
+        te_loss_map = 0.0
+        C_edge_t = []
+        eng = self.engine
+        start_time = time.time()
+        end_time = start_time
+        for db in self._device_batches(test, maps):
+            probs, logits, ce_sum = eng.forward(db)
+            p = probs.cpu().numpy()
+            ce = self._allsum(float(ce_sum.item())) / (self.mini_batch_num * self.Ncr)
+            th1 = self.vars["map_conv/map_theta1:0"].reshape(-1).astype(np.float64)
+            th2 = self.vars["map_conv/map_theta2:0"].reshape(-1).astype(np.float64)
+            lmap = 0.01 * (np.sqrt((th2 ** 2).sum()) + np.sqrt((th1 ** 2).sum()))
+            end_time = time.time()
+            te_loss_Hedge += ce
+            te_loss_map += lmap
+            self.C_edge_output2 = p
+            C_edge_t.append(self._gather(p))
+        n_used = len(C_edge_t) * self.mini_batch_num
+        C_edge_t1 = (np.array(C_edge_t).reshape(n_used, self.Dr, self.Ncr) if C_edge_t
+                     else np.zeros((0, self.Dr, self.Ncr), np.float32))
+        if self.rank != 0:
+            return
+        step_dir = 'outputSelf/' + args.Repo + '/model_2/' + str(self.Step) + '/'
+        os.makedirs(step_dir, exist_ok=True)
+        np.save(step_dir + 'C_edge_t' + str(self.Ne) + '.npy', C_edge_t1)
+        np.save(step_dir + 'C_edge_y' + str(self.Ne) + '.npy',
+                C_edge_test.reshape(len(C_edge_test), self.Dr, self.Ncr))
+        C_edge_t2 = metrics.process_edge(C_edge_t1)
+        C_edge_y = C_edge_test[:n_used]
+        print('topol_acc: ' + str(metrics.top_ACC(C_edge_y, C_edge_t2)))
+        print('prec: ' + str(metrics.prec(C_edge_y, C_edge_t2)))
+        print('recall: ' + str(metrics.recall(C_edge_y, C_edge_t2)))
+        print('F1-score: ' + str(metrics.f1(C_edge_y, C_edge_t2)))
+        print('AUC-score: ' + str(metrics.AUC(C_edge_y, C_edge_t2)))
+        print('test time:' + str(end_time - start_time))

@@ -1,0 +1,77 @@
+"""hdgnn.model.graph2graph (the drop-in for model_2.graph2graph) end to end on the GPU:
+train(args) for 2 epochs on the reference loader's golden 12-tuple (Ne=7, Nc=5,
+50 train / 50 test commits, Mini_batch=25 -> 2 steps per epoch) against the oracle
+driven through the same batch plan; then test(args) and its output files."""
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from hdgnn import data, layout
+from oracle import model_ref
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["E_node_train", "E_node_test", "E_edge_train", "E_edge_test", "C_edge_train",
+         "C_edge_test", "Es_data", "Et_data", "Cs_label", "Ct_label", "Esc_data", "Etc_data"]
+
+
+def _tuple(golden_dir):
+    z = np.load(os.path.join(golden_dir, "loader_tiny.npz"))
+    with open(os.path.join(golden_dir, "loader_tiny.json")) as f:
+        meta = json.load(f)
+    return tuple(z[n] for n in NAMES), meta
+
+
+def test_graph2graph_train_and_test(golden_dir, tmp_path, monkeypatch):
+    from hdgnn.model import graph2graph
+    tup, meta = _tuple(golden_dir)
+    ne, nc, mb = meta["Ne"], meta["Nc"], 25
+    monkeypatch.chdir(tmp_path)
+    args = types.SimpleNamespace(Repo="tiny", checkpoint_dir=str(tmp_path / "ckpt"))
+    m = graph2graph(None, Ds=1, Ne=ne, Nc=nc, Ner=ne * (ne - 1), Ncr=nc * (nc - 1), Dr=2,
+                    De_e=20, De_er=20, Mini_batch=mb, checkpoint_dir=args.checkpoint_dir,
+                    epoch=2, Ds_inter=1, Dr_inter=2, Step=2, Repo="tiny",
+                    reader=lambda model, step: tup, seed=7)
+    m.train(args)
+    torch.cuda.synchronize()
+
+    # oracle through the same plan: 2 epochs x 2 batches, maps of positions [:mb]
+    train, test, maps = data.compact_from_read_data(tup, ne, nc, mb)
+    theta = layout.init_flat(7).astype(np.float64)
+    opt = model_ref.AdamTF(theta.size)
+    for _ in range(2):
+        for j in range(2):
+            sh = train.slice(j * mb, (j + 1) * mb).with_maps(maps)
+            P = model_ref.unflatten(theta.astype(np.float32).astype(np.float64))
+            _, g = model_ref.loss_and_grads(P, sh.x.astype(np.float64), sh.a, sh.y, sh.hid,
+                                            sh.nlen)
+            from oracle import layout as olayout
+            keys = [k for k, _, _ in olayout.keyed_specs(2)]
+            theta = opt.step(theta, np.concatenate([g[k].reshape(-1) for k in keys]))
+    np.testing.assert_allclose(m.engine.get_params(), theta, rtol=0, atol=5e-6)
+
+    res = tmp_path / "outputSelf" / "tiny" / "model_2" / "2" / "result_2.npy"
+    lines = res.read_text().splitlines()
+    assert len(lines) == 2 and lines[0].startswith("Epoch 1 acc: ")
+    ck = tmp_path / "ckpt" / "tiny" / "model_2" / "2"
+    assert (ck / "checkpoint").exists() and (ck / "g2g.model-3.npz").exists()
+    z = np.load(ck / "g2g.model-3.npz")
+    np.testing.assert_array_equal(z["phi_E_O1/r1_w1o:0"].reshape(-1),
+                                  m.engine.get_params()[:80])
+
+    # test(): checkpoint looked up under checkpoint_dir/Repo/Repo/... (reference quirk)
+    m.test(args)
+    out = np.load(tmp_path / "outputSelf" / "tiny" / "model_2" / "2" / "C_edge_t7.npy")
+    assert out.shape == (50, 2, nc * (nc - 1))
+    P0 = model_ref.unflatten(layout.init_flat(7).astype(np.float64))
+    ref = []
+    for j in range(2):
+        sh = test.slice(j * mb, (j + 1) * mb).with_maps(maps)
+        o = model_ref.forward(model_ref.to_torch_params(P0, requires_grad=False),
+                              sh.x.astype(np.float64), sh.a, sh.y, sh.hid, sh.nlen)
+        ref.append(o["probs"].detach().numpy().transpose(0, 2, 1))
+    np.testing.assert_allclose(out, np.concatenate(ref), atol=1e-5)
