@@ -118,7 +118,12 @@ def main():
 
     B, ne, nc = args.batch, args.ne, args.nc
     cb = synth_commits(B, ne, nc, seed_for(1, rank))
-    db = cb.to_device(dev)
+    cb.to_device(dev)                            # warm the upload / prepare path once
+    torch.cuda.synchronize(dev)
+    t_up = time.perf_counter()
+    db = cb.to_device(dev)                       # host arrays -> HBM + hdg_prepare
+    torch.cuda.synchronize(dev)
+    upload_ms = 1e3 * (time.perf_counter() - t_up)
     eng = Engine(ne, nc, B, device=dev, batch_global=B * world)
     eng.set_params(layout.init_flat(0))
 
@@ -203,6 +208,8 @@ def main():
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world},
             "roofline": roofline, "cpu_baseline": cpu,
+            "upload_prepare_ms": round(upload_ms, 3),
+            "pcie_inclusive_commits_per_s": round(world * B / ((ms_per_step + upload_ms) * 1e-3), 1),
             "kernels_ms": {k: round(v, 5) for k, v in kern_ms.items()}}
     print(json.dumps(line), flush=True)
     if world > 1:
