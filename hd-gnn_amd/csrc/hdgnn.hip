@@ -123,30 +123,44 @@ __device__ __forceinline__ void pair_tile(
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
     float* __restrict__ ysum, float* __restrict__ cred) {
+  typedef float p2 __attribute__((ext_vector_type(2)));
   constexpr int NP16 = 16 * SMAX;
   constexpr int NW = (SMAX + 1) / 2;
+  constexpr int KP = KK / 2, KT = KK & 1;      // packed fp32 pairs (v_pk_*) + odd tail
   const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
   const int S = (N + 15) >> 4;
+  const p2 z2 = {0.f, 0.f};
 
-  float cacc[SMAX][KK];
+  p2 cacc2[SMAX][KP > 0 ? KP : 1];
+  float cacct[SMAX];
 #pragma unroll
-  for (int c = 0; c < SMAX; ++c)
+  for (int c = 0; c < SMAX; ++c) {
 #pragma unroll
-    for (int k = 0; k < KK; ++k) cacc[c][k] = 0.f;
-  float yacc[KK], dk[KK];
+    for (int p = 0; p < KP; ++p) cacc2[c][p] = z2;
+    cacct[c] = 0.f;
+  }
+  p2 yacc2[KP > 0 ? KP : 1], dk2[KP > 0 ? KP : 1];
+  float yacct = 0.f, dkt = KT ? dl[k0 + KK - 1] : 0.f;
 #pragma unroll
-  for (int k = 0; k < KK; ++k) { yacc[k] = 0.f; dk[k] = dl[k0 + k]; }
+  for (int p = 0; p < KP; ++p) {
+    yacc2[p] = z2;
+    dk2[p] = (p2){dl[k0 + 2 * p], dl[k0 + 2 * p + 1]};
+  }
 
   for (int s = 0; s < S; ++s) {
     const int i = ti + 16 * s;
     const bool iv = i < N;
-    float a[KK], rw[KK], racc[KK];
+    p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
+    const float* Ai = A + i * LD + k0;
 #pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      a[k] = A[i * LD + k0 + k];
-      rw[k] = (MODE == 1) ? wr[i * LD + k0 + k] : 0.f;
-      racc[k] = 0.f;
+    for (int p = 0; p < KP; ++p) {
+      a2[p] = (p2){Ai[2 * p], Ai[2 * p + 1]};
+      rw2[p] = (MODE == 1) ? (p2){wr[i * LD + k0 + 2 * p], wr[i * LD + k0 + 2 * p + 1]} : z2;
+      racc2[p] = z2;
     }
+    const float at = KT ? Ai[KK - 1] : 0.f;
+    const float rwt = (MODE == 1 && KT) ? wr[i * LD + k0 + KK - 1] : 0.f;
+    float racct = 0.f;
     uint32_t wrow[NW];
     const int ib = iv ? i : 0;
 #pragma unroll
@@ -158,33 +172,75 @@ __device__ __forceinline__ void pair_tile(
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
       const float af = (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
+      const p2 af2 = {af, af};
       float g = 0.f;
       if constexpr (MODE == 2) {   // branch-free: clamped load, masked value
         const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;
         g = gam[ic * gld + jc] * ((iv && j < N && j != i) ? 1.f : 0.f);
       }
+      const float* Bj = Bv + j * LD + k0;
 #pragma unroll
-      for (int k = 0; k < KK; ++k) {
-        const float z = a[k] + fmaf(af, dk[k], Bv[j * LD + k0 + k]);
+      for (int p = 0; p < KP; ++p) {
+        const p2 bb = {Bj[2 * p], Bj[2 * p + 1]};
+        const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
+        p2 e;
+        if constexpr (MODE == 0) {
+          e = __builtin_elementwise_max(z, z2);
+        } else {
+          p2 w;
+          if constexpr (MODE == 1) {
+            w = rw2[p] + (p2){wc[j * LD + k0 + 2 * p], wc[j * LD + k0 + 2 * p + 1]};
+          } else {
+            w = (p2){g, g};
+          }
+          e = (p2){z.x > 0.f ? w.x : 0.f, z.y > 0.f ? w.y : 0.f};
+          yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
+        }
+        racc2[p] += e;
+        cacc2[c][p] += e;
+      }
+      if constexpr (KT) {
+        const float z = at + fmaf(af, dkt, Bj[KK - 1]);
         float e;
         if constexpr (MODE == 0) {
           e = reluf(z);
         } else {
-          const float w = (MODE == 1) ? (rw[k] + wc[j * LD + k0 + k]) : g;
+          const float w = (MODE == 1) ? (rwt + wc[j * LD + k0 + KK - 1]) : g;
           e = (z > 0.f) ? w : 0.f;
-          yacc[k] = fmaf(af, e, yacc[k]);
+          yacct = fmaf(af, e, yacct);
         }
-        racc[k] += e;
-        cacc[c][k] += e;
+        racct += e;
+        cacct[c] += e;
       }
     }
+    float rs[KK];
 #pragma unroll
-    for (int k = 0; k < KK; ++k) racc[k] = row16_sum(racc[k]);
+    for (int p = 0; p < KP; ++p) {
+      rs[2 * p] = row16_sum(racc2[p].x);
+      rs[2 * p + 1] = row16_sum(racc2[p].y);
+    }
+    if constexpr (KT) rs[KK - 1] = row16_sum(racct);
     if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
 #pragma unroll
-      for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = racc[k];
+      for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = rs[k];
     }
   }
+  float cacc[SMAX][KK], yacc[KK];
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c) {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      cacc[c][2 * p] = cacc2[c][p].x;
+      cacc[c][2 * p + 1] = cacc2[c][p].y;
+    }
+    if constexpr (KT) cacc[c][KK - 1] = cacct[c];
+  }
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
+    yacc[2 * p] = yacc2[p].x;
+    yacc[2 * p + 1] = yacc2[p].y;
+  }
+  if constexpr (KT) yacc[KK - 1] = yacct;
   // close the column partials: 4 ti per wave by shuffles, then 4 waves via LDS
   float* credy = cred + 4 * NP16 * KK;
 #pragma unroll
@@ -520,6 +576,34 @@ __device__ __forceinline__ float dot20(const float* row, const float (&w)[HS], f
   return acc;
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// One 16x16 tile of C = A.B on v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate; exact
+// f32 fmaf-chain numerics).  fa(r, k) = A[row0 + r][k], fb(k, c) = B[k][col0 + c], both
+// 0 outside the matrix, so K is zero-padded to a multiple of 4.  Lane l's fragment holds
+// C[row0 + 4*(l>>4) + i][col0 + (l&15)] in c[i].  Wave-uniform call (MFMA needs all lanes).
+template <class FA, class FB>
+__device__ __forceinline__ f4v mfma_tile16(FA fa, FB fb, const int K, const int lane) {
+  const int r = lane & 15, q = lane >> 4;
+  f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  int k = 0;
+  for (; k + 16 <= K; k += 16) {      // operands of 4 steps issued before their MFMAs
+    float a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = fa(r, k + 4 * u + q);
+      b[u] = fb(k + 4 * u + q, r);
+    }
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c1, 0, 0, 0);
+  }
+  for (; k < K; k += 4)
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(fa(r, k + q), fb(k + q, r), c0, 0, 0, 0);
+  return c0 + c1;
+}
+
 // first layer of mlp_entity_B1 for hidden unit kk (model_2.py:165-170):
 //   W1^T [x_i, x_j, [a=0], [a=1]] + b1 = u_i + v_j + a_ij d,
 //   u = fma(x, W1[0], W1[2] + b1), v = x * W1[1], d = W1[3] - W1[2]
@@ -708,7 +792,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float* __restrict__ Wg, float* __restrict__ Esave, uint16_t* __restrict__ rowq,
     float* __restrict__ gamg, float* __restrict__ part, float* __restrict__ probs,
     float* __restrict__ logits, int Ne, int Nc, float ce_scale,
-    unsigned long long* __restrict__ stamps) {
+    unsigned long long* __restrict__ stamps, float* __restrict__ aux,
+    const float* __restrict__ bpow) {
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
@@ -783,7 +868,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* hE = U + 2 * NE4 * HS;
   uint32_t* abL = (uint32_t*)(U + 3 * NE4 * HS);
   uint32_t* atL = abL + ((Ne * WE + 3) & ~3);
-  for (int i = t; i < NP; i += NT_MID) Ws[i] = Wg[i];
+  float l2 = 0.f;
+  for (int i = t; i < NP; i += NT_MID) {
+    const float w = Wg[i];
+    Ws[i] = w;
+    l2 = fmaf(w, w, l2);
+  }
+  if (aux && b == 0) {                     // pre-update loss_para / loss_map / Adam factor
+    l2 = wave_sum(l2);
+    if (lane == 0) red[wv * 32] = l2;
+  }
   for (int i = t; i < Ne; i += NT_MID) {
     xs[i] = x[(size_t)b * Ne + i];
     xsrt[i] = reinterpret_cast<const float*>(pp + PL.xsrt)[i];
@@ -800,6 +894,20 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   __syncthreads();
+  if (aux && b == 0 && t == 0) {           // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
+    float s2 = 0.f;
+    for (int w = 0; w < NT_MID / 64; ++w) s2 += red[w * 32];
+    const float n1 = sqrtf(Ws[TH1] * Ws[TH1] + Ws[TH1 + 1] * Ws[TH1 + 1]);
+    const float n2 = sqrtf(Ws[TH2] * Ws[TH2] + Ws[TH2 + 1] * Ws[TH2 + 1]);
+    const float b1p = bpow[0], b2p = bpow[1];
+    aux[0] = 0.0005f * s2;
+    aux[1] = 0.01f * (n2 + n1);
+    aux[2] = n1;
+    aux[3] = n2;
+    aux[4] = sqrtf(1.f - b2p) / (1.f - b1p);
+    aux[5] = b1p * 0.9f;
+    aux[6] = b2p * 0.999f;
+  }
   MID_STAMP();
 
   // ---- E1: mlp_entity_B1 pair sums (model_2.py:161-175, agg model_2.py:181-188) -----
@@ -816,29 +924,55 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   MID_STAMP();
 
   // ---- M1: E_bar = P W5 + 2(Ne-1) b5   (agg_entity_B1, model_2.py:181-188) ----------
-  if (msl < NSL) {
-    float w[HS];
+  //   node GEMMs run as 16x16 MFMA tiles: (node block, column block) per wave
+  const int ntm_e = (Ne + 15) >> 4;
+  for (int tile = wv; tile < 2 * ntm_e; tile += NT_MID / 64) {
+    const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
+    const f4v c = mfma_tile16(
+        [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? Ps[i * HS + k] : 0.f; },
+        [&](int k, int j) {
+          const int m = col0 + j;
+          return (k < HS && m < HS) ? Ws[E1_W5 + k * HS + m] : 0.f;
+        }, HS, lane);
+    const int m = col0 + (lane & 15);
+    if (m < HS) {
+      const float bias = twoNe1 * Ws[E1_B5 + m];
 #pragma unroll
-    for (int m = 0; m < HS; ++m) w[m] = Ws[E1_W5 + m * HS + mk];
-    const float bias = twoNe1 * Ws[E1_B5 + mk];
-    for (int i = msl; i < Ne; i += NSL) {
-      const float v = dot20(Ps + i * HS, w, 0.f) + bias;
-      Eb[i * HS + mk] = v;
-      EbG[i * HS + mk] = v;
+      for (int q = 0; q < 4; ++q) {
+        const int i = row0 + 4 * (lane >> 4) + q;
+        if (i < Ne) {
+          Eb[i * HS + m] = c[q] + bias;
+          EbG[i * HS + m] = c[q] + bias;
+        }
+      }
     }
   }
   __syncthreads();
   MID_STAMP();
-  // ---- M2: mlp2_entity_B1 (model_2.py:190-205) --------------------------------------
-  if (msl < NSL) {
-    float w[HS];
+  // ---- M2: mlp2_entity_B1 (model_2.py:190-205): h = relu([x, E_bar] W1' + b1') -------
+  for (int tile = wv; tile < 2 * ntm_e; tile += NT_MID / 64) {
+    const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
+    const f4v c = mfma_tile16(
+        [&](int r, int k) {
+          const int i = row0 + r;
+          return (i < Ne && k <= HS) ? (k == 0 ? xs[i] : Eb[i * HS + k - 1]) : 0.f;
+        },
+        [&](int k, int j) {
+          const int m = col0 + j;
+          return (k <= HS && m < HS) ? Ws[E3_W1 + k * HS + m] : 0.f;
+        }, HS + 1, lane);
+    const int m = col0 + (lane & 15);
+    if (m < HS) {
+      const float bias = Ws[E3_B1 + m];
 #pragma unroll
-    for (int m = 0; m < HS; ++m) w[m] = Ws[E3_W1 + (1 + m) * HS + mk];
-    const float w0 = Ws[E3_W1 + mk], bb = Ws[E3_B1 + mk];
-    for (int i = msl; i < Ne; i += NSL) {
-      const float v = reluf(dot20(Eb + i * HS, w, fmaf(xs[i], w0, bb)));
-      hE[i * HS + mk] = v;
-      hEG[i * HS + mk] = v;
+      for (int q = 0; q < 4; ++q) {
+        const int i = row0 + 4 * (lane >> 4) + q;
+        if (i < Ne) {
+          const float v = reluf(c[q] + bias);
+          hE[i * HS + m] = v;
+          hEG[i * HS + m] = v;
+        }
+      }
     }
   }
   __syncthreads();
@@ -862,13 +996,34 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
     const float* ncst = reinterpret_cast<const float*>(pp + PL.ncst);
-    for (int task = wv; task < 2 * Nc; task += NT_MID / 64) {      // wave-uniform
-      const int c = task >> 1, m = task & 1;
-      const uint16_t* kr = (m ? kt : ks) + (size_t)c * Ne;
-      float acc = 0.f;
-      for (int I = lane; I < Ne; I += 64) acc = fmaf((float)kr[I], xps[I], acc);
-      acc = wave_sum(acc);
-      if (lane == 0) nb[4 * c + m] = acc;
+    // 4 tasks (c, m) per trip, each lane's <= 4 elements per task unrolled: all 16 global
+    // loads of a trip are in flight before the first reduction
+    for (int t0 = 4 * wv; t0 < 2 * Nc; t0 += 4 * (NT_MID / 64)) {   // wave-uniform
+      float kv[4][4], xv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int I = lane + 64 * q;
+        xv[q] = I < Ne ? xps[I] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int task = t0 + u < 2 * Nc ? t0 + u : 2 * Nc - 1;
+        const uint16_t* kr = ((task & 1) ? kt : ks) + (size_t)(task >> 1) * Ne;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int I = lane + 64 * q;
+          kv[u][q] = (float)kr[I < Ne ? I : Ne - 1];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a = fmaf(kv[u][q], xv[q], a);
+        const float v = wave_sum(a);
+        const int task = t0 + u;
+        if (lane == 0 && task < 2 * Nc) nb[4 * (task >> 1) + (task & 1)] = v;
+      }
     }
     for (int c = t; c < Nc; c += NT_MID) {
       nb[4 * c + 2] = ncst[2 * c];
@@ -948,20 +1103,26 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* sig = Bf[4];
   float* tau = Bf[5];
   float* tauE = TAUE ? Bf[6] : nullptr;     // tau + eps: the y = 1 column operand of pass A
-  if (msl < NSL) {
-    float w[HS];
+  for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {
+    const int which = tile & 1, row0 = ((tile >> 2)) * 16, col0 = ((tile >> 1) & 1) * 16;
+    const float* src = which ? Hh : G;
+    const f4v c = mfma_tile16(
+        [&](int r, int k) { const int p = row0 + r; return (p < Nc && k < HS) ? src[p * HS + k] : 0.f; },
+        [&](int k, int j) { const int m = col0 + j; return (k < HS && m < HS) ? Mm[k * HS + m] : 0.f; },
+        HS, lane);
+    const int m = col0 + (lane & 15);
+    if (m < HS) {
+      const float off = which ? t0v[m] : s0v[m], ek = eps[m];
+      float* dst = which ? tau : sig;
 #pragma unroll
-    for (int l = 0; l < HS; ++l) w[l] = Mm[l * HS + mk];
-    const float s0 = s0v[mk], t0 = t0v[mk], ek = eps[mk];
-    for (int p = msl; p < NC16; p += NSL) {
-      float as = -INFINITY, at = -INFINITY;
-      if (p < Nc) {
-        as = dot20(G + p * HS, w, s0);
-        at = dot20(Hh + p * HS, w, t0);
+      for (int q = 0; q < 4; ++q) {
+        const int p = row0 + 4 * (lane >> 4) + q;
+        const float v = p < Nc ? c[q] + off : -INFINITY;
+        dst[p * HS + m] = v;
+        if constexpr (TAUE) {
+          if (which) tauE[p * HS + m] = v + ek;
+        }
       }
-      sig[p * HS + mk] = as;
-      tau[p * HS + mk] = at;
-      if constexpr (TAUE) tauE[p * HS + mk] = at + ek;
     }
   }
   __syncthreads();
@@ -990,7 +1151,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           reinterpret_cast<const float4*>((TAUE && yf > 0.f ? tauE : tau) + q * HS);
       const float4* ep4 = reinterpret_cast<const float4*>(eps);
       const float ey = TAUE ? 0.f : yf;       // without tau+eps: add y*eps here
-      float z0 = b0, z1 = b1;
+      typedef float p2 __attribute__((ext_vector_type(2)));
+      p2 zz = {b0, b1};                       // (z0, z1) += kappa_k (U2[k][0], U2[k][1])
       float kap[HS];
 #pragma unroll
       for (int v = 0; v < HS / 4; ++v) {
@@ -1003,19 +1165,22 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           c.z = fmaf(ey, ee.z, c.z);
           c.w = fmaf(ey, ee.w, c.w);
         }
-        kap[4 * v] = reluf(a.x + c.x);
-        kap[4 * v + 1] = reluf(a.y + c.y);
-        kap[4 * v + 2] = reluf(a.z + c.z);
-        kap[4 * v + 3] = reluf(a.w + c.w);
+        const p2 k01 = __builtin_elementwise_max((p2){a.x, a.y} + (p2){c.x, c.y}, (p2){0.f, 0.f});
+        const p2 k23 = __builtin_elementwise_max((p2){a.z, a.w} + (p2){c.z, c.w}, (p2){0.f, 0.f});
+        kap[4 * v] = k01.x;
+        kap[4 * v + 1] = k01.y;
+        kap[4 * v + 2] = k23.x;
+        kap[4 * v + 3] = k23.y;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const float4 w = u2[2 * v + h];           // w0_k, w1_k, w0_k+1, w1_k+1
-          z0 = fmaf(kap[4 * v + 2 * h], w.x, z0);
-          z1 = fmaf(kap[4 * v + 2 * h], w.y, z1);
-          z0 = fmaf(kap[4 * v + 2 * h + 1], w.z, z0);
-          z1 = fmaf(kap[4 * v + 2 * h + 1], w.w, z1);
+          zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h], kap[4 * v + 2 * h]},
+                                         (p2){w.x, w.y}, zz);
+          zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h + 1], kap[4 * v + 2 * h + 1]},
+                                         (p2){w.z, w.w}, zz);
         }
       }
+      const float z0 = zz.x, z1 = zz.y;
       const float mx = fmaxf(z0, z1);
       const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
       const float ssum = e0 + e1;
@@ -1030,7 +1195,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         gam[p * NC16 + q] = gmm;
         gsum += gmm;
 #pragma unroll
-        for (int k = 0; k < HS; ++k) zacc[k] = fmaf(kap[k], gmm, zacc[k]);
+        for (int k = 0; k < HS; k += 2) {       // packed: two hidden units per v_pk_fma
+          typedef float p2 __attribute__((ext_vector_type(2)));
+          const p2 r = __builtin_elementwise_fma((p2){kap[k], kap[k + 1]}, (p2){gmm, gmm},
+                                                 (p2){zacc[k], zacc[k + 1]});
+          zacc[k] = r.x;
+          zacc[k + 1] = r.y;
+        }
       }
     }
   }
@@ -1075,26 +1246,54 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   __syncthreads();
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
-  for (int e = t; e < HS * HS + HS; e += NT_MID) {
-    const int l = e / HS, k = e - l * HS;
-    if (l < HS) {
-      float a0 = 0.f, a1 = 0.f;
-      int p = 0;
-      for (; p + 1 < Nc; p += 2) {
-        a0 = fmaf(G[p * HS + l], Dsig[p * HS + k], fmaf(Hh[p * HS + l], Dtau[p * HS + k], a0));
-        a1 = fmaf(G[(p + 1) * HS + l], Dsig[(p + 1) * HS + k],
-                  fmaf(Hh[(p + 1) * HS + l], Dtau[(p + 1) * HS + k], a1));
+  //   one MFMA GEMM [G^T; 1; 0 | H^T; 0; 1] (22 x 2Nc) . [Dsig; Dtau] (2Nc x 20): rows
+  //   20, 21 are sum_p Dsig, sum_p Dtau.  4 tiles x 4 K-quarters, partials in the pair-
+  //   tile scratch (dead after pass B), then one fixed-order sum.
+  {
+    float* xpart = U + NBUF_H * NC16 * HS;            // [4 kq][4 tiles][256]
+    const int Nc4 = (Nc + 3) & ~3, K2 = 2 * Nc4;
+    const int kq = wv >> 2, tl = wv & 3;
+    const int row0 = (tl >> 1) * 16, col0 = (tl & 1) * 16;
+    const int kl = ((K2 / 4 + 3) & ~3) * kq;
+    const int kh = (kl + ((K2 / 4 + 3) & ~3) < K2) ? kl + ((K2 / 4 + 3) & ~3) : K2;
+    const f4v c = mfma_tile16(
+        [&](int r, int k) {
+          const int kk = kl + k, l = row0 + r;
+          const bool hi = kk >= Nc4;
+          const int p = hi ? kk - Nc4 : kk;
+          if (kk >= kh || p >= Nc) return 0.f;
+          if (l < HS) return (hi ? Hh : G)[p * HS + l];
+          return (l == HS + (hi ? 1 : 0)) ? 1.f : 0.f;
+        },
+        [&](int k, int j) {
+          const int kk = kl + k, m = col0 + j;
+          const bool hi = kk >= Nc4;
+          const int p = hi ? kk - Nc4 : kk;
+          return (kk < kh && p < Nc && m < HS) ? (hi ? Dtau : Dsig)[p * HS + m] : 0.f;
+        }, kh > kl ? kh - kl : 0, lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      xpart[(kq * 4 + tl) * 256 + (4 * (lane >> 4) + q) * 16 + (lane & 15)] = c[q];
+    __syncthreads();
+    {
+      const int tl2 = t >> 8, e = t & 255;
+      const float v = (xpart[(0 * 4 + tl2) * 256 + e] + xpart[(1 * 4 + tl2) * 256 + e]) +
+                      (xpart[(2 * 4 + tl2) * 256 + e] + xpart[(3 * 4 + tl2) * 256 + e]);
+      const int l = (tl2 >> 1) * 16 + (e >> 4), m = (tl2 & 1) * 16 + (e & 15);
+      if (m < HS) {
+        if (l < HS) Xm[l * HS + m] = v;
+        else if (l == HS) sumD[m] = v;                  // sum_p Dsig (completed below)
+        else if (l == HS + 1) red[m] = v;               // sum_p Dtau
       }
-      if (p < Nc) a0 = fmaf(G[p * HS + l], Dsig[p * HS + k], fmaf(Hh[p * HS + l], Dtau[p * HS + k], a0));
-      Xm[e] = a0 + a1;
-    } else {
-      float dd1 = 0.f, dt = 0.f;
-      for (int p = 0; p < Nc; ++p) { dd1 += Dsig[p * HS + k]; dt += Dtau[p * HS + k]; }
-      sumD[k] = dd1 + dt;
-      const float dy1 = cvec[k] * ysumv[k];
-      pb[H2_B1 + k] = dd1;
-      pb[H2_W1 + HS + k] = dy1;
-      pb[H2_W1 + k] = dd1 - dy1;
+    }
+    __syncthreads();
+    if (t < HS) {
+      const float dd1 = sumD[t], dt = red[t];
+      const float dy1 = cvec[t] * ysumv[t];
+      pb[H2_B1 + t] = dd1;
+      pb[H2_W1 + HS + t] = dy1;
+      pb[H2_W1 + t] = dd1 - dy1;
+      sumD[t] = dd1 + dt;
     }
   }
   __syncthreads();
@@ -1122,18 +1321,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   float* dG = G;       // G, H dead once X is formed
   float* dH = Hh;
-  if (msl < NSL) {     // dG_p[l] = sum_k M[l][k] Dsig_p[k]
-    float w[HS];
+  for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {   // dG = Dsig M^T, dH = Dtau M^T
+    const int which = tile & 1, row0 = (tile >> 2) * 16, col0 = ((tile >> 1) & 1) * 16;
+    const float* src = which ? Dtau : Dsig;
+    const f4v c = mfma_tile16(
+        [&](int r, int k) { const int p = row0 + r; return (p < Nc && k < HS) ? src[p * HS + k] : 0.f; },
+        [&](int k, int j) { const int l = col0 + j; return (k < HS && l < HS) ? Mm[l * HS + k] : 0.f; },
+        HS, lane);
+    const int l = col0 + (lane & 15);
+    if (l < HS) {
+      float* dst = which ? dH : dG;
 #pragma unroll
-    for (int k = 0; k < HS; ++k) w[k] = Mm[mk * HS + k];
-    for (int p = msl; p < NC16; p += NSL) {
-      float ag = 0.f, ah = 0.f;
-      if (p < Nc) {
-        ag = dot20(Dsig + p * HS, w, 0.f);
-        ah = dot20(Dtau + p * HS, w, 0.f);
-      }
-      dG[p * HS + mk] = ag;
-      dH[p * HS + mk] = ah;
+      for (int q = 0; q < 4; ++q) dst[(row0 + 4 * (lane >> 4) + q) * HS + l] = c[q];
     }
   }
   __syncthreads();
@@ -1151,20 +1350,27 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  for (int e = t; e < 10 * HS; e += NT_MID) {       // dV1 rows 0..9, dc1
-    const int r = e / HS, k = e - r * HS;
-    float acc = 0.f;
-    if (r < 4) {
-      for (int p = 0; p < Nc; ++p) acc = fmaf(nb[4 * p + r], Dal[p * HS + k], acc);
-    } else if (r < 8) {
-      for (int p = 0; p < Nc; ++p) acc = fmaf(nb[4 * p + r - 4], Dbe[p * HS + k], acc);
-    } else {
-      float dc1 = 0.f;
-      for (int p = 0; p < Nc; ++p) dc1 += Dal[p * HS + k];
-      acc = (r == 9) ? ysumv[k] : dc1 - ysumv[k];
-      if (r == 8) pb[H1_B1 + k] = dc1;
+  if (wv < 4) {         // dV1 rows 0..7 and dc1: [n^T; 1] . Dalpha, n^T . Dbeta  (MFMA)
+    const int side = wv >> 1, col0 = (wv & 1) * 16;
+    const float* D = side ? Dbe : Dal;
+    const f4v c = mfma_tile16(
+        [&](int r, int p) {
+          return (p < Nc) ? (r < 4 ? nb[4 * p + r] : ((r == 4 && side == 0) ? 1.f : 0.f)) : 0.f;
+        },
+        [&](int p, int j) { const int m = col0 + j; return (p < Nc && m < HS) ? D[p * HS + m] : 0.f; },
+        Nc, lane);
+    const int m = col0 + (lane & 15);
+    if (m < HS) {
+      if (lane < 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pb[H1_W1 + (4 * side + q) * HS + m] = c[q];
+      } else if (lane < 32 && side == 0) {            // row 4: dc1 = sum_p Dalpha
+        const float dc1 = c[0];
+        pb[H1_B1 + m] = dc1;
+        pb[H1_W1 + 8 * HS + m] = dc1 - ysumv[m];
+        pb[H1_W1 + 9 * HS + m] = ysumv[m];
+      }
     }
-    pb[H1_W1 + e] = acc;
   }
   for (int e = t; e < NC16 * 2; e += NT_MID) {      // dn_c[m], m in {0,1} (x' components)
     const int c = e >> 1, m = e & 1;
@@ -1222,70 +1428,94 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const int i = e / HS, k = e - i * HS;
     dq[e] = (hE[e] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
   }
-  if (t >= NT_MID - 64) {                           // one wave: dw2' (20), db2' (1)
-    const int k = t - (NT_MID - 64);
-    if (k <= HS) {
-      float acc = 0.f;
-      if (k < HS) {
-        for (int i = 0; i < Ne; ++i) acc = fmaf(hE[i * HS + k], dxp[i], acc);
-        pb[E3_W2 + k] = acc;
-      } else {
-        for (int i = 0; i < Ne; ++i) acc += dxp[i];
-        pb[E3_B2] = acc;
-      }
-    }
+  for (int o = wv; o <= HS; o += NT_MID / 64) {     // dw2'[k] = sum_i h_ik do_i, db2' = sum do
+    float acc = 0.f;
+    for (int i = lane; i < Ne; i += 64) acc = fmaf(o < HS ? hE[i * HS + o] : 1.f, dxp[i], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) pb[(o < HS ? E3_W2 + o : E3_B2)] = acc;
   }
   __syncthreads();
   MID_STAMP();
-  for (int e = t; e < 22 * HS; e += NT_MID) {       // dW1' (21 rows) + db1'
-    const int r = e / HS, k = e - r * HS;
-    float a0 = 0.f, a1 = 0.f;
-    const float* src = (r == 0) ? xs : Eb + (r - 1);
-    const int sst = (r == 0) ? 1 : HS;
-    if (r <= HS) {
-      int i = 0;
-      for (; i + 1 < Ne; i += 2) {
-        a0 = fmaf(src[i * sst], dq[i * HS + k], a0);
-        a1 = fmaf(src[(i + 1) * sst], dq[(i + 1) * HS + k], a1);
-      }
-      if (i < Ne) a0 = fmaf(src[i * sst], dq[i * HS + k], a0);
-      pb[E3_W1 + r * HS + k] = a0 + a1;
-    } else {
-      for (int i = 0; i < Ne; ++i) a0 += dq[i * HS + k];
-      pb[E3_B1 + k] = a0;
-    }
-  }
-  if (msl < NSL) {      // dE_i[m] = sum_k W1'[1+m][k] dq_i[k]
-    float w[HS];
+  // dW1' = [x, E_bar, 1]^T dq (waves 0-3, K = Ne) | dE = dq W1'[1:]^T (waves 4-15)
+  if (wv < 4) {
+    const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
+    const f4v c = mfma_tile16(
+        [&](int r, int i) {
+          const int l = row0 + r;
+          if (i >= Ne) return 0.f;
+          return l == 0 ? xs[i] : (l <= HS ? Eb[i * HS + l - 1] : (l == HS + 1 ? 1.f : 0.f));
+        },
+        [&](int i, int j) { const int k = col0 + j; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
+        Ne, lane);
+    const int k = col0 + (lane & 15);
+    if (k < HS) {
 #pragma unroll
-    for (int k = 0; k < HS; ++k) w[k] = Ws[E3_W1 + (1 + mk) * HS + k];
-    for (int i = msl; i < Ne; i += NSL) dE[i * HS + mk] = dot20(dq + i * HS, w, 0.f);
+      for (int q = 0; q < 4; ++q) {
+        const int l = row0 + 4 * (lane >> 4) + q;
+        if (l <= HS) pb[E3_W1 + l * HS + k] = c[q];
+        else if (l == HS + 1) pb[E3_B1 + k] = c[q];
+      }
+    }
+  } else {
+    for (int tile = wv - 4; tile < 2 * ntm_e; tile += NT_MID / 64 - 4) {
+      const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k < HS && m < HS) ? Ws[E3_W1 + (1 + m) * HS + k] : 0.f;
+          }, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) dE[i * HS + m] = c[q];
+        }
+      }
+    }
   }
   __syncthreads();
   MID_STAMP();
   // ---- M13: agg_entity_B1 / mlp_entity_B1 second layer backward; rho = dL/dP ----------
+  //   dW5 = [P, 1]^T dE (waves 0-3; row 20 -> db5 / 2(Ne-1)) | rho = dE W5^T (waves 4-15)
   float* rho = Eb;      // E_bar dead after dW1'
-  for (int e = t; e < HS * HS + HS; e += NT_MID) {
-    const int m = e / HS, k = e - m * HS;
-    float a0 = 0.f, a1 = 0.f;
-    if (m < HS) {
-      int i = 0;
-      for (; i + 1 < Ne; i += 2) {
-        a0 = fmaf(Ps[i * HS + m], dE[i * HS + k], a0);
-        a1 = fmaf(Ps[(i + 1) * HS + m], dE[(i + 1) * HS + k], a1);
-      }
-      if (i < Ne) a0 = fmaf(Ps[i * HS + m], dE[i * HS + k], a0);
-      pb[E1_W5 + e] = a0 + a1;
-    } else {
-      for (int i = 0; i < Ne; ++i) a0 += dE[i * HS + k];
-      pb[E1_B5 + k] = twoNe1 * a0;
-    }
-  }
-  if (msl < NSL) {      // rho_i[m] = sum_k W5[m][k] dE_i[k]
-    float w[HS];
+  if (wv < 4) {
+    const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
+    const f4v c = mfma_tile16(
+        [&](int r, int i) {
+          const int l = row0 + r;
+          return i < Ne ? (l < HS ? Ps[i * HS + l] : (l == HS ? 1.f : 0.f)) : 0.f;
+        },
+        [&](int i, int j) { const int k = col0 + j; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
+        Ne, lane);
+    const int k = col0 + (lane & 15);
+    if (k < HS) {
 #pragma unroll
-    for (int k = 0; k < HS; ++k) w[k] = Ws[E1_W5 + mk * HS + k];
-    for (int i = msl; i < Ne; i += NSL) rho[i * HS + mk] = dot20(dE + i * HS, w, 0.f);
+      for (int q = 0; q < 4; ++q) {
+        const int l = row0 + 4 * (lane >> 4) + q;
+        if (l < HS) pb[E1_W5 + l * HS + k] = c[q];
+        else if (l == HS) pb[E1_B5 + k] = twoNe1 * c[q];
+      }
+    }
+  } else {
+    for (int tile = wv - 4; tile < 2 * ntm_e; tile += NT_MID / 64 - 4) {
+      const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k < HS && m < HS) ? Ws[E1_W5 + m * HS + k] : 0.f;
+          }, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) rho[i * HS + m] = c[q];
+        }
+      }
+    }
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 4) pb[NP + 1 + t] = 0.f;                  // trailer / pad
@@ -1359,30 +1589,88 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 }
 
 // ------------------------------------------------------------------------------
-// deterministic reduction of per-commit partial rows (fixed commit order per lane,
-// fixed 4-way combine): block = 64 parameters x 4 commit phases
+// deterministic reduction of per-commit partial rows: a 1024-thread block takes 64
+// parameters x 16 commit phases (commit b -> phase b % 16, fixed order), then a fixed
+// 16-way combine.  Bitwise reproducible.
 // ------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_grad_reduce(const float* __restrict__ part, int B,
-                                                     int p_begin, int p_end,
-                                                     float* __restrict__ out) {
-  __shared__ float sh[4][64];
+constexpr int RED_PH = 16;
+
+__device__ __forceinline__ float reduce_commits(const float* __restrict__ part, int B, int p,
+                                                bool valid, float (*sh)[64]) {
   const int pl = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int p = p_begin + blockIdx.x * 64 + pl;
   float acc = 0.f;
-  if (p < p_end) {
+  if (valid) {
     int b = ph;
-    for (; b + 12 < B; b += 16) {
+    for (; b + 3 * RED_PH < B; b += 4 * RED_PH) {
       const float v0 = part[(size_t)b * NPART + p];
-      const float v1 = part[(size_t)(b + 4) * NPART + p];
-      const float v2 = part[(size_t)(b + 8) * NPART + p];
-      const float v3 = part[(size_t)(b + 12) * NPART + p];
+      const float v1 = part[(size_t)(b + RED_PH) * NPART + p];
+      const float v2 = part[(size_t)(b + 2 * RED_PH) * NPART + p];
+      const float v3 = part[(size_t)(b + 3 * RED_PH) * NPART + p];
       acc += v0; acc += v1; acc += v2; acc += v3;
     }
-    for (; b < B; b += 4) acc += part[(size_t)b * NPART + p];
+    for (; b < B; b += RED_PH) acc += part[(size_t)b * NPART + p];
   }
   sh[ph][pl] = acc;
   __syncthreads();
-  if (ph == 0 && p < p_end) out[p - p_begin] = (sh[0][pl] + sh[1][pl]) + (sh[2][pl] + sh[3][pl]);
+  float g = 0.f;
+  if (ph == 0) {
+#pragma unroll
+    for (int q = 0; q < RED_PH; ++q) g += sh[q][pl];
+  }
+  return g;
+}
+
+__global__ __launch_bounds__(1024) void k_grad_reduce(const float* __restrict__ part, int B,
+                                                      int p_begin, int p_end,
+                                                      float* __restrict__ out) {
+  __shared__ float sh[RED_PH][64];
+  const int p = p_begin + blockIdx.x * 64 + (threadIdx.x & 63);
+  const float g = reduce_commits(part, B, p, p < p_end, sh);
+  if ((threadIdx.x >> 6) == 0 && p < p_end) out[p - p_begin] = g;
+}
+
+// Single-process training step tail: the reduction above fused with TF1 Adam for the
+// block's 64 parameters.  aux (written by block 0 of k_commit_step from the pre-update
+// parameters): [lpara, lmap, |theta1|, |theta2|, sqrt(1-b2^t)/(1-b1^t), b1^(t+1),
+// b2^(t+1)], so no block here depends on another.
+__global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ part, int B,
+                                                      float* __restrict__ params,
+                                                      float* __restrict__ mm,
+                                                      float* __restrict__ vv,
+                                                      float* __restrict__ bpow,
+                                                      const float* __restrict__ aux, float lr,
+                                                      float inv_pairs, float* __restrict__ stats,
+                                                      float* __restrict__ grad) {
+  using namespace m2;
+  __shared__ float sh[RED_PH][64];
+  const int p = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh);
+  if ((threadIdx.x >> 6) != 0) return;
+  if (p < GRAD_LEN) grad[p] = g;
+  if (p == NP) {
+    const float ce = g * inv_pairs;
+    if (stats) {
+      stats[0] = ce;
+      stats[1] = aux[1];
+      stats[2] = aux[0];
+      stats[3] = 10.f * ce + 0.1f * aux[1] + aux[0];
+    }
+  }
+  if (p < NP) {
+    const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
+    const float lr_t = lr * aux[4];
+    const float w = params[p];
+    float gg = g + 0.001f * w;
+    if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / aux[2];
+    if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / aux[3];
+    float m = mm[p], v = vv[p];
+    m += (gg - m) * (1.f - b1);
+    v += (gg * gg - v) * (1.f - b2);
+    mm[p] = m;
+    vv[p] = v;
+    params[p] = w - lr_t * m / (sqrtf(v) + ep);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) { bpow[0] = aux[5]; bpow[1] = aux[6]; }
 }
 
 // ------------------------------------------------------------------------------
@@ -1467,7 +1755,7 @@ int fail(int code, const char* fmt, ...) {
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
 
 struct Work {   // workspace carve (floats)
-  size_t Esave, rowq, gam, part, total;
+  size_t Esave, rowq, gam, part, aux, total;
 };
 
 Work work_layout(const hdg_shape* s) {
@@ -1480,6 +1768,7 @@ Work work_layout(const hdg_shape* s) {
   w.rowq = take((B * Ne * HS + 1) / 2);     // u16
   w.gam = take(B * NC16 * NC16);
   w.part = take(B * (size_t)NPART);
+  w.aux = take(8);
   w.total = o;
   return w;
 }
@@ -1520,7 +1809,7 @@ int check_batch(const hdg_batch* bt) {
 template <int SMAXC, bool TRAIN, bool STAMPS>
 hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                        const Work& w, float* probs, float* logits, float ce_scale,
-                       unsigned long long* stamps, hipStream_t st) {
+                       unsigned long long* stamps, const float* bpow, hipStream_t st) {
   const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
   const size_t lds = (size_t)L.total * 4;
   static bool attr_set = false;   // the attribute is per function; 160 KiB covers every shape
@@ -1533,18 +1822,18 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
   hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS>), dim3(s->batch), dim3(NT_MID), lds, st,
                      bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params, ws + w.Esave,
                      (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, probs, logits, s->ne,
-                     s->nc, ce_scale, stamps);
+                     s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow);
   return hipGetLastError();
 }
 
 template <bool TRAIN, bool STAMPS = false>
 hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                          const Work& w, float* probs, float* logits, float ce_scale,
-                         unsigned long long* stamps, hipStream_t st) {
+                         unsigned long long* stamps, hipStream_t st, const float* bpow = nullptr) {
   switch (smax_c(s->nc)) {
-    case 5: return launch_step<5, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
-    case 8: return launch_step<8, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
-    default: return launch_step<10, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, st);
+    case 5: return launch_step<5, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
+    case 8: return launch_step<8, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
+    default: return launch_step<10, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
   }
 }
 
@@ -1606,7 +1895,7 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
   HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
                               out ? out->logits : nullptr, ce_scale, nullptr, st));
   HIP_TRY(mark(1));
-  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st,
                      ws + w.part, s->batch, 0, GRAD_LEN, grad);
   HIP_TRY(hipGetLastError());
   HIP_TRY(mark(2));
@@ -1646,9 +1935,26 @@ int hdg_adam_tf(const hdg_shape* s, hdg_state* state, const float* grad, float l
 
 int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, float lr,
                    hdg_outputs* out, float* grad, void* workspace, void* stream) {
-  if (!state) return fail(HDG_EINVAL, "NULL state");
-  if (int rc = hdg_fwd_bwd(s, bt, state->params, grad, out, workspace, stream)) return rc;
-  return hdg_adam_tf(s, state, grad, lr, out ? out->stats : nullptr, stream);
+  // single process: k_commit_step (+ loss stats / Adam factor from block 0) then the
+  // fused deterministic reduction + TF Adam; no all-reduce point in between
+  if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow)
+    return fail(HDG_EINVAL, "NULL state pointer");
+  if (int rc = check_shape(s)) return rc;
+  if (int rc = check_batch(bt)) return rc;
+  if (!grad || !workspace) return fail(HDG_EINVAL, "NULL grad/workspace");
+  hipStream_t st = (hipStream_t)stream;
+  const Work w = work_layout(s);
+  float* ws = (float*)workspace;
+  const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
+  const float pairs = (float)bg * (float)(s->nc * (s->nc - 1));
+  HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, out ? out->probs : nullptr,
+                              out ? out->logits : nullptr, 10.f / pairs, nullptr, st,
+                              state->beta_pow));
+  hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st, ws + w.part,
+                     s->batch, state->params, state->adam_m, state->adam_v, state->beta_pow,
+                     ws + w.aux, lr, 1.f / pairs, out ? out->stats : nullptr, grad);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hdg_outputs* out,
@@ -1662,7 +1968,7 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
   HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, out ? out->probs : nullptr,
                                out ? out->logits : nullptr, 0.f, nullptr, st));
   if (ce_sum) {
-    hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(256), 0, st, ws + w.part, s->batch, m2::NP,
+    hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part, s->batch, m2::NP,
                        m2::NP + 1, ce_sum);
     HIP_TRY(hipGetLastError());
   }

@@ -10,7 +10,7 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
   constexpr int SMAXC = 5, NC16 = 80;
   __shared__ __attribute__((aligned(16))) float A[NC16 * HS], B[NC16 * HS], R[NC16 * HS],
-      C[NC16 * HS], wr[NC16 * HS], wc[NC16 * HS], dl[HS], ys[HS], zs[HS];
+      C[NC16 * HS], wr[NC16 * HS], wc[NC16 * HS], dl[HS], ys[HS];
   __shared__ __attribute__((aligned(16))) float cred[4 * tile_cred_words<SMAXC, 5>()];
   __shared__ uint32_t bits[NC16 * 3];
   __shared__ float gam[NC16 * NC16];
@@ -29,34 +29,9 @@ __global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
   __syncthreads();
   const int g = t >> 8, tg = t & 255;
   for (int it = 0; it < iters; ++it)
-    pair_tile<5, SMAXC, MODE, HS>(N, tg, A, B, g * 5, dl, bits, 3, wr, wc, gam, NC16, R, C, ys, zs,
+    pair_tile<5, SMAXC, MODE, HS>(N, tg, A, B, g * 5, dl, bits, 3, wr, wc, gam, NC16, R, C, ys,
                                   cred + g * tile_cred_words<SMAXC, 5>());
   if (t == 0) out[blockIdx.x] = R[7] + C[11] + ys[3];
-}
-
-template <int VW>
-__global__ __launch_bounds__(1024) void mb_sweep(int N, int iters, float* out) {
-  __shared__ __attribute__((aligned(16))) float xv[256], R[256 * VW], C[256 * VW],
-      scr[sweep_scratch_words(16, VW, 4)];
-  __shared__ uint32_t ab[256 * 8];
-  const int t = threadIdx.x;
-  for (int e = t; e < 256; e += 1024) xv[e] = (float)(e % 17) * 0.1f;
-  for (int e = t; e < 256 * 8; e += 1024) ab[e] = e * 2654435761u;
-  __syncthreads();
-  const int Ne1 = N - 1, n1 = N - 3;
-  const float invNe1 = 1.f / (float)Ne1;
-  for (int it = 0; it < iters; ++it)
-    grid_sweep<VW, 16, 4>(N - 2, t, [&](int ip, int jp, float* v) {
-      const int r = __mul24(ip, n1) + jp - (jp > ip ? 1 : 0);
-      int I, jj;
-      divmod_bf(r < 0 ? 0 : r, Ne1, invNe1, I, jj);
-      const int J = jj + (jj >= I ? 1 : 0);
-      const float a = (float)((ab[__mul24(I, 7) + (J >> 5)] >> (J & 31)) & 1u);
-      v[0] = xv[I];
-      v[1] = xv[J];
-      if constexpr (VW > 2) { v[2] = 1.f - a; v[3] = a; }
-    }, R, C, scr);
-  if (t == 0) out[blockIdx.x] = R[5] + C[9];
 }
 
 }  // namespace
@@ -87,9 +62,6 @@ int main() {
   printf("  MODE0 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<0>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE1 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<1>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE2 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<2>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
-  printf("grid_sweep n=198 on Ne=200 (per call):\n");
-  printf("  VW4   %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_sweep<4>, dim3(nb), dim3(1024), 0, 0, 200, it, out); }, B, IT));
-  printf("  VW2   %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_sweep<2>, dim3(nb), dim3(1024), 0, 0, 200, it, out); }, B, IT));
   CK(hipDeviceSynchronize());
   return 0;
 }

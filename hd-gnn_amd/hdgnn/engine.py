@@ -80,9 +80,7 @@ class Engine:
                                         self._stream()))
 
     def allreduce(self):
-        if self.pg is not None or (torch.distributed.is_available()
-                                   and torch.distributed.is_initialized()
-                                   and torch.distributed.get_world_size() > 1):
+        if self._distributed():
             torch.distributed.all_reduce(self.grad, group=self.pg)
 
     def adam(self):
@@ -91,12 +89,30 @@ class Engine:
                                         ctypes.c_float(self.lr),
                                         ctypes.c_void_p(self.stats.data_ptr()), self._stream()))
 
+    def _distributed(self):
+        return self.pg is not None or (torch.distributed.is_available()
+                                       and torch.distributed.is_initialized()
+                                       and torch.distributed.get_world_size() > 1)
+
     def train_step(self, dbatch, outputs=True):
         """sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer]) equivalent:
-        outputs land in self.probs / self.stats (pre-update), params updated in place."""
-        self.fwd_bwd(dbatch, outputs)
-        self.allreduce()
-        self.adam()
+        outputs land in self.probs / self.stats (pre-update), params updated in place.
+        Single process: hdg_train_step (step kernel + fused reduce/Adam).  Data parallel:
+        hdg_fwd_bwd -> all-reduce of the flat gradient -> hdg_adam_tf."""
+        if self._distributed():
+            self.fwd_bwd(dbatch, outputs)
+            self.allreduce()
+            self.adam()
+            return
+        assert dbatch.B == self.batch and dbatch.Ne == self.ne and dbatch.Nc == self.nc
+        b = dbatch.struct()
+        out = self._out if outputs else None
+        _lib.check(self.lib.hdg_train_step(ctypes.byref(self.shape), ctypes.byref(b),
+                                           ctypes.byref(self._state), ctypes.c_float(self.lr),
+                                           ctypes.byref(out) if out is not None else None,
+                                           ctypes.c_void_p(self.grad.data_ptr()),
+                                           ctypes.c_void_p(self.workspace.data_ptr()),
+                                           self._stream()))
 
     # ---- HIP graph of one training step ----------------------------------------
     def capture(self, dbatch, outputs=True):
