@@ -289,60 +289,31 @@ __device__ __forceinline__ T wave_incl_scan(T v, int lane) {
   return v;
 }
 
-// A bit row of nw <= 8 words in registers with prefix popcounts, for rank-select:
-// the lanes of a node group each pick a DIFFERENT set bit (lane r -> r-th neighbour),
-// so neighbour extraction costs O(1) per neighbour instead of per (neighbour, lane).
-struct BitRow {
-  uint32_t rw[8];
-  int pre[9];          // pre[q] = set bits in words < q; pre[8] = degree
-  __device__ __forceinline__ void init(const uint32_t* row, int nw) {
-    pre[0] = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      rw[q] = q < nw ? row[q] : 0u;
-      pre[q + 1] = pre[q] + __builtin_popcount(rw[q]);
-    }
-  }
-  __device__ __forceinline__ int degree() const { return pre[8]; }
-  // column index of the r-th set bit (0 <= r < degree())
-  __device__ __forceinline__ int select(int r) const {
-    int w = 0;
-#pragma unroll
-    for (int q = 1; q < 8; ++q) w += (pre[q] <= r) ? 1 : 0;
-    uint32_t m = 0u;
-    int base = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      m = (w == q) ? rw[q] : m;
-      base = (w == q) ? pre[q] : base;
-    }
-    int rr = r - base, pos = 0;
-#pragma unroll
-    for (int width = 16; width > 0; width >>= 1) {
-      const int c = __builtin_popcount(m & ((1u << width) - 1u));
-      const bool up = rr >= c;
-      rr = up ? rr - c : rr;
-      m = up ? m >> width : m;
-      pos = up ? pos + width : pos;
-    }
-    return 32 * w + pos;
-  }
-};
-
-// For every neighbour j of the node owned by this lane's group (GL lanes starting at
-// lane gbase) call f(j, x_j).  Lane r of the group rank-selects neighbour c0+r and
-// loads its x once; the group reads (j, x_j) back with ds_bpermute (LDS pipe, not
-// VALU).  All lanes of a group share the trip count, so bpermute sources are active.
-template <int GL, class F>
-__device__ __forceinline__ void for_each_nbr(const BitRow& row, const int gbase, const int r,
-                                             const float* xs, F f) {
-  const int d = row.degree();
+// For every neighbour j in list[0..d) of the node owned by this lane's group (GL lanes
+// starting at lane gbase) call f(j, x_j).  Lane r of the group loads neighbour c0+r and
+// its x once; the group reads (j, x_j) back with ds_bpermute (LDS pipe, not VALU), four
+// neighbours per trip so their bpermutes are in flight together.  All lanes of a group
+// share the trip count, so bpermute sources are active.  list may point to LDS or HBM.
+template <int GL, bool NEED_J, class F>
+__device__ __forceinline__ void for_each_nbr(const uint8_t* list, const int d, const int gbase,
+                                             const int r, const float* xs, F f) {
   for (int c0 = 0; c0 < d; c0 += GL) {
-    const int jl = (c0 + r < d) ? row.select(c0 + r) : 0;
+    const int jl = (c0 + r < d) ? (int)list[c0 + r] : 0;
     const float xl = xs[jl];
     const int nn = (d - c0 < GL) ? d - c0 : GL;
-#pragma unroll 2
-    for (int n = 0; n < nn; ++n) f(__shfl(jl, gbase + n), __shfl(xl, gbase + n));
+    int n = 0;
+    for (; n + 4 <= nn; n += 4) {
+      float x[4];
+      int j[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        x[q] = __shfl(xl, gbase + n + q);
+        j[q] = NEED_J ? __shfl(jl, gbase + n + q) : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f(j[q], x[q]);
+    }
+    for (; n < nn; ++n) f(NEED_J ? __shfl(jl, gbase + n) : 0, __shfl(xl, gbase + n));
   }
 }
 
@@ -360,12 +331,13 @@ __device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n 
 //   xsrt[NE4]    x sorted ascending            perm[NE4]  node at sorted slot m
 //   xu[NE4]      the nd distinct x values      cum[NE4+4] cum[q] = #nodes with x < xu[q]
 //   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
-//   atb[Ne*WE]   transposed entity class bits (bit i of row j = a_ij)
+//   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
+//   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // ------------------------------------------------------------------------------
 struct PrepLayout {
-  int xsrt, perm, xu, cum, pxd, meta, atb, ks, kt, ncst, words;
+  int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, words;
 };
 
 __host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
@@ -378,12 +350,15 @@ __host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
   L.xu = o;   o += NE4;
   L.cum = o;  o += NE4 + 4;
   L.pxd = o;  o += 2 * (NE4 + 4);     // even word offset: 8-byte aligned
-  L.meta = o; o += 4;
-  L.atb = o;  o += (Ne * WE + 3) & ~3;
+  L.meta = o; o += 4;                 // nd, nnz_r, nnz_c, byte offset of the column lists
+  L.offr = o; o += NE4 + 4;           // CSR row offsets (a_ij = 1, j != i)
+  L.offc = o; o += NE4 + 4;           // CSR column offsets (a_ji = 1)
   L.ks = o;   o += kw;
   L.kt = o;   o += kw;
   L.ncst = o; o += (2 * Nc + 3) & ~3;
+  L.lists = o; o += (2 * Ne * (Ne - 1) + 4 + 3) / 4;   // u8 neighbour ids: rows | columns
   L.words = (o + 63) & ~63;
+  (void)WE;
   return L;
 }
 
@@ -405,6 +380,8 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
   if (t < Ne) xl[t] = x[(size_t)b * Ne + t];
   for (int w = t; w < Ne * WE; w += 256) al[w] = abits[(size_t)b * Ne * WE + w];
   __syncthreads();
+  if (t < Ne) al[t * WE + (t >> 5)] &= ~(1u << (t & 31));      // a_ii is not a relation
+  __syncthreads();
   if (t < Ne) {
     const float xi = xl[t];
     int r = 0;
@@ -416,14 +393,55 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
     xsrt[r] = xi;
     perm[r] = t;
   }
-  for (int e = t; e < Ne * WE; e += 256) {
+  __shared__ uint32_t atl[256 * 8];
+  __shared__ int offl[2][260];
+  for (int e = t; e < Ne * WE; e += 256) {          // a^T bits
     const int j = e / WE, w = e - j * WE;
     uint32_t bits = 0;
     for (int l = 0; l < 32; ++l) {
       const int i = 32 * w + l;
       if (i < Ne) bits |= ((al[i * WE + (j >> 5)] >> (j & 31)) & 1u) << l;
     }
-    pb[L.atb + e] = bits;
+    atl[e] = bits;
+  }
+  __syncthreads();
+  if (t < Ne) {
+    int dr = 0, dc = 0;
+    for (int w = 0; w < WE; ++w) {
+      dr += __builtin_popcount(al[t * WE + w]);
+      dc += __builtin_popcount(atl[t * WE + w]);
+    }
+    offl[0][t] = dr;
+    offl[1][t] = dc;
+  }
+  __syncthreads();
+  if (t < 2) {                                       // serial exclusive scans, once per batch
+    int acc = 0;
+    for (int i = 0; i < Ne; ++i) {
+      const int d = offl[t][i];
+      offl[t][i] = acc;
+      ((int*)(pb + (t ? L.offc : L.offr)))[i] = acc;
+      acc += d;
+    }
+    offl[t][Ne] = acc;
+    ((int*)(pb + (t ? L.offc : L.offr)))[Ne] = acc;
+  }
+  __syncthreads();
+  const int cbase = (offl[0][Ne] + 3) & ~3;
+  if (t == 0) {
+    pb[L.meta + 1] = (uint32_t)offl[0][Ne];
+    pb[L.meta + 2] = (uint32_t)offl[1][Ne];
+    pb[L.meta + 3] = (uint32_t)cbase;
+  }
+  if (t < Ne) {
+    uint8_t* lb = reinterpret_cast<uint8_t*>(pb + L.lists);
+    int nr = offl[0][t], nc2 = cbase + offl[1][t];
+    for (int w = 0; w < WE; ++w) {
+      uint32_t m = al[t * WE + w];
+      while (m) { lb[nr++] = (uint8_t)(32 * w + __builtin_ctz(m)); m &= m - 1u; }
+      m = atl[t * WE + w];
+      while (m) { lb[nc2++] = (uint8_t)(32 * w + __builtin_ctz(m)); m &= m - 1u; }
+    }
   }
   __syncthreads();
   if (t == 0) {   // serial over <= 256 sorted values, once per batch
@@ -520,8 +538,8 @@ __host__ __device__ constexpr int nbuf_h(int smaxc) { return smaxc <= 8 ? 7 : 6;
 constexpr int NSL = NT_MID / HS;                // 51 node slices for (k, slice) matvecs
 
 struct StepLayout {   // offsets in 4-byte words into the dynamic LDS arena
-  int W, xs, xps, os, dxp, xsrt, perm, xu, cum, pxd, yb, nb, dnb, misc, u2, Mm, Xm, red, U,
-      Uwords, total;
+  int W, xs, xps, os, dxp, xsrt, perm, xu, cum, pxd, offr, offc, yb, nb, dnb, misc, u2, Mm, Xm,
+      red, U, Uwords, total;
 };
 
 __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
@@ -541,6 +559,8 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.xu = o;   o += NE4;
   L.cum = o;  o += NE4 + 4;
   L.pxd = o;  o += 2 * (NE4 + 4);     // f64 (offset is a multiple of 4 words)
+  L.offr = o; o += NE4 + 4;           // CSR offsets of the entity neighbour lists
+  L.offc = o; o += NE4 + 4;
   L.yb = o;   o += (Nc * WC + 3) & ~3;
   L.nb = o;   o += 4 * NC16;
   L.dnb = o;  o += 2 * NC16;
@@ -549,8 +569,7 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.Mm = o;   o += HS * HS;           // V2 . U1e
   L.Xm = o;   o += HS * HS;           // sum_p G_p (x) Dsig_p + H_p (x) Dtau_p
   L.red = o;  o += (NT_MID / 64) * 32;
-  const int bw = (Ne * WE + 3) & ~3;
-  int u = 3 * NE4 * HS + 2 * bw;                                   // entity fwd
+  int u = 3 * NE4 * HS;                                            // P | E_bar | h
   const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred;        // hunk phases
   int ueb = 5 * NE4 * HS;                                          // E3 bwd
   const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2
@@ -636,8 +655,9 @@ template <int ABL = 0>
 __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const float* Ws,
                                            const float* xs, const float* xu, const int* cum,
                                            const double* pxd, const int nd,
-                                           const uint32_t* abL, const uint32_t* atL,
-                                           const int WE, const int Ne, float* Ps,
+                                           const int* offr, const int* offc,
+                                           const uint8_t* lr, const uint8_t* lc,
+                                           const int Ne, float* Ps,
                                            float* __restrict__ EG, uint16_t* __restrict__ rq) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
@@ -677,22 +697,26 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
         tot[h] = acc;
       }
     }
+    // a = 1 corrections relu(z0 + d) - relu(z0) = med3(s z0 + t, 0, d) with (s, t) =
+    // (1, d) for d >= 0 and (-1, 0) for d < 0: one packed fma + two v_med3 per
+    // neighbour and hidden-unit pair (value within an ulp of the two-relu form)
     f2 sp = {0.f, 0.f};
-    const int wl = live ? WE : 0;
+    const f2 sg = {dd.x >= 0.f ? 1.f : -1.f, dd.y >= 0.f ? 1.f : -1.f};
+    const f2 tg = {dd.x >= 0.f ? dd.x : 0.f, dd.y >= 0.f ? dd.y : 0.f};
     {
-      BitRow row;
-      row.init(abL + ic * WE, (ABL & 4) ? 0 : wl);
-      for_each_nbr<EG_L>(row, sub * EG_L, kp, xs, [&](int, float xj) {
-        const f2 z0 = u + xj * w1;
-        sp += relu2(z0 + dd) - relu2(z0);
+      const f2 bw = sg * w1, aa = __builtin_elementwise_fma(sg, u, tg);
+      const int d = ((ABL & 4) || !live) ? 0 : offr[ic + 1] - offr[ic];
+      for_each_nbr<EG_L, false>(lr + offr[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
+        const f2 zz = __builtin_elementwise_fma((f2){xj, xj}, bw, aa);
+        sp += (f2){__builtin_amdgcn_fmed3f(zz.x, 0.f, dd.x), __builtin_amdgcn_fmed3f(zz.y, 0.f, dd.y)};
       });
     }
     {
-      BitRow col;
-      col.init(atL + ic * WE, (ABL & 8) ? 0 : wl);
-      for_each_nbr<EG_L>(col, sub * EG_L, kp, xs, [&](int, float xj) {
-        const f2 z0 = __builtin_elementwise_fma((f2){xj, xj}, w0, c0) + v;
-        sp += relu2(z0 + dd) - relu2(z0);
+      const f2 bw = sg * w0, aa = __builtin_elementwise_fma(sg, c0 + v, tg);
+      const int d = ((ABL & 8) || !live) ? 0 : offc[ic + 1] - offc[ic];
+      for_each_nbr<EG_L, false>(lc + offc[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
+        const f2 zz = __builtin_elementwise_fma((f2){xj, xj}, bw, aa);
+        sp += (f2){__builtin_amdgcn_fmed3f(zz.x, 0.f, dd.x), __builtin_amdgcn_fmed3f(zz.y, 0.f, dd.y)};
       });
     }
     if (live && kp < EG_L) {
@@ -711,7 +735,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
                                            const float* xs, const int* cum, const double* pxd,
                                            const int nd, const uint16_t* __restrict__ rq,
                                            const float* rho, const float* Tr, const float* Tx,
-                                           const int TL, const uint32_t* abE, const int WE,
+                                           const int TL, const int* offr, const uint8_t* lr,
                                            const int Ne, float* red2) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
@@ -748,9 +772,9 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       s1[h] = a1;
       s2[h] = rs;
     }
-    BitRow row;
-    row.init(abE + ic * WE, live ? WE : 0);
-    for_each_nbr<EG_L>(row, sub * EG_L, kp, xs, [&](int j, float xj) {
+    f2 sd = {0.f, 0.f}, sx = sd;                     // sum dm, sum x_j dm
+    const int d = live ? offr[ic + 1] - offr[ic] : 0;
+    for_each_nbr<EG_L, true>(lr + offr[ic], d, sub * EG_L, kp, xs, [&](int j, float xj) {
       const f2 rj = *reinterpret_cast<const f2*>(rho + j * HS + k0);
       const f2 z0 = u + xj * w1;
       const f2 z1 = z0 + dd;
@@ -758,11 +782,13 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       const f2 m1g = {z1.x > 0.f ? gs.x : 0.f, z1.y > 0.f ? gs.y : 0.f};
       const f2 m0g = {z0.x > 0.f ? gs.x : 0.f, z0.y > 0.f ? gs.y : 0.f};
       const f2 dm = m1g - m0g;
-      s0 = __builtin_elementwise_fma((f2){xi, xi}, dm, s0);
-      s1 = __builtin_elementwise_fma((f2){xj, xj}, dm, s1);
-      s2 += dm;
+      sd += dm;
+      sx = __builtin_elementwise_fma((f2){xj, xj}, dm, sx);
       s3 += m1g;
     });
+    s0 = __builtin_elementwise_fma((f2){xi, xi}, sd, s0);
+    s1 += sx;
+    s2 += sd;
     if (live) { S0 += s0; S1 += s1; S2 += s2; S3 += s3; }
   }
   // fold the 6 node groups (lanes kp + 10 s), then lanes 0..9 write the wave's sums
@@ -836,6 +862,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* xu = lds + L.xu;
   int* cum = (int*)(lds + L.cum);
   double* pxd = (double*)(lds + L.pxd);
+  int* offr = (int*)(lds + L.offr);
+  int* offc = (int*)(lds + L.offc);
   uint32_t* yb = (uint32_t*)(lds + L.yb);
   float* nb = lds + L.nb;
   float* dnb = lds + L.dnb;
@@ -866,8 +894,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Ps = U;
   float* Eb = U + NE4 * HS;
   float* hE = U + 2 * NE4 * HS;
-  uint32_t* abL = (uint32_t*)(U + 3 * NE4 * HS);
-  uint32_t* atL = abL + ((Ne * WE + 3) & ~3);
+  // neighbour lists (u8 ids, rows | columns): staged behind P when they fit, else read
+  // from the prepared buffer in HBM through the same (generic) pointer
+  const int nnz_r = (int)pp[PL.meta + 1], nnz_c = (int)pp[PL.meta + 2];
+  const int cbase = (int)pp[PL.meta + 3];
+  const int lwords = (cbase + nnz_c + 3) >> 2;
+  const bool lfit = lwords <= L.Uwords - NE4 * HS;
+  const uint8_t* lrow = lfit ? reinterpret_cast<const uint8_t*>(U + NE4 * HS)
+                             : reinterpret_cast<const uint8_t*>(pp + PL.lists);
   float l2 = 0.f;
   for (int i = t; i < NP; i += NT_MID) {
     const float w = Wg[i];
@@ -888,10 +922,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     cum[q] = reinterpret_cast<const int*>(pp + PL.cum)[q];
     pxd[q] = reinterpret_cast<const double*>(pp + PL.pxd)[q];
   }
-  for (int w = t; w < Ne * WE; w += NT_MID) {
-    abL[w] = abits[(size_t)b * Ne * WE + w];
-    atL[w] = pp[PL.atb + w];
+  for (int i = t; i <= Ne; i += NT_MID) {
+    offr[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
+    offc[i] = reinterpret_cast<const int*>(pp + PL.offc)[i];
   }
+  if (lfit)
+    for (int w = t; w < lwords; w += NT_MID) U[NE4 * HS + w] = __builtin_bit_cast(float, pp[PL.lists + w]);
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   __syncthreads();
   if (aux && b == 0 && t == 0) {           // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
@@ -919,7 +955,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   i of a and of a^T); the diagonal is removed once.  Lane map: a wave takes 3 nodes,
   //   lane = (node sub, hidden unit k), so the 20 lanes of a node walk its bits together.
   //   The row-set boundaries are kept for the backward.
-  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, abL, atL, WE, Ne, Ps, EG, rq);
+  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, lrow, lrow + cbase, Ne, Ps, EG, rq);
   __syncthreads();
   MID_STAMP();
 
@@ -1534,8 +1570,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Tr = hE;                          // [HS][TL]
   float* Tx = hE + HS * TL;                // [HS][TL]
   float* red2 = hE + 2 * HS * TL;          // [16 waves][4][HS]
-  uint32_t* abE = (uint32_t*)Ps;           // P dead after dW5
-  for (int w = t; w < Ne * WE; w += NT_MID) abE[w] = abits[(size_t)b * Ne * WE + w];
+  // row neighbour lists again, staged into the P slot (dead after dW5) when they fit
+  const bool rfit = ((nnz_r + 3) >> 2) <= NE4 * HS;
+  const uint8_t* lrow2 = rfit ? reinterpret_cast<const uint8_t*>(Ps)
+                              : reinterpret_cast<const uint8_t*>(pp + PL.lists);
+  if (rfit)
+    for (int w = t; w < ((nnz_r + 3) >> 2); w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
   for (int task = wv; task < 2 * HS; task += NT_MID / 64) {        // wave-uniform
     const int k = task >> 1, which = task & 1;
     const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
@@ -1567,7 +1607,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, abE, WE, Ne, red2);
+  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, lrow2, Ne, red2);
   __syncthreads();
   if (t < 4 * HS) {
     const int w = t / HS, k = t - w * HS;
