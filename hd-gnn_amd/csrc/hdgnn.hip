@@ -116,7 +116,7 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 template <int SMAX, int KK>
 constexpr int tile_cred_words() { return 4 * 16 * SMAX * KK + 8 * KK; }
 
-template <int KK, int SMAX, int MODE, int LD>
+template <int KK, int SMAX, int MODE, int LD, int ABL = 0>
 __device__ __forceinline__ void pair_tile(
     const int N, const int t, const float* A, const float* Bv, const int k0,
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
@@ -171,7 +171,7 @@ __device__ __forceinline__ void pair_tile(
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
-      const float af = (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
+      const float af = (ABL & 1) ? 0.f : (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
       const p2 af2 = {af, af};
       float g = 0.f;
       if constexpr (MODE == 2) {   // branch-free: clamped load, masked value
@@ -215,11 +215,16 @@ __device__ __forceinline__ void pair_tile(
     }
     float rs[KK];
 #pragma unroll
-    for (int p = 0; p < KP; ++p) {
-      rs[2 * p] = row16_sum(racc2[p].x);
-      rs[2 * p + 1] = row16_sum(racc2[p].y);
+    for (int p = 0; p < KP; ++p) {     // unpack first: DPP adds do not fuse on 64-bit halves
+      rs[2 * p] = racc2[p].x;
+      rs[2 * p + 1] = racc2[p].y;
     }
-    if constexpr (KT) rs[KK - 1] = row16_sum(racct);
+    if constexpr (KT) rs[KK - 1] = racct;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+      asm volatile("" : "+v"(rs[k]));
+      if constexpr (!(ABL & 2)) rs[k] = row16_sum(rs[k]);
+    }
     if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
 #pragma unroll
       for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = rs[k];
@@ -320,6 +325,23 @@ __device__ __forceinline__ void for_each_nbr(const uint8_t* list, const int d, c
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
 
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+
+// inclusive scan over the 64 lanes of a wave with DPP only (GFX9 row_shr + row_bcast):
+// no LDS round trips.  Lanes shifted in from outside a row read 0 (bound_ctrl).
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_in(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               RMASK, 0xF, true));
+}
+__device__ __forceinline__ float wave_incl_scan_dpp(float v) {
+  v += dpp_in<0x111, 0xF>(v);   // row_shr:1
+  v += dpp_in<0x112, 0xF>(v);   // row_shr:2
+  v += dpp_in<0x114, 0xF>(v);   // row_shr:4
+  v += dpp_in<0x118, 0xF>(v);   // row_shr:8
+  v += dpp_in<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+  v += dpp_in<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
+  return v;
+}
 
 __device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n (n >= 1)
   return 1 << (31 - __builtin_clz((unsigned)n));
@@ -571,8 +593,8 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.red = o;  o += (NT_MID / 64) * 32;
   int u = 3 * NE4 * HS;                                            // P | E_bar | h
   const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred;        // hunk phases
-  int ueb = 5 * NE4 * HS;                                          // E3 bwd
-  const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2
+  int ueb = 5 * NE4 * HS;                         // E3 bwd: P | E_bar | dq | dE | h/rho
+  const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2 + rho
   if (ue2 > ueb) ueb = ue2;
   if (uh > u) u = uh;
   if (ueb > u) u = ueb;
@@ -959,66 +981,66 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   __syncthreads();
   MID_STAMP();
 
-  // ---- M1: E_bar = P W5 + 2(Ne-1) b5   (agg_entity_B1, model_2.py:181-188) ----------
-  //   node GEMMs run as 16x16 MFMA tiles: (node block, column block) per wave
+  // ---- M1/M2: per 16-row block, one wave runs the row-local chain (MFMA tiles):
+  //   E_bar = P W5 + 2(Ne-1) b5          (agg_entity_B1, model_2.py:181-188)
+  //   h = relu([x, E_bar] W1' + b1')     (mlp2_entity_B1, model_2.py:190-205)
+  //   o = h w2' + b2',  x' = relu(o)
   const int ntm_e = (Ne + 15) >> 4;
-  for (int tile = wv; tile < 2 * ntm_e; tile += NT_MID / 64) {
-    const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
-    const f4v c = mfma_tile16(
-        [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? Ps[i * HS + k] : 0.f; },
-        [&](int k, int j) {
-          const int m = col0 + j;
-          return (k < HS && m < HS) ? Ws[E1_W5 + k * HS + m] : 0.f;
-        }, HS, lane);
-    const int m = col0 + (lane & 15);
-    if (m < HS) {
-      const float bias = twoNe1 * Ws[E1_B5 + m];
+  for (int rb = wv; rb < ntm_e; rb += NT_MID / 64) {          // wave-uniform
+    const int row0 = rb * 16;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = row0 + 4 * (lane >> 4) + q;
-        if (i < Ne) {
-          Eb[i * HS + m] = c[q] + bias;
-          EbG[i * HS + m] = c[q] + bias;
+    for (int cb = 0; cb < 2; ++cb) {
+      const int col0 = cb * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? Ps[i * HS + k] : 0.f; },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k < HS && m < HS) ? Ws[E1_W5 + k * HS + m] : 0.f;
+          }, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+        const float bias = twoNe1 * Ws[E1_B5 + m];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) {
+            Eb[i * HS + m] = c[q] + bias;
+            EbG[i * HS + m] = c[q] + bias;
+          }
         }
       }
     }
-  }
-  __syncthreads();
-  MID_STAMP();
-  // ---- M2: mlp2_entity_B1 (model_2.py:190-205): h = relu([x, E_bar] W1' + b1') -------
-  for (int tile = wv; tile < 2 * ntm_e; tile += NT_MID / 64) {
-    const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
-    const f4v c = mfma_tile16(
-        [&](int r, int k) {
-          const int i = row0 + r;
-          return (i < Ne && k <= HS) ? (k == 0 ? xs[i] : Eb[i * HS + k - 1]) : 0.f;
-        },
-        [&](int k, int j) {
-          const int m = col0 + j;
-          return (k <= HS && m < HS) ? Ws[E3_W1 + k * HS + m] : 0.f;
-        }, HS + 1, lane);
-    const int m = col0 + (lane & 15);
-    if (m < HS) {
-      const float bias = Ws[E3_B1 + m];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = row0 + 4 * (lane >> 4) + q;
-        if (i < Ne) {
-          const float v = reluf(c[q] + bias);
-          hE[i * HS + m] = v;
-          hEG[i * HS + m] = v;
+    for (int cb = 0; cb < 2; ++cb) {   // same wave: its E_bar rows are complete (LDS in order)
+      const int col0 = cb * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) {
+            const int i = row0 + r;
+            return (i < Ne && k <= HS) ? (k == 0 ? xs[i] : Eb[i * HS + k - 1]) : 0.f;
+          },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k <= HS && m < HS) ? Ws[E3_W1 + k * HS + m] : 0.f;
+          }, HS + 1, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+        const float bias = Ws[E3_B1 + m];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) {
+            const float v = reluf(c[q] + bias);
+            hE[i * HS + m] = v;
+            hEG[i * HS + m] = v;
+          }
         }
       }
     }
-  }
-  __syncthreads();
-  MID_STAMP();
-  {
-    float w[HS];
+    if (lane < 16 && row0 + lane < Ne) {
+      const int i = row0 + lane;
+      float o = Ws[E3_B2];
 #pragma unroll
-    for (int k = 0; k < HS; ++k) w[k] = Ws[E3_W2 + k];
-    for (int i = t; i < Ne; i += NT_MID) {
-      const float o = dot20(hE + i * HS, w, Ws[E3_B2]);
+      for (int k = 0; k < HS; ++k) o = fmaf(hE[i * HS + k], Ws[E3_W2 + k], o);
       os[i] = o;
       xps[i] = reluf(o);
     }
@@ -1442,9 +1464,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   __syncthreads();
   MID_STAMP();
 
-  // ---- M12: mlp2_entity_B1 backward (U re-carved: P | E_bar | h | dq | dE) ------------
-  float* dq = U + 3 * NE4 * HS;
-  float* dE = U + 4 * NE4 * HS;
+  // ---- M12: mlp2_entity_B1 backward.  U re-carved: P | E_bar | dq | dE | ... | h (-> rho)
+  float* dq = U + 2 * NE4 * HS;
+  float* dE = U + 3 * NE4 * HS;
+  const int rho_off = (4 * NE4 * HS > NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS)
+                          ? 4 * NE4 * HS
+                          : NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;
+  float* hB = U + rho_off;                          // h, overwritten by rho row block by row block
+  float* rho = hB;
+  float* dw2p = Xm;                                 // [row block][21] partial dw2', db2'
   for (int i = t; i < Ne; i += NT_MID) {
     const float d = (dxpart[i] + dxpart[NE4 + i]) + (dxpart[2 * NE4 + i] + dxpart[3 * NE4 + i]);
     dxp[i] = (os[i] > 0.f) ? d : 0.f;               // d o_i (x' = relu(o))
@@ -1455,24 +1483,68 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float4* s2 = reinterpret_cast<const float4*>(hEG);
     float4* d0 = reinterpret_cast<float4*>(Ps);
     float4* d1 = reinterpret_cast<float4*>(Eb);
-    float4* d2 = reinterpret_cast<float4*>(hE);
+    float4* d2 = reinterpret_cast<float4*>(hB);
     for (int e = t; e < Ne * HS / 4; e += NT_MID) { d0[e] = s0[e]; d1[e] = s1[e]; d2[e] = s2[e]; }
   }
   __syncthreads();
   MID_STAMP();
-  for (int e = t; e < Ne * HS; e += NT_MID) {
-    const int i = e / HS, k = e - i * HS;
-    dq[e] = (hE[e] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
-  }
-  for (int o = wv; o <= HS; o += NT_MID / 64) {     // dw2'[k] = sum_i h_ik do_i, db2' = sum do
-    float acc = 0.f;
-    for (int i = lane; i < Ne; i += 64) acc = fmaf(o < HS ? hE[i * HS + o] : 1.f, dxp[i], acc);
-    acc = wave_sum(acc);
-    if (lane == 0) pb[(o < HS ? E3_W2 + o : E3_B2)] = acc;
+  // row-local chain per 16-row block: dq = [h > 0] w2' do;  dE = dq W1'[1:]^T;
+  // rho = dE W5^T (into h's rows, consumed first); partial dw2' / db2' of the block
+  for (int rb = wv; rb < ntm_e; rb += NT_MID / 64) {          // wave-uniform
+    const int row0 = rb * 16;
+    for (int e = lane; e < 16 * HS; e += 64) {
+      const int i = row0 + e / HS, k = e - (e / HS) * HS;
+      if (i < Ne) dq[i * HS + k] = (hB[i * HS + k] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
+    }
+    if (lane <= HS) {
+      float acc = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        const int i = row0 + r;
+        if (i < Ne) acc = fmaf(lane < HS ? hB[i * HS + lane] : 1.f, dxp[i], acc);
+      }
+      dw2p[rb * 21 + lane] = acc;
+    }
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int col0 = cb * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k < HS && m < HS) ? Ws[E3_W1 + (1 + m) * HS + k] : 0.f;
+          }, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) dE[i * HS + m] = c[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int col0 = cb * 16;
+      const f4v c = mfma_tile16(
+          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
+          [&](int k, int j) {
+            const int m = col0 + j;
+            return (k < HS && m < HS) ? Ws[E1_W5 + m * HS + k] : 0.f;
+          }, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = row0 + 4 * (lane >> 4) + q;
+          if (i < Ne) rho[i * HS + m] = c[q];
+        }
+      }
+    }
   }
   __syncthreads();
   MID_STAMP();
-  // dW1' = [x, E_bar, 1]^T dq (waves 0-3, K = Ne) | dE = dq W1'[1:]^T (waves 4-15)
+  // ---- M13: reductions over rows: dW1' = [x, E_bar, 1]^T dq (waves 0-3),
+  //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8)
   if (wv < 4) {
     const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
     const f4v c = mfma_tile16(
@@ -1492,32 +1564,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         else if (l == HS + 1) pb[E3_B1 + k] = c[q];
       }
     }
-  } else {
-    for (int tile = wv - 4; tile < 2 * ntm_e; tile += NT_MID / 64 - 4) {
-      const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k < HS && m < HS) ? Ws[E3_W1 + (1 + m) * HS + k] : 0.f;
-          }, HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) dE[i * HS + m] = c[q];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  MID_STAMP();
-  // ---- M13: agg_entity_B1 / mlp_entity_B1 second layer backward; rho = dL/dP ----------
-  //   dW5 = [P, 1]^T dE (waves 0-3; row 20 -> db5 / 2(Ne-1)) | rho = dE W5^T (waves 4-15)
-  float* rho = Eb;      // E_bar dead after dW1'
-  if (wv < 4) {
-    const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
+  } else if (wv < 8) {
+    const int row0 = ((wv - 4) >> 1) * 16, col0 = ((wv - 4) & 1) * 16;
     const f4v c = mfma_tile16(
         [&](int r, int i) {
           const int l = row0 + r;
@@ -1534,24 +1582,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         else if (l == HS) pb[E1_B5 + k] = twoNe1 * c[q];
       }
     }
-  } else {
-    for (int tile = wv - 4; tile < 2 * ntm_e; tile += NT_MID / 64 - 4) {
-      const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k < HS && m < HS) ? Ws[E1_W5 + m * HS + k] : 0.f;
-          }, HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) rho[i * HS + m] = c[q];
-        }
-      }
-    }
+  } else if (wv == 8 && lane <= HS) {
+    float acc = 0.f;
+    for (int rb = 0; rb < ntm_e; ++rb) acc += dw2p[rb * 21 + lane];
+    pb[lane < HS ? E3_W2 + lane : E3_B2] = acc;
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 4) pb[NP + 1 + t] = 0.f;                  // trailer / pad
@@ -1567,9 +1601,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   so each set sum is one table read.  a = 1 corrections over the set bits of row i,
   //   same (node, k) lane map as E1.
   const int TL = NE4 + 4;
-  float* Tr = hE;                          // [HS][TL]
-  float* Tx = hE + HS * TL;                // [HS][TL]
-  float* red2 = hE + 2 * HS * TL;          // [16 waves][4][HS]
+  float* Tr = U + NE4 * HS;                // [HS][TL]   (E_bar, dq, dE slots are dead)
+  float* Tx = Tr + HS * TL;                // [HS][TL]
+  float* red2 = Tx + HS * TL;              // [16 waves][4][HS]  (ends below rho_off)
   // row neighbour lists again, staged into the P slot (dead after dW5) when they fit
   const bool rfit = ((nnz_r + 3) >> 2) <= NE4 * HS;
   const uint8_t* lrow2 = rfit ? reinterpret_cast<const uint8_t*>(Ps)
@@ -1594,7 +1628,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       r += val;
       run[q] = r;
     }
-    const float off = wave_incl_scan(r, lane) - r;
+    const float off = wave_incl_scan_dpp(r) - r;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int s = 4 * lane + q;

@@ -6,7 +6,7 @@
 
 namespace {
 
-template <int MODE>
+template <int MODE, int ABL = 0>
 __global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
   constexpr int SMAXC = 5, NC16 = 80;
   __shared__ __attribute__((aligned(16))) float A[NC16 * HS], B[NC16 * HS], R[NC16 * HS],
@@ -29,7 +29,7 @@ __global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
   __syncthreads();
   const int g = t >> 8, tg = t & 255;
   for (int it = 0; it < iters; ++it)
-    pair_tile<5, SMAXC, MODE, HS>(N, tg, A, B, g * 5, dl, bits, 3, wr, wc, gam, NC16, R, C, ys,
+    pair_tile<5, SMAXC, MODE, HS, ABL>(N, tg, A, B, g * 5, dl, bits, 3, wr, wc, gam, NC16, R, C, ys,
                                   cred + g * tile_cred_words<SMAXC, 5>());
   if (t == 0) out[blockIdx.x] = R[7] + C[11] + ys[3];
 }
@@ -62,6 +62,11 @@ int main() {
   printf("  MODE0 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<0>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE1 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<1>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE2 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<2>, dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("  MODE0 no y    %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<0, 1>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("  MODE0 no rowr %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<0, 2>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("  MODE0 neither %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<0, 3>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("  MODE1 no y    %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<1, 1>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("  MODE2 no y    %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<2, 1>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   CK(hipDeviceSynchronize());
   return 0;
 }
