@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include "hdgnn.h"
+#include "hdgnn_internal.h"
 
 namespace {
 
@@ -358,31 +359,8 @@ __device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n 
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // ------------------------------------------------------------------------------
-struct PrepLayout {
-  int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, words;
-};
-
-__host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
-  PrepLayout L;
-  const int NE4 = (Ne + 3) & ~3, WE = (Ne + 31) >> 5;
-  const int kw = ((Nc * Ne + 1) / 2 + 3) & ~3;
-  int o = 0;
-  L.xsrt = o; o += NE4;
-  L.perm = o; o += NE4;
-  L.xu = o;   o += NE4;
-  L.cum = o;  o += NE4 + 4;
-  L.pxd = o;  o += 2 * (NE4 + 4);     // even word offset: 8-byte aligned
-  L.meta = o; o += 4;                 // nd, nnz_r, nnz_c, byte offset of the column lists
-  L.offr = o; o += NE4 + 4;           // CSR row offsets (a_ij = 1, j != i)
-  L.offc = o; o += NE4 + 4;           // CSR column offsets (a_ji = 1)
-  L.ks = o;   o += kw;
-  L.kt = o;   o += kw;
-  L.ncst = o; o += (2 * Nc + 3) & ~3;
-  L.lists = o; o += (2 * Ne * (Ne - 1) + 4 + 3) / 4;   // u8 neighbour ids: rows | columns
-  L.words = (o + 63) & ~63;
-  (void)WE;
-  return L;
-}
+using hdg::PrepLayout;
+using hdg::prep_layout;
 
 // sort x (stable rank count), distinct values + f64 prefix sums, transposed class bits
 __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
@@ -1761,7 +1739,7 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
                                                   const float* __restrict__ grad, int np,
                                                   float lr, float inv_pairs,
                                                   float* __restrict__ stats) {
-  using namespace m2;
+  const int TH1 = np - 4, TH2 = np - 2;   // map_conv thetas close every variant
   __shared__ float red[16 * 4];
   __shared__ float sh[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1787,7 +1765,7 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
   const float b1p = bpow[0], b2p = bpow[1];
   const float lr_t = lr * sqrtf(1.f - b2p) / (1.f - b1p);
   if (t == 0 && stats) {
-    const float ce = grad[NP] * inv_pairs;
+    const float ce = grad[np] * inv_pairs;
     const float lmap = 0.01f * (n2 + n1);
     const float lpara = 0.0005f * sh[0];
     stats[0] = ce;
@@ -1815,17 +1793,6 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
 // ------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------
-thread_local char g_err[512] = "";
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(g_err, sizeof(g_err), fmt, ap);
-  va_end(ap);
-  return code;
-}
-
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
 
 struct Work {   // workspace carve (floats)
@@ -1854,18 +1821,88 @@ int prep_chunk(int ne, int nc) {
   return ch < nc ? ch : nc;
 }
 
-int check_shape(const hdg_shape* s) {
-  if (!s) return fail(HDG_EINVAL, "shape is NULL");
-  if (s->variant != 2)
-    return fail(HDG_EINVAL, "variant %d not built (this engine implements model_2)", s->variant);
-  if (s->batch < 1) return fail(HDG_EINVAL, "batch must be >= 1 (got %d)", s->batch);
-  if (s->ne < 2 || s->ne > 256) return fail(HDG_EINVAL, "ne must be in [2,256] (got %d)", s->ne);
-  if (s->nc < 2 || s->nc > 160) return fail(HDG_EINVAL, "nc must be in [2,160] (got %d)", s->nc);
+}  // namespace
+
+namespace hdg {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_prep_maps,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ch = prep_chunk(s->ne, s->nc);
+  const size_t lds = (size_t)(2 * ch * s->ne + 2 * s->nc) * 4;
+  hipLaunchKernelGGL(k_prep_maps, dim3(s->batch), dim3(1024), lds, st, bt->abits, bt->hid,
+                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch);
+  return hipGetLastError();
+}
+
+// tf.global_variables() order per variant: E1 E3 | EE EC | H1 H2 TH
+Off param_offsets(int v) {
+  Off o;
+  memset(&o, 0xff, sizeof(o));   // -1 everywhere
+  if (v < 1 || v > 4) return o;
+  int p = 0;
+  if (v == 2 || v == 4) {
+    o.E1_W1 = p; p += 80;  o.E1_B1 = p; p += 20;  o.E1_W5 = p; p += 400; o.E1_B5 = p; p += 20;
+    o.E3_W1 = p; p += 420; o.E3_B1 = p; p += 20;  o.E3_W2 = p; p += 20;  o.E3_B2 = p; p += 1;
+  }
+  if (v == 3 || v == 4) {
+    o.EE_W11 = p; p += 20; o.EE_W12 = p; p += 40; o.EE_B1 = p; p += 20;
+    o.EE_W2 = p; p += 400; o.EE_B2 = p; p += 20;
+    o.EC_W1 = p; p += 440; o.EC_B1 = p; p += 20; o.EC_W2 = p; p += 40; o.EC_B2 = p; p += 2;
+  }
+  o.H1_W1 = p; p += 200; o.H1_B1 = p; p += 20; o.H1_W2 = p; p += 400; o.H1_B2 = p; p += 20;
+  o.H2_W1 = p; p += 440; o.H2_B1 = p; p += 20; o.H2_W2 = p; p += 40;  o.H2_B2 = p; p += 2;
+  o.TH1 = p; p += 2; o.TH2 = p; p += 2;
+  o.NP = p;
+  return o;
+}
+
+}  // namespace hdg
+
+namespace {
+
+using hdg::fail;
+
+bool fused_fits(const hdg_shape* s) {
+  if (s->variant != 2 || s->ne > 256 || s->nc > 160) return false;
   const StepLayout L = step_layout(s->ne, s->nc, smax_c(s->nc));
-  if ((size_t)L.total * 4 > 160 * 1024)
-    return fail(HDG_EINVAL, "ne=%d nc=%d needs %zu B of LDS in k_commit_step (> 160 KiB)", s->ne,
-                s->nc, (size_t)L.total * 4);
-  return 0;
+  return (size_t)L.total * 4 <= 160 * 1024;
+}
+
+// validates the shape; returns the resolved path (HDG_PATH_FUSED / _GENERAL) or -1
+int resolve(const hdg_shape* s) {
+  if (!s) return fail(HDG_EINVAL, "shape is NULL"), -1;
+  if (s->variant < 1 || s->variant > 4)
+    return fail(HDG_EINVAL, "variant must be 1..4 (model_<variant>.py), got %d", s->variant), -1;
+  if (s->batch < 1) return fail(HDG_EINVAL, "batch must be >= 1 (got %d)", s->batch), -1;
+  if (s->ne < 2 || s->ne > 4096) return fail(HDG_EINVAL, "ne must be in [2,4096] (got %d)", s->ne), -1;
+  if (s->nc < 2 || s->nc > 2048) return fail(HDG_EINVAL, "nc must be in [2,2048] (got %d)", s->nc), -1;
+  if (s->path == HDG_PATH_GENERAL) return HDG_PATH_GENERAL;
+  const bool fits = fused_fits(s);
+  if (s->path == HDG_PATH_FUSED) {
+    if (!fits)
+      return fail(HDG_EINVAL, "the fused path runs model_2 with ne <= 256, nc <= 160 "
+                              "(got variant %d, ne=%d, nc=%d)", s->variant, s->ne, s->nc), -1;
+    return HDG_PATH_FUSED;
+  }
+  if (s->path != HDG_PATH_AUTO) return fail(HDG_EINVAL, "unknown path %d", s->path), -1;
+  return fits ? HDG_PATH_FUSED : HDG_PATH_GENERAL;
 }
 
 int check_batch(const hdg_batch* bt) {
@@ -1879,6 +1916,10 @@ int check_batch(const hdg_batch* bt) {
     hipError_t e_ = (expr);                                                               \
     if (e_ != hipSuccess) return fail((int)e_, "%s: %s", #expr, hipGetErrorString(e_));   \
   } while (0)
+
+#define RESOLVE(s, var)                          \
+  const int var = resolve(s);                    \
+  if (var < 0) return HDG_EINVAL
 
 template <int SMAXC, bool TRAIN, bool STAMPS>
 hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
@@ -1911,63 +1952,72 @@ hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* p
   }
 }
 
+float pair_count(const hdg_shape* s) {
+  const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
+  return (float)bg * (float)(s->nc * (s->nc - 1));
+}
+
 }  // namespace
 
 extern "C" {
 
 int hdg_version(void) { return HDG_ABI_VERSION; }
-const char* hdg_last_error(void) { return g_err; }
-int hdg_param_count(int32_t variant) { return variant == 2 ? m2::NP : -1; }
-int hdg_grad_len(int32_t variant) { return variant == 2 ? GRAD_LEN : -1; }
+const char* hdg_last_error(void) { return hdg::g_err; }
+int hdg_resolve_path(const hdg_shape* shape) { return resolve(shape); }
+int hdg_param_count(int32_t variant) { return hdg::param_offsets(variant).NP; }
+int hdg_grad_len(int32_t variant) {
+  const int np = hdg::param_offsets(variant).NP;
+  return np < 0 ? -1 : np + 4;
+}
 
 size_t hdg_workspace_bytes(const hdg_shape* shape) {
-  if (check_shape(shape)) return 0;
+  const int path = resolve(shape);
+  if (path < 0) return 0;
+  if (path == HDG_PATH_GENERAL) return hdg::wide_workspace_bytes(shape);
   return work_layout(shape).total * sizeof(float);
 }
 
 size_t hdg_prep_bytes(const hdg_shape* shape) {
-  if (check_shape(shape)) return 0;
+  const int path = resolve(shape);
+  if (path < 0) return 0;
+  if (path == HDG_PATH_GENERAL) return hdg::wide_prep_bytes(shape);
   return (size_t)shape->batch * prep_layout(shape->ne, shape->nc).words * 4;
 }
 
 int hdg_prepare(const hdg_shape* s, const hdg_batch* bt, void* stream) {
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
   if (int rc = check_batch(bt)) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (path == HDG_PATH_GENERAL) return hdg::wide_prepare(s, bt, st);
   hipLaunchKernelGGL(k_prep_sort, dim3(s->batch), dim3(256), 0, st, bt->x, bt->abits,
                      (uint32_t*)bt->prep, s->ne, s->nc);
   HIP_TRY(hipGetLastError());
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_TRY(hipFuncSetAttribute((const void*)k_prep_maps,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
-  const int ch = prep_chunk(s->ne, s->nc);
-  const size_t lds = (size_t)(2 * ch * s->ne + 2 * s->nc) * 4;
-  hipLaunchKernelGGL(k_prep_maps, dim3(s->batch), dim3(1024), lds, st, bt->abits, bt->hid,
-                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(hdg::launch_prep_maps(s, bt, st));
   return 0;
 }
 
 int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* params,
                        float* grad, hdg_outputs* out, void* workspace, void* stream,
                        void* const* events) {
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
   if (int rc = check_batch(bt)) return rc;
   if (!params || !grad || !workspace) return fail(HDG_EINVAL, "NULL params/grad/workspace");
   hipStream_t st = (hipStream_t)stream;
-  const Work w = work_layout(s);
-  float* ws = (float*)workspace;
-  const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
-  const float ce_scale = 10.f / ((float)bg * (float)(s->nc * (s->nc - 1)));
   auto mark = [&](int k) -> hipError_t {
     return events ? hipEventRecord((hipEvent_t)events[k], st) : hipSuccess;
   };
+  if (path == HDG_PATH_GENERAL) {
+    HIP_TRY(mark(0));
+    if (int rc = hdg::wide_run(s, bt, params, grad, out, nullptr, workspace, true, st)) return rc;
+    HIP_TRY(mark(1));
+    HIP_TRY(mark(2));
+    return 0;
+  }
+  const Work w = work_layout(s);
+  float* ws = (float*)workspace;
   HIP_TRY(mark(0));
   HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, ce_scale, nullptr, st));
+                              out ? out->logits : nullptr, 10.f / pair_count(s), nullptr, st));
   HIP_TRY(mark(1));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st,
                      ws + w.part, s->batch, 0, GRAD_LEN, grad);
@@ -1983,7 +2033,8 @@ int hdg_fwd_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, fl
 
 int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* params,
                           void* workspace, unsigned long long* stamps, void* stream) {
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
+  if (path != HDG_PATH_FUSED) return fail(HDG_EINVAL, "phase stamps exist on the fused path only");
   if (int rc = check_batch(bt)) return rc;
   if (!stamps || !workspace || !params) return fail(HDG_EINVAL, "NULL stamps/workspace/params");
   const Work w = work_layout(s);
@@ -1995,32 +2046,35 @@ int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* 
 
 int hdg_adam_tf(const hdg_shape* s, hdg_state* state, const float* grad, float lr, float* stats,
                 void* stream) {
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
+  (void)path;
   if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow || !grad)
     return fail(HDG_EINVAL, "NULL state/grad pointer");
-  const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
-  const float inv_pairs = 1.f / ((float)bg * (float)(s->nc * (s->nc - 1)));
   hipLaunchKernelGGL(k_adam_tf, dim3(1), dim3(1024), 0, (hipStream_t)stream, state->params,
-                     state->adam_m, state->adam_v, state->beta_pow, grad, m2::NP, lr, inv_pairs,
-                     stats);
+                     state->adam_m, state->adam_v, state->beta_pow, grad,
+                     hdg::param_offsets(s->variant).NP, lr, 1.f / pair_count(s), stats);
   HIP_TRY(hipGetLastError());
   return 0;
 }
 
 int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, float lr,
                    hdg_outputs* out, float* grad, void* workspace, void* stream) {
-  // single process: k_commit_step (+ loss stats / Adam factor from block 0) then the
-  // fused deterministic reduction + TF Adam; no all-reduce point in between
   if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow)
     return fail(HDG_EINVAL, "NULL state pointer");
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
   if (int rc = check_batch(bt)) return rc;
   if (!grad || !workspace) return fail(HDG_EINVAL, "NULL grad/workspace");
   hipStream_t st = (hipStream_t)stream;
+  if (path == HDG_PATH_GENERAL) {
+    if (int rc = hdg::wide_run(s, bt, state->params, grad, out, nullptr, workspace, true, st))
+      return rc;
+    return hdg_adam_tf(s, state, grad, lr, out ? out->stats : nullptr, stream);
+  }
+  // single process, fused path: k_commit_step (+ loss stats / Adam factor from block 0),
+  // then the fused deterministic reduction + TF Adam; no all-reduce point in between
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
-  const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
-  const float pairs = (float)bg * (float)(s->nc * (s->nc - 1));
+  const float pairs = pair_count(s);
   HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, out ? out->probs : nullptr,
                               out ? out->logits : nullptr, 10.f / pairs, nullptr, st,
                               state->beta_pow));
@@ -2033,10 +2087,12 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
 
 int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hdg_outputs* out,
                 float* ce_sum, void* workspace, void* stream) {
-  if (int rc = check_shape(s)) return rc;
+  RESOLVE(s, path);
   if (int rc = check_batch(bt)) return rc;
   if (!params || !workspace) return fail(HDG_EINVAL, "NULL params/workspace");
   hipStream_t st = (hipStream_t)stream;
+  if (path == HDG_PATH_GENERAL)
+    return hdg::wide_run(s, bt, params, nullptr, out, ce_sum, workspace, false, st);
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
   HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, out ? out->probs : nullptr,

@@ -1,0 +1,88 @@
+// hdgnn_internal.h -- declarations shared by the two engine paths of libhdgnn.so
+// (not part of the public C ABI; see include/hdgnn.h).
+//
+//   fused path   hdgnn.hip  one 1024-thread block per commit, LDS-resident commit state;
+//                           model_2 with ne <= 256, nc <= 160 (the benchmark shape)
+//   general path wide.hip   any ne / nc, model variants 1-4, one phase per launch with
+//                           many 256-thread blocks per commit, state in HBM
+#ifndef HDGNN_INTERNAL_H
+#define HDGNN_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hdgnn.h"
+
+namespace hdg {
+
+constexpr int HS = 20;   // h_size = De_e = De_er (model_2.py:163, 192, 247, 306)
+
+// ------------------------------------------------------------------------------
+// Prepared batch, fused-path layout (hdg_prepare: once per uploaded batch, independent
+// of the parameters).  Per commit, in 4-byte words:
+//   xsrt[NE4]    x sorted ascending            perm[NE4]  node at sorted slot m
+//   xu[NE4]      the nd distinct x values      cum[NE4+4] cum[q] = #nodes with x < xu[q]
+//   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
+//   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
+//   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
+//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
+//   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
+// The general path uses only ks / kt / ncst of this block and appends, after all B
+// commits, the transposed class bits a^T [B][Ne][WE] and y^T [B][Nc][WC].
+// ------------------------------------------------------------------------------
+struct PrepLayout {
+  int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, words;
+};
+
+__host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
+  PrepLayout L;
+  const int NE4 = (Ne + 3) & ~3;
+  const int kw = ((Nc * Ne + 1) / 2 + 3) & ~3;
+  int o = 0;
+  L.xsrt = o; o += NE4;
+  L.perm = o; o += NE4;
+  L.xu = o;   o += NE4;
+  L.cum = o;  o += NE4 + 4;
+  L.pxd = o;  o += 2 * (NE4 + 4);     // even word offset: 8-byte aligned
+  L.meta = o; o += 4;                 // nd, nnz_r, nnz_c, byte offset of the column lists
+  L.offr = o; o += NE4 + 4;           // CSR row offsets (a_ij = 1, j != i)
+  L.offc = o; o += NE4 + 4;           // CSR column offsets (a_ji = 1)
+  L.ks = o;   o += kw;
+  L.kt = o;   o += kw;
+  L.ncst = o; o += (2 * Nc + 3) & ~3;
+  L.lists = o; o += (2 * Ne * (Ne - 1) + 4 + 3) / 4;   // u8 neighbour ids: rows | columns
+  L.words = (o + 63) & ~63;
+  return L;
+}
+
+// Flat parameter offsets of one model variant (tf.global_variables order, SURVEY
+// Appendix A); -1 for blocks the variant does not have.
+struct Off {
+  int E1_W1, E1_B1, E1_W5, E1_B5;            // phi_E_O1  mlp_entity_B1
+  int E3_W1, E3_B1, E3_W2, E3_B2;            // phi_U_O1  mlp2_entity_B1
+  int EE_W11, EE_W12, EE_B1, EE_W2, EE_B2;   // phi_E_R1  mlp_entityedge_B1 (model_4)
+  int EC_W1, EC_B1, EC_W2, EC_B2;            // phi_U_R1  mlp2_entityedge_B1 (model_4)
+  int H1_W1, H1_B1, H1_W2, H1_B2;            // mlp_hunk_B2
+  int H2_W1, H2_B1, H2_W2, H2_B2;            // phi_U_R1(_1)  mlp_hunkedge_B2
+  int TH1, TH2, NP;                          // map_conv thetas, parameter count
+};
+
+Off param_offsets(int variant);   // NP = -1 for an unknown variant
+
+// general path (wide.hip)
+size_t wide_workspace_bytes(const hdg_shape* s);
+size_t wide_prep_bytes(const hdg_shape* s);
+int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
+// train: forward + backward -> grad[NP + 4] (slot NP = CE sum); !train: forward only,
+// CE sum -> *ce_sum (may be NULL).  Outputs as in hdg_fwd_bwd.
+int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
+             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st);
+
+// fused path pieces the general path reuses (hdgnn.hip)
+hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+}  // namespace hdg
+
+#endif  // HDGNN_INTERNAL_H

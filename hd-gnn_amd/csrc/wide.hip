@@ -1,0 +1,1507 @@
+// wide.hip -- general path of the HD-GNN training step: any Ne / Nc (<= 4096 / 2048) and
+// all four model variants (model_1..model_4.py), built from many 256-thread blocks per
+// commit with the commit state in HBM.  The fused path (hdgnn.hip) covers model_2 at the
+// benchmark shapes; this path covers everything else (model_4's entity-edge stage, the
+// model_1 / model_3 wirings, the stress shapes Ne=1024 / Nc=512) and doubles as a
+// cross-check of the fused kernel.
+//
+// One training step, as a sequence of launches on the caller's stream (x' = x for
+// model_1 / model_3, ENT = model_2/4 entity stage, EE = model_4 entity-edge stage):
+//   kw_derive       derived weight products (M = V2 U1e, offsets, differences)
+//   kw_ent_fwd      ENT: P_i  = sum_j relu(z_ij) + relu(z_ji)     (mlp_entity_B1 + agg)
+//                   EE : R1_i = sum_j relu(z'_ij), C1_i = sum_j relu(z'_ji)
+//   kw_node_fwd     ENT: E_bar, h, o, x'          EE: R, C, rho, gam (classifier operands)
+//   kw_ee_fwd       EE : entity-edge classifier + softmax on every relation the index file
+//                   maps, aggregated into n_c[2:4] (marshalling_B2 of B_2's edge part)
+//   kw_cross_fwd    n_c = [K_s x', K_t x', n_c[2:4]]; hunk first-layer alpha, beta
+//   kw_hunk_fwd     G_p = sum_q relu(a_p + b_q + y d) (row pass), H_q (column pass),
+//                   sigma / tau (classifier first layer on eff = S_p + T_q)
+//   kw_hunk_cls     classifier + softmax-CE per hunk pair, gamma = dL/dz1
+//   -- backward --
+//   kw_hunk_clsb    Dsig / Dtau (row / column pass), dG / dH, classifier + V2 grads
+//   kw_hunk_mlpb    Dalpha / Dbeta, V1 / c1 grads
+//   kw_dn           dn_c (gradient of the cross-graph aggregate)
+//   kw_node_bwd     ENT: dx', E3 and W5 grads, rho = dP
+//   kw_ent_bwd      ENT: first-layer grads of mlp_entity_B1
+//   kw_ee_clsb      EE : classifier backward (column pass: dgam + classifier grads, row
+//                   pass: drho)
+//   kw_ee_nodeb     EE : dR, dC -> phi, psi; classifier U1e, Q2, q2 grads
+//   kw_ee_firstb    EE : first-layer grads of mlp_entityedge_B1 (shared w1_1)
+//   kw_grad_reduce  fixed-order sum of every per-block partial row -> flat gradient
+//
+// Determinism: no floating-point atomics anywhere.  Per-block partial gradient rows are
+// summed in a fixed order; row/column sums over pairs are recomputed by a row pass and a
+// column pass instead of being scattered.  The one scatter (relation -> hunk bins of
+// kw_ee_fwd) accumulates in 2^-32 fixed point with integer atomics, order-independent.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "hdgnn.h"
+#include "hdgnn_internal.h"
+
+namespace hdg {
+namespace {
+
+constexpr int H = HS;
+constexpr int HP = H + 1;   // padded LDS rows (odd stride: conflict-free column access)
+constexpr int TN = 64;      // nodes per tile, one per lane
+constexpr int NT = 256;     // threads per block
+constexpr int NW = NT / 64;
+constexpr double FIX = 4294967296.0;   // 2^32 fixed-point scale of the hunk bins
+
+__device__ __forceinline__ float relu(float v) { return fmaxf(v, 0.f); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// wave sum by xor butterfly: every lane ends with the same (fixed-order) total
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long qfix(float v) {
+  return (unsigned long long)__double2ll_rn((double)v * FIX);
+}
+
+// q = r / d, rem = r % d for 0 <= r < 2^24, d >= 1 (float estimate, exact correction)
+__device__ __forceinline__ void divmod24(int r, int d, float inv, int& q, int& rem) {
+  q = (int)((float)r * inv);
+  rem = r - q * d;
+  while (rem < 0) { --q; rem += d; }
+  while (rem >= d) { ++q; rem -= d; }
+}
+
+// derived weights (kw_derive), float offsets into the D buffer
+enum : int {
+  D_M = 0,                 // [20][20] V2 . U1e  (hunk MLP second layer into the classifier)
+  D_S0 = 400,              // sigma offset  (Nc-1) c2 U1e + U1[0] + d1
+  D_T0 = 420,              // tau offset    (Nc-1) c2 U1e
+  D_EPS = 440,             // U1[1] - U1[0]
+  D_CV = 460,              // U2[:,1] - U2[:,0]
+  D_DLT = 480,             // V1[9] - V1[8]
+  D_EED = 500,             // EE classifier P1[1] - P1[0]
+  D_EEC = 520,             // EE classifier U2'[:,1] - U2'[:,0]
+  D_WORDS = 544
+};
+
+// per-block partial gradient rows: segment s holds n consecutive parameters starting at
+// flat index p0, laid out [n][rows] at part + off
+constexpr int MAXSEG = 16;
+struct Seg {
+  int p0, n, rows;
+  long long off;
+};
+struct Segs {
+  Seg s[MAXSEG];
+  int count;
+};
+enum : int {
+  SG_CLS = 0,   // H2_W2 .. H2_B2 (42)                 kw_hunk_cls
+  SG_CE,        // CE sum slot NP                      kw_hunk_cls
+  SG_CLSB_H2,   // H2_W1 .. H2_B1 (460)                kw_hunk_clsb (2 passes)
+  SG_CLSB_H1,   // H1_W2 .. H1_B2 (420)                kw_hunk_clsb (2 passes)
+  SG_MLPB,      // H1_W1 .. H1_B1 (220)                kw_hunk_mlpb (2 passes)
+  SG_E3,        // E3_W1 .. E3_B2 (461)                kw_node_bwd
+  SG_E1W5,      // E1_W5 .. E1_B5 (420)                kw_node_bwd
+  SG_E1W1,      // E1_W1 .. E1_B1 (100)                kw_ent_bwd
+  SG_ECW1A,     // EC_W1 rows 0, 1 (40)                kw_ee_clsb column pass
+  SG_ECB1,      // EC_B1 .. EC_B2 (62)                 kw_ee_clsb column pass
+  SG_ECW1E,     // EC_W1 rows 2..21 (400)              kw_ee_nodeb
+  SG_EEW2,      // EE_W2 .. EE_B2 (420)                kw_ee_nodeb
+  SG_EEW11,     // EE_W11 .. EE_B1 (80)                kw_ee_firstb
+  SG_COUNT
+};
+
+__device__ __forceinline__ void put(float* part, const Seg& s, int q, int row, float v) {
+  part[s.off + (long long)q * s.rows + row] = v;
+}
+
+// ---------------------------------------------------------------------------------
+// kw_derive: weight products every phase reads (1 block)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_derive(const float* __restrict__ W, Off o, int Nc,
+                                                float* __restrict__ D) {
+  const int t = threadIdx.x;
+  const float Nc1 = (float)(Nc - 1);
+  for (int e = t; e < H * H; e += NT) {           // M[l][k] = sum_m V2[l][m] U1e[m][k]
+    const int l = e / H, k = e - l * H;
+    float acc = 0.f;
+    for (int m = 0; m < H; ++m)
+      acc = fmaf(W[o.H1_W2 + l * H + m], W[o.H2_W1 + (2 + m) * H + k], acc);
+    D[D_M + e] = acc;
+  }
+  if (t < H) {
+    float cu = 0.f;
+    for (int m = 0; m < H; ++m) cu = fmaf(W[o.H1_B2 + m], W[o.H2_W1 + (2 + m) * H + t], cu);
+    cu *= Nc1;
+    D[D_T0 + t] = cu;
+    D[D_S0 + t] = cu + (W[o.H2_W1 + t] + W[o.H2_B1 + t]);
+    D[D_EPS + t] = W[o.H2_W1 + H + t] - W[o.H2_W1 + t];
+    D[D_CV + t] = W[o.H2_W2 + 2 * t + 1] - W[o.H2_W2 + 2 * t];
+    D[D_DLT + t] = W[o.H1_W1 + 9 * H + t] - W[o.H1_W1 + 8 * H + t];
+    if (o.EC_W1 >= 0) {
+      D[D_EED + t] = W[o.EC_W1 + H + t] - W[o.EC_W1 + t];
+      D[D_EEC + t] = W[o.EC_W2 + 2 * t + 1] - W[o.EC_W2 + 2 * t];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// block helpers
+// ---------------------------------------------------------------------------------
+// Combine per-wave accumulators acc[H] of the 64 lane-nodes over the 4 waves (fixed order)
+// into res[64][HP].  buf: [NW][64][HP].
+__device__ __forceinline__ void combine4(const float (&acc)[H], float* buf, float* res) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < H; ++k) buf[(w * TN + lane) * HP + k] = acc[k];
+  __syncthreads();
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    res[n * HP + k] = ((buf[(0 * TN + n) * HP + k] + buf[(1 * TN + n) * HP + k]) +
+                       buf[(2 * TN + n) * HP + k]) + buf[(3 * TN + n) * HP + k];
+  }
+  __syncthreads();
+}
+
+// Block sum of nv per-thread values (each wave xor-reduces, then a fixed 4-way sum);
+// result in out[0..nv) of LDS.  red: [NW][nv].
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* red, float* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const float s = wsum(v[q]);
+    if (lane == 0) red[w * NV + q] = s;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NV; q += NT)
+    out[q] = ((red[q] + red[NV + q]) + red[2 * NV + q]) + red[3 * NV + q];
+  __syncthreads();
+}
+
+// The m-range of the other index a wave sweeps, split around this tile's own nodes
+// [t0, t0 + 64) so the self pair (m == node) is masked only where it can occur.
+template <class F>
+__device__ __forceinline__ void sweep(int N, int t0, F f) {
+  const int w = uni(threadIdx.x >> 6);
+  const int lo = (N * w) / NW, hi = (N * (w + 1)) / NW;
+  const int a = lo < t0 ? lo : t0, e1 = hi < t0 ? hi : t0;
+  const int t1 = t0 + TN;
+  const int b0 = lo > t0 ? lo : t0, b1 = hi < t1 ? hi : t1;
+  const int c0 = lo > t1 ? lo : t1;
+  for (int m = a; m < e1; ++m) f(m, false);
+  for (int m = b0; m < b1; ++m) f(m, true);
+  for (int m = c0; m < hi; ++m) f(m, false);
+}
+
+__device__ __forceinline__ float bitf(const uint32_t* row, int m) {
+  return ((row[m >> 5] >> (m & 31)) & 1u) ? 1.f : 0.f;
+}
+
+// ---------------------------------------------------------------------------------
+// kw_ent_fwd  grid (te, B, 1 + EE): z = 0 entity stage (if the variant has it) else EE
+//   E1 (model_2.py:161-188): pair (i,j) pre-activation u_i + x_j w1 + a_ij d with
+//     u = x w0 + w2 + b1, d = w3 - w2; P_i = sum_{j!=i} relu(z_ij) + relu(z_ji)
+//   EE (model_4.py:206-243, shared w1_1): z'_ij = (x_i + x_j) w + e + a_ij d',
+//     R1_i = sum_{j!=i} relu(z'_ij) (source side), C1_i = sum_{j!=i} relu(z'_ji)
+// ---------------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ void ent_fwd_body(const float* __restrict__ x,
+                                             const uint32_t* __restrict__ abits,
+                                             const uint32_t* __restrict__ aT,
+                                             const float* __restrict__ W, const Off& o, int Ne,
+                                             float* __restrict__ out0, float* __restrict__ out1,
+                                             float* buf) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.y, t0 = blockIdx.x * TN;
+  const int lane = threadIdx.x & 63;
+  const int i = t0 + lane, ic = i < Ne ? i : Ne - 1;
+  const int WE = (Ne + 31) >> 5;
+  const float* xb = x + (size_t)b * Ne;
+  const float xi = xb[ic];
+  float wr[H], wc[H], ur[H], uc[H], dd[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    if constexpr (MODE == 0) {
+      const float w0 = W[o.E1_W1 + k], w1 = W[o.E1_W1 + H + k], w2 = W[o.E1_W1 + 2 * H + k];
+      const float c0 = w2 + W[o.E1_B1 + k];
+      dd[k] = W[o.E1_W1 + 3 * H + k] - w2;
+      wr[k] = w1;
+      wc[k] = w0;
+      ur[k] = fmaf(xi, w0, c0);
+      uc[k] = fmaf(xi, w1, c0);
+    } else {
+      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
+      dd[k] = W[o.EE_W12 + H + k] - w20;
+      wr[k] = w;
+      wc[k] = w;
+      ur[k] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
+      uc[k] = ur[k];
+    }
+  }
+  float ar[H], ac[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) { ar[k] = 0.f; ac[k] = 0.f; }
+  const uint32_t* rowb = abits + ((size_t)b * Ne + ic) * WE;
+  const uint32_t* colb = aT + ((size_t)b * Ne + ic) * WE;
+  sweep(Ne, t0, [&](int j, bool self) {
+    const float xj = xb[j];
+    const float fr = bitf(rowb, j), fc = bitf(colb, j);
+    const bool on = !(self && j == i);
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const float zr = fmaf(fr, dd[k], fmaf(xj, wr[k], ur[k]));
+      const float zc = fmaf(fc, dd[k], fmaf(xj, wc[k], uc[k]));
+      ar[k] += on ? relu(zr) : 0.f;
+      ac[k] += on ? relu(zc) : 0.f;
+    }
+  });
+  float* bufr = buf;
+  float* bufc = buf + NW * TN * HP;
+  float* resr = buf + 2 * NW * TN * HP;
+  float* resc = resr + TN * HP;
+  combine4(ar, bufr, resr);
+  combine4(ac, bufc, resc);
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    if (t0 + n >= Ne) continue;
+    const size_t g = ((size_t)b * Ne + t0 + n) * H + k;
+    if constexpr (MODE == 0) {
+      out0[g] = resr[n * HP + k] + resc[n * HP + k];
+    } else {
+      out0[g] = resr[n * HP + k];
+      out1[g] = resc[n * HP + k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
+                                                 const uint32_t* __restrict__ abits,
+                                                 const uint32_t* __restrict__ aT,
+                                                 const float* __restrict__ W, Off o, int Ne,
+                                                 int ent, float* __restrict__ P,
+                                                 float* __restrict__ R1, float* __restrict__ C1) {
+  __shared__ float buf[2 * NW * TN * HP + 2 * TN * HP];
+  if (blockIdx.z == 0 && ent)
+    ent_fwd_body<0>(x, abits, aT, W, o, Ne, P, nullptr, buf);
+  else
+    ent_fwd_body<1>(x, abits, aT, W, o, Ne, R1, C1, buf);
+}
+
+// ---------------------------------------------------------------------------------
+// kw_node_fwd  grid (te, B, 1 + EE)
+//   ENT (model_2.py:181-205): E_bar = P W5 + 2(Ne-1) b5; h = relu([x, E_bar] W1' + b1');
+//        o = h w2' + b2'; x' = relu(o)
+//   EE  (model_4.py:232-243, 282-304): R = R1 Q2 + (Ne-1) q2, C = C1 Q2 + (Ne-1) q2;
+//        classifier first-layer operands rho = R U1e' + U1'[0] + b1', gam = C U1e'
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_node_fwd(
+    const float* __restrict__ x, const float* __restrict__ W, Off o, int Ne, int ent,
+    const float* __restrict__ P, float* __restrict__ Eb, float* __restrict__ hE,
+    float* __restrict__ ov, float* __restrict__ xp, const float* __restrict__ R1,
+    const float* __restrict__ C1, float* __restrict__ Rn, float* __restrict__ Cn,
+    float* __restrict__ rho, float* __restrict__ gmm) {
+  __shared__ float A[TN * HP], Bs[TN * HP], Cs[TN * HP], Ds[TN * HP];
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x;
+  const int nn = Ne - t0 < TN ? Ne - t0 : TN;
+  const size_t base = ((size_t)b * Ne + t0) * H;
+  const float Ne1 = (float)(Ne - 1);
+  if (blockIdx.z == 0 && ent) {
+    for (int e = t; e < nn * H; e += NT) A[(e / H) * HP + e % H] = P[base + e];
+    __syncthreads();
+    for (int e = t; e < nn * H; e += NT) {
+      const int n = e / H, k = e - n * H;
+      float acc = 0.f;
+      for (int m = 0; m < H; ++m) acc = fmaf(A[n * HP + m], W[o.E1_W5 + m * H + k], acc);
+      acc += (2.f * Ne1) * W[o.E1_B5 + k];
+      Bs[n * HP + k] = acc;
+      Eb[base + e] = acc;
+    }
+    __syncthreads();
+    for (int e = t; e < nn * H; e += NT) {
+      const int n = e / H, k = e - n * H;
+      float acc = x[(size_t)b * Ne + t0 + n] * W[o.E3_W1 + k];
+      for (int m = 0; m < H; ++m) acc = fmaf(Bs[n * HP + m], W[o.E3_W1 + (1 + m) * H + k], acc);
+      const float v = relu(acc + W[o.E3_B1 + k]);
+      Cs[n * HP + k] = v;
+      hE[base + e] = v;
+    }
+    __syncthreads();
+    for (int n = t; n < nn; n += NT) {
+      float acc = W[o.E3_B2];
+      for (int k = 0; k < H; ++k) acc = fmaf(Cs[n * HP + k], W[o.E3_W2 + k], acc);
+      ov[(size_t)b * Ne + t0 + n] = acc;
+      xp[(size_t)b * Ne + t0 + n] = relu(acc);
+    }
+    return;
+  }
+  for (int e = t; e < nn * H; e += NT) {
+    A[(e / H) * HP + e % H] = R1[base + e];
+    Bs[(e / H) * HP + e % H] = C1[base + e];
+  }
+  __syncthreads();
+  for (int e = t; e < nn * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    float ar = 0.f, ac = 0.f;
+    for (int m = 0; m < H; ++m) {
+      const float q = W[o.EE_W2 + m * H + k];
+      ar = fmaf(A[n * HP + m], q, ar);
+      ac = fmaf(Bs[n * HP + m], q, ac);
+    }
+    const float qb = Ne1 * W[o.EE_B2 + k];
+    Cs[n * HP + k] = ar + qb;
+    Ds[n * HP + k] = ac + qb;
+    Rn[base + e] = ar + qb;
+    Cn[base + e] = ac + qb;
+  }
+  __syncthreads();
+  for (int e = t; e < nn * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    float ar = 0.f, ac = 0.f;
+    for (int m = 0; m < H; ++m) {
+      const float q = W[o.EC_W1 + (2 + m) * H + k];
+      ar = fmaf(Cs[n * HP + m], q, ar);
+      ac = fmaf(Ds[n * HP + m], q, ac);
+    }
+    rho[base + e] = ar + (W[o.EC_W1 + k] + W[o.EC_B1 + k]);
+    gmm[base + e] = ac;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_ee_fwd  grid (te, B), dynamic LDS u64 bins[Nc][2]
+//   model_4: e'_ij = softmax(U2'^T relu(P1'^T [1-a, a, eff_ij] + p1) + p2) replaces the
+//   one-hot E_edge in B_2 (model_4.py:95-97), and marshalling_B2 bins B_2 by the index
+//   file's hunk maps: n_c[2+m] += e'_r[m] for c in {hid[i'], hid[j']} of every relation
+//   r < n(n-1) on the n-grid (utils2.py:121-137).  Relations outside that range feed
+//   nothing, so only they are evaluated.  Lanes walk index rows i' (one per lane), each
+//   wave a quarter of the j' range; relation r -> entity pair (i, j) on the Ne-grid is
+//   advanced incrementally.  Source bins: per-lane sums; target bins: wave sums.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abits,
+                                                const int32_t* __restrict__ hidg,
+                                                const int32_t* __restrict__ nleng,
+                                                const float* __restrict__ W, Off o,
+                                                const float* __restrict__ D, int Ne, int Nc,
+                                                const float* __restrict__ rho,
+                                                const float* __restrict__ gmm,
+                                                unsigned long long* __restrict__ ncacc) {
+#pragma clang fp contract(off)
+  extern __shared__ unsigned long long bins[];
+  const int b = blockIdx.y, t0 = blockIdx.x * TN;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  int n = nleng[b];
+  n = n < 0 ? 0 : (n > Ne ? Ne : n);
+  if (n < 2 || t0 >= n) return;   // block-uniform
+  for (int c = threadIdx.x; c < 2 * Nc; c += NT) bins[c] = 0ull;
+  __syncthreads();
+  const int WE = (Ne + 31) >> 5;
+  const int32_t* hid = hidg + (size_t)b * Ne;
+  const int ip = t0 + lane;
+  const bool live = ip < n;
+  const int ipc = live ? ip : 0;
+  const int jlo = (n * wv) / NW, jhi = (n * (wv + 1)) / NW;
+  const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
+  int ei = r0 / (Ne - 1), ejj = r0 - ei * (Ne - 1);
+  float rh[H], dl[H], u0[H], u1[H];
+  const float* rb = rho + (size_t)b * Ne * H;
+  const float* gb = gmm + (size_t)b * Ne * H;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    rh[k] = rb[(ei < Ne ? ei : Ne - 1) * H + k];
+    dl[k] = D[D_EED + k];
+    u0[k] = W[o.EC_W2 + 2 * k];
+    u1[k] = W[o.EC_W2 + 2 * k + 1];
+  }
+  int cur = ei;
+  const float b0 = W[o.EC_B2], b1 = W[o.EC_B2 + 1];
+  float s0 = 0.f, s1 = 0.f;
+  for (int jp = jlo; jp < jhi; ++jp) {
+    const bool valid = live && jp != ip;
+    float p0 = 0.f, p1 = 0.f;
+    if (valid) {
+      const int ej = ejj + (ejj >= ei ? 1 : 0);
+      if (ei != cur) {
+#pragma unroll
+        for (int k = 0; k < H; ++k) rh[k] = rb[ei * H + k];
+        cur = ei;
+      }
+      const float af = bitf(abits + ((size_t)b * Ne + ei) * WE, ej);
+      const float4* g4 = reinterpret_cast<const float4*>(gb + (size_t)ej * H);
+      float z0 = b0, z1 = b1;
+#pragma unroll
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 q = g4[v];
+        const float qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = 4 * v + u;
+          const float kk = relu(fmaf(af, dl[k], rh[k] + qq[u]));
+          z0 = fmaf(kk, u0[k], z0);
+          z1 = fmaf(kk, u1[k], z1);
+        }
+      }
+      const float mx = fmaxf(z0, z1);
+      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+      const float inv = 1.f / (e0 + e1);
+      p0 = e0 * inv;
+      p1 = e1 * inv;
+      if (++ejj == Ne - 1) { ejj = 0; ++ei; }
+    }
+    s0 += p0;
+    s1 += p1;
+    const float w0 = wsum(p0), w1 = wsum(p1);
+    const int ht = hid[jp];
+    if (lane == 0 && ht >= 0 && ht < Nc) {
+      atomicAdd(&bins[2 * ht], qfix(w0));
+      atomicAdd(&bins[2 * ht + 1], qfix(w1));
+    }
+  }
+  if (live) {
+    const int hs = hid[ip];
+    if (hs >= 0 && hs < Nc) {
+      atomicAdd(&bins[2 * hs], qfix(s0));
+      atomicAdd(&bins[2 * hs + 1], qfix(s1));
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * Nc; c += NT)
+    if (bins[c]) atomicAdd(&ncacc[(size_t)b * 2 * Nc + c], bins[c]);
+}
+
+// ---------------------------------------------------------------------------------
+// kw_cross_fwd  grid (ceil(Nc/4), B), one wave per hunk c
+//   marshalling_B2 (model_2.py:146-158): n_c = [K_s x', K_t x', class part] with the
+//   class part = static relation counts (ncst) or the EE aggregate; then the hunk MLP
+//   first layer split per node (model_2.py:257-260):
+//     alpha_c = n_c V1[0:4] + V1[8] + c1,   beta_c = n_c V1[4:8]
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_cross_fwd(
+    const uint32_t* __restrict__ prep, const float* __restrict__ xv, const float* __restrict__ W,
+    Off o, int Ne, int Nc, const unsigned long long* __restrict__ ncacc,
+    float* __restrict__ nvec, float* __restrict__ alpha, float* __restrict__ beta) {
+  const PrepLayout PL = prep_layout(Ne, Nc);
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * NW + uni(threadIdx.x >> 6);
+  if (c >= Nc) return;   // wave-uniform; no block barrier below
+  const uint32_t* pp = prep + (size_t)b * PL.words;
+  const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks) + (size_t)c * Ne;
+  const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt) + (size_t)c * Ne;
+  const float* xb = xv + (size_t)b * Ne;
+  float a0 = 0.f, a1 = 0.f;
+  for (int I = lane; I < Ne; I += 64) {
+    const float xi = xb[I];
+    a0 = fmaf((float)ks[I], xi, a0);
+    a1 = fmaf((float)kt[I], xi, a1);
+  }
+  float nv[4];
+  nv[0] = wsum(a0);
+  nv[1] = wsum(a1);
+  if (ncacc) {
+    nv[2] = (float)((double)ncacc[((size_t)b * Nc + c) * 2] * (1.0 / FIX));
+    nv[3] = (float)((double)ncacc[((size_t)b * Nc + c) * 2 + 1] * (1.0 / FIX));
+  } else {
+    const float* ncst = reinterpret_cast<const float*>(pp + PL.ncst);
+    nv[2] = ncst[2 * c];
+    nv[3] = ncst[2 * c + 1];
+  }
+  if (lane < 4) nvec[((size_t)b * Nc + c) * 4 + lane] = nv[lane];
+  if (lane < H) {
+    const int k = lane;
+    float al = W[o.H1_W1 + 8 * H + k] + W[o.H1_B1 + k], be = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      al = fmaf(nv[m], W[o.H1_W1 + m * H + k], al);
+      be = fmaf(nv[m], W[o.H1_W1 + (4 + m) * H + k], be);
+    }
+    alpha[((size_t)b * Nc + c) * H + k] = al;
+    beta[((size_t)b * Nc + c) * H + k] = be;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_hunk_fwd  grid (tc, B, 2): z = 0 row pass (G), 1 column pass (H)
+//   mlp_hunk_B2 first layer relu sums (model_2.py:257-275):
+//     G_p = sum_{q!=p} relu(alpha_p + beta_q + y_pq delta),  H_q = sum_{p!=q} (same)
+//   epilogue: sigma_p = G_p M + s0, tau_q = H_q M + t0 (classifier first layer, 304-318)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_hunk_fwd(const uint32_t* __restrict__ ybits,
+                                                  const uint32_t* __restrict__ yT,
+                                                  const float* __restrict__ D, int Nc,
+                                                  const float* __restrict__ alpha,
+                                                  const float* __restrict__ beta,
+                                                  float* __restrict__ G, float* __restrict__ Hh,
+                                                  float* __restrict__ sig, float* __restrict__ tau) {
+#pragma clang fp contract(off)
+  __shared__ float buf[NW * TN * HP + TN * HP];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
+  const int lane = threadIdx.x & 63;
+  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
+  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
+  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  float ow[H], dl[H], acc[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    ow[k] = own[ncl * H + k];
+    dl[k] = D[D_DLT + k];
+    acc[k] = 0.f;
+  }
+  sweep(Nc, t0, [&](int m, bool self) {
+    const float yf = bitf(brow, m);
+    const bool on = !(self && m == nd);
+    const float* om = oth + (size_t)m * H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const float v = relu(fmaf(yf, dl[k], ow[k] + om[k]));
+      acc[k] += on ? v : 0.f;
+    }
+  });
+  float* res = buf + NW * TN * HP;
+  combine4(acc, buf, res);
+  float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
+  float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
+  const float* off = D + (z ? D_T0 : D_S0);
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float s = 0.f;
+    for (int l = 0; l < H; ++l) s = fmaf(res[n * HP + l], D[D_M + l * H + k], s);
+    gout[(t0 + n) * H + k] = res[n * HP + k];
+    sout[(t0 + n) * H + k] = s + off[k];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_hunk_cls  grid (tc, B): lane = hunk column q, waves split the rows p
+//   mlp_hunkedge_B2 (model_2.py:304-324) + softmax CE (115-118):
+//     kappa_pq = relu(sigma_p + tau_q + y_pq eps), z = kappa U2 + d2, CE = lse(z) - z_y
+//   TRAIN: gamma_pq = 10 / (B Pc) (p1 - y) = dL/dz1 (= -dL/dz0), parked for the backward;
+//   partial rows of dU2, dd2 and the CE sum
+// ---------------------------------------------------------------------------------
+template <bool TRAIN>
+__global__ __launch_bounds__(NT) void kw_hunk_cls(
+    const uint32_t* __restrict__ ybits, const float* __restrict__ W, Off o,
+    const float* __restrict__ D, int Nc, const float* __restrict__ sig,
+    const float* __restrict__ tau, float* __restrict__ probs, float* __restrict__ logits,
+    float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float red[NW * 22];
+  __shared__ float tot[22];
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  const int q = t0 + lane;
+  const bool live = q < Nc;
+  const int qc = live ? q : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const int Pc = Nc * (Nc - 1);
+  float tq[H], ep[H], u0[H], u1[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    tq[k] = tau[((size_t)b * Nc + qc) * H + k];
+    ep[k] = D[D_EPS + k];
+    u0[k] = W[o.H2_W2 + 2 * k];
+    u1[k] = W[o.H2_W2 + 2 * k + 1];
+  }
+  const float b0 = W[o.H2_B2], b1 = W[o.H2_B2 + 1];
+  float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
+  float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
+  float acc[22];   // 0: CE, 1: sum gamma, 2..21: sum kappa_k gamma
+#pragma unroll
+  for (int k = 0; k < 22; ++k) acc[k] = 0.f;
+  const int lo = (Nc * wv) / NW, hi = (Nc * (wv + 1)) / NW;
+  for (int p = lo; p < hi; ++p) {
+    const float* sp = sig + ((size_t)b * Nc + p) * H;
+    const float yf = bitf(ybits + ((size_t)b * Nc + p) * WC, qc);
+    float kk[H];
+    float z0 = b0, z1 = b1;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      kk[k] = relu(fmaf(yf, ep[k], sp[k] + tq[k]));
+      z0 = fmaf(kk[k], u0[k], z0);
+      z1 = fmaf(kk[k], u1[k], z1);
+    }
+    const bool valid = live && q != p;
+    if (valid) {
+      const float mx = fmaxf(z0, z1);
+      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+      const float ssum = e0 + e1, inv = 1.f / ssum;
+      const float p0 = e0 * inv, p1 = e1 * inv;
+      const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
+      if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
+      if (lgb) { lgb[r] = z0; lgb[Pc + r] = z1; }
+      acc[0] += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+      if constexpr (TRAIN) {
+        const float g = ce_scale * (p1 - yf);
+        gam[((size_t)b * Nc + p) * Nc + q] = g;
+        acc[1] += g;
+#pragma unroll
+        for (int k = 0; k < H; ++k) acc[2 + k] = fmaf(kk[k], g, acc[2 + k]);
+      }
+    } else if (TRAIN && live) {
+      gam[((size_t)b * Nc + p) * Nc + q] = 0.f;   // defined diagonal, read by the passes
+    }
+  }
+  block_sum<22>(acc, red, tot);
+  const int row = b * tc + blockIdx.x;
+  if (threadIdx.x == 0) put(part, sg.s[SG_CE], 0, row, tot[0]);
+  if constexpr (TRAIN) {
+    const int t = threadIdx.x;
+    if (t < H) {
+      put(part, sg.s[SG_CLS], 2 * t, row, -tot[2 + t]);       // dU2[k][0]
+      put(part, sg.s[SG_CLS], 2 * t + 1, row, tot[2 + t]);    // dU2[k][1]
+    } else if (t < H + 2) {
+      const int c = t - H;                                      // dd2
+      put(part, sg.s[SG_CLS], 2 * H + c, row, c ? tot[1] : -tot[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_hunk_clsb  grid (tc, B, 2): classifier backward (model_2.py:304-321)
+//   e_pqk = [kappa_pqk > 0] gamma_pq;  row pass: Dsig_p = c (.) sum_q e_pq, ysum = sum y e
+//   column pass: Dtau_q = c (.) sum_p e_pq.  Epilogue: dG = Dsig M^T (dH = Dtau M^T) and
+//   the partial rows of dU1 (rows 0..1 from the row pass, rows 2..21 through
+//   X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p), dd1, dV2 and dc2 (model_2.py:265-275).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_hunk_clsb(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ W, Off o, const float* __restrict__ D, int Nc,
+    const float* __restrict__ sig, const float* __restrict__ tau, const float* __restrict__ gam,
+    const float* __restrict__ G, const float* __restrict__ Hh, float* __restrict__ Dsig,
+    float* __restrict__ Dtau, float* __restrict__ dG, float* __restrict__ dH,
+    float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float buf[NW * TN * HP];
+  __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
+  __shared__ float X[H * H], sumD[H], ysum[H];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const float* own = (z ? tau : sig) + (size_t)b * Nc * H;
+  const float* oth = (z ? sig : tau) + (size_t)b * Nc * H;
+  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  const float* gb = gam + (size_t)b * Nc * Nc;
+  float ow[H], ep[H], acc[H], ya[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    ow[k] = own[ncl * H + k];
+    ep[k] = D[D_EPS + k];
+    acc[k] = 0.f;
+    ya[k] = 0.f;
+  }
+  sweep(Nc, t0, [&](int m, bool) {   // gamma's diagonal is 0: no self mask needed
+    const float yf = bitf(brow, m);
+    const float g = z ? gb[(size_t)m * Nc + ncl] : gb[(size_t)ncl * Nc + m];
+    const float* om = oth + (size_t)m * H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const float e = (fmaf(yf, ep[k], ow[k] + om[k]) > 0.f) ? g : 0.f;
+      acc[k] += e;
+      ya[k] = fmaf(yf, e, ya[k]);
+    }
+  });
+  combine4(acc, buf, res);
+  if (z == 0) combine4(ya, buf, yres);
+  const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
+  float* dout = (z ? Dtau : Dsig) + (size_t)b * Nc * H;
+  float* gout = (z ? dH : dG) + (size_t)b * Nc * H;
+  for (int e = threadIdx.x; e < TN * H; e += NT) {   // D = c (.) sums; padding rows -> 0
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Nc;
+    const float d = in ? res[n * HP + k] * D[D_CV + k] : 0.f;
+    res[n * HP + k] = d;
+    Gt[n * HP + k] = in ? gsrc[(t0 + n) * H + k] : 0.f;
+    if (z == 0 && !in) yres[n * HP + k] = 0.f;
+    if (in) dout[(t0 + n) * H + k] = d;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TN * H; e += NT) {   // dG_n[l] = sum_k M[l][k] D_n[k]
+    const int n = e / H, l = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float s = 0.f;
+    for (int k = 0; k < H; ++k) s = fmaf(D[D_M + l * H + k], res[n * HP + k], s);
+    gout[(t0 + n) * H + l] = s;
+  }
+  for (int e = threadIdx.x; e < H * H; e += NT) {    // X_blk = sum_n G_n (x) D_n
+    const int l = e / H, k = e - l * H;
+    float s = 0.f;
+    for (int n = 0; n < TN; ++n) s = fmaf(Gt[n * HP + l], res[n * HP + k], s);
+    X[e] = s;
+  }
+  if (threadIdx.x < H) {
+    const int k = threadIdx.x;
+    float s = 0.f, y = 0.f;
+    for (int n = 0; n < TN; ++n) {
+      s += res[n * HP + k];
+      if (z == 0) y += yres[n * HP + k];
+    }
+    sumD[k] = s;
+    ysum[k] = y;
+  }
+  __syncthreads();
+  const int row = (b * tc + blockIdx.x) * 2 + z;
+  const float Nc1 = (float)(Nc - 1);
+  const Seg& s2 = sg.s[SG_CLSB_H2];
+  const Seg& s1 = sg.s[SG_CLSB_H1];
+  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += NT) {
+    if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
+      const int m = e / H, k = e - m * H;
+      float a = Nc1 * W[o.H1_B2 + m] * sumD[k];
+      for (int l = 0; l < H; ++l) a = fmaf(W[o.H1_W2 + l * H + m], X[l * H + k], a);
+      put(part, s2, (2 + m) * H + k, row, a);
+    } else if (e < 2 * H * H) {   // dV2[l][m] = sum_k X[l][k] U1e[m][k]
+      const int f = e - H * H, l = f / H, m = f - l * H;
+      float a = 0.f;
+      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], W[o.H2_W1 + (2 + m) * H + k], a);
+      put(part, s1, f, row, a);
+    } else if (e < 2 * H * H + H) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
+      const int m = e - 2 * H * H;
+      float a = 0.f;
+      for (int k = 0; k < H; ++k) a = fmaf(W[o.H2_W1 + (2 + m) * H + k], sumD[k], a);
+      put(part, s1, H * H + m, row, Nc1 * a);
+    } else {                      // dU1[0], dU1[1], dd1 (row pass only)
+      const int f = e - 2 * H * H - H;   // 0 .. 2H-1
+      const int k = f % H;
+      const float dd1 = z == 0 ? sumD[k] : 0.f;
+      const float dy1 = z == 0 ? D[D_CV + k] * ysum[k] : 0.f;
+      if (f < H) {
+        put(part, s2, k, row, dd1 - dy1);
+        put(part, s2, H + k, row, dy1);
+      } else {
+        put(part, s2, 22 * H + k, row, dd1);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_hunk_mlpb  grid (tc, B, 2): hunk pair MLP backward (model_2.py:257-275)
+//   dz_pq = [alpha_p + beta_q + y delta > 0] (dG_p + dH_q)
+//   row pass: Dalpha_p = sum_q dz, sum y dz;  column pass: Dbeta_q = sum_p dz
+//   partial rows of dV1 (rows 0..3 / 4..7 / 8, 9) and dc1
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_hunk_mlpb(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
+    const float* __restrict__ nvec, float* __restrict__ Dal, float* __restrict__ Dbe,
+    float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float buf[NW * TN * HP];
+  __shared__ float res[TN * HP], yres[TN * HP], nt[TN * 4];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
+  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
+  const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
+  const float* woth = (z ? dG : dH) + (size_t)b * Nc * H;
+  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  float ow[H], wo[H], dl[H], acc[H], ya[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    ow[k] = own[ncl * H + k];
+    wo[k] = wown[ncl * H + k];
+    dl[k] = D[D_DLT + k];
+    acc[k] = 0.f;
+    ya[k] = 0.f;
+  }
+  sweep(Nc, t0, [&](int m, bool self) {
+    const float yf = bitf(brow, m);
+    const bool on = !(self && m == nd);
+    const float* om = oth + (size_t)m * H;
+    const float* wm = woth + (size_t)m * H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const bool pos = on && fmaf(yf, dl[k], ow[k] + om[k]) > 0.f;
+      const float dz = pos ? wo[k] + wm[k] : 0.f;
+      acc[k] += dz;
+      ya[k] = fmaf(yf, dz, ya[k]);
+    }
+  });
+  combine4(acc, buf, res);
+  if (z == 0) combine4(ya, buf, yres);
+  float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H;
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Nc;
+    if (!in) { res[n * HP + k] = 0.f; yres[n * HP + k] = 0.f; }
+    else dout[(t0 + n) * H + k] = res[n * HP + k];
+  }
+  for (int e = threadIdx.x; e < TN * 4; e += NT)
+    nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
+  __syncthreads();
+  const int row = (b * tc + blockIdx.x) * 2 + z;
+  const Seg& s = sg.s[SG_MLPB];
+  for (int e = threadIdx.x; e < 11 * H; e += NT) {   // rows 0..9 of V1, then c1
+    const int l = e / H, k = e - l * H;
+    float a = 0.f;
+    if (l < 8) {
+      const int m = l & 3;
+      if ((l >> 2) == z)
+        for (int n = 0; n < TN; ++n) a = fmaf(nt[n * 4 + m], res[n * HP + k], a);
+    } else if (z == 0) {
+      float sd = 0.f, sy = 0.f;
+      for (int n = 0; n < TN; ++n) { sd += res[n * HP + k]; sy += yres[n * HP + k]; }
+      a = l == 8 ? sd - sy : (l == 9 ? sy : sd);
+    }
+    put(part, s, e, row, a);
+  }
+}
+
+// kw_dn  grid (tc, B): dn_c[m] = sum_k V1[m][k] Dalpha_c[k] + V1[4+m][k] Dbeta_c[k]
+__global__ __launch_bounds__(NT) void kw_dn(const float* __restrict__ W, Off o, int Nc,
+                                            const float* __restrict__ Dal,
+                                            const float* __restrict__ Dbe,
+                                            float* __restrict__ dn) {
+  const int b = blockIdx.y, c = blockIdx.x * TN + (threadIdx.x & 63), m = threadIdx.x >> 6;
+  if (c >= Nc) return;
+  const float* da = Dal + ((size_t)b * Nc + c) * H;
+  const float* db = Dbe + ((size_t)b * Nc + c) * H;
+  float a = 0.f;
+  for (int k = 0; k < H; ++k)
+    a = fmaf(W[o.H1_W1 + m * H + k], da[k], fmaf(W[o.H1_W1 + (4 + m) * H + k], db[k], a));
+  dn[((size_t)b * Nc + c) * 4 + m] = a;
+}
+
+// ---------------------------------------------------------------------------------
+// kw_node_bwd  grid (te, B): cross-graph + mlp2_entity_B1 backward (model_2.py:146-150,
+// 190-205, 181-188): dx'_I = sum_c dn_c[0] K_s[c][I] + dn_c[1] K_t[c][I];
+// do = [o > 0] dx';  dq = [h > 0] w2' do;  dE = dq W1'[1:]^T;  rho = dP = dE W5^T.
+// Partial rows of dW1', db1', dw2', db2', dW5, db5.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_node_bwd(
+    const uint32_t* __restrict__ prep, const float* __restrict__ x, const float* __restrict__ W,
+    Off o, int Ne, int Nc, const float* __restrict__ dn, const float* __restrict__ ov,
+    const float* __restrict__ P, const float* __restrict__ Eb, const float* __restrict__ hE,
+    float* __restrict__ rhoE, float* __restrict__ part, Segs sg) {
+  __shared__ float dxq[NW * TN], xs[TN], dov[TN];
+  __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
+  const PrepLayout PL = prep_layout(Ne, Nc);
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
+  const int lane = t & 63, w = t >> 6;
+  const int I = t0 + lane;
+  const uint32_t* pp = prep + (size_t)b * PL.words;
+  {
+    const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
+    const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
+    const float* dnb = dn + (size_t)b * Nc * 4;
+    const int c0 = (Nc * w) / NW, c1 = (Nc * (w + 1)) / NW;
+    float a = 0.f;
+    if (I < Ne)
+      for (int c = c0; c < c1; ++c) {
+        a = fmaf(dnb[4 * c], (float)ks[(size_t)c * Ne + I], a);
+        a = fmaf(dnb[4 * c + 1], (float)kt[(size_t)c * Ne + I], a);
+      }
+    dxq[w * TN + lane] = a;
+  }
+  const size_t base = ((size_t)b * Ne + t0) * H;
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Ne;
+    Pt[n * HP + k] = in ? P[base + e] : 0.f;
+    Et[n * HP + k] = in ? Eb[base + e] : 0.f;
+    ht[n * HP + k] = in ? hE[base + e] : 0.f;
+  }
+  __syncthreads();
+  if (t < TN) {
+    const bool in = t0 + t < Ne;
+    const float d = ((dxq[t] + dxq[TN + t]) + dxq[2 * TN + t]) + dxq[3 * TN + t];
+    dov[t] = (in && ov[(size_t)b * Ne + t0 + t] > 0.f) ? d : 0.f;
+    xs[t] = in ? x[(size_t)b * Ne + t0 + t] : 0.f;
+  }
+  __syncthreads();
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    dq[n * HP + k] = ht[n * HP + k] > 0.f ? W[o.E3_W2 + k] * dov[n] : 0.f;
+  }
+  __syncthreads();
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, m = e - n * H;
+    float a = 0.f;
+    for (int k = 0; k < H; ++k) a = fmaf(dq[n * HP + k], W[o.E3_W1 + (1 + m) * H + k], a);
+    dE[n * HP + m] = a;
+  }
+  __syncthreads();
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, l = e - n * H;
+    if (t0 + n >= Ne) continue;
+    float a = 0.f;
+    for (int m = 0; m < H; ++m) a = fmaf(dE[n * HP + m], W[o.E1_W5 + l * H + m], a);
+    rhoE[base + e] = a;
+  }
+  const int row = b * te + blockIdx.x;
+  const Seg& s3 = sg.s[SG_E3];
+  const Seg& s5 = sg.s[SG_E1W5];
+  const float twoNe1 = 2.f * (float)(Ne - 1);
+  for (int e = t; e < 461 + 420; e += NT) {
+    float a = 0.f;
+    if (e < 420) {                 // dW1'[l][k]: l = 0 -> x, l >= 1 -> E_bar[l-1]
+      const int l = e / H, k = e - l * H;
+      for (int n = 0; n < TN; ++n) a = fmaf(l ? Et[n * HP + l - 1] : xs[n], dq[n * HP + k], a);
+      put(part, s3, e, row, a);
+    } else if (e < 440) {          // db1'
+      const int k = e - 420;
+      for (int n = 0; n < TN; ++n) a += dq[n * HP + k];
+      put(part, s3, e, row, a);
+    } else if (e < 460) {          // dw2'
+      const int k = e - 440;
+      for (int n = 0; n < TN; ++n) a = fmaf(ht[n * HP + k], dov[n], a);
+      put(part, s3, e, row, a);
+    } else if (e == 460) {         // db2'
+      for (int n = 0; n < TN; ++n) a += dov[n];
+      put(part, s3, e, row, a);
+    } else {
+      const int f = e - 461;
+      if (f < 400) {               // dW5[l][m] = sum_n P[n][l] dE[n][m]
+        const int l = f / H, m = f - l * H;
+        for (int n = 0; n < TN; ++n) a = fmaf(Pt[n * HP + l], dE[n * HP + m], a);
+      } else {                     // db5[m] = 2(Ne-1) sum_n dE[n][m]
+        const int m = f - 400;
+        for (int n = 0; n < TN; ++n) a += dE[n * HP + m];
+        a *= twoNe1;
+      }
+      put(part, s5, f, row, a);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_ent_bwd  grid (te, B): mlp_entity_B1 first layer backward (model_2.py:165-170):
+//   dz_ij = [z_ij > 0] (rho_i + rho_j);  dW1 = [sum x_i dz, sum x_j dz, sum (1-a) dz,
+//   sum a dz], db1 = sum dz.  Lane = row i, the j sweep split over the waves.
+// ---------------------------------------------------------------------------------
+template <int MODE>   // 0: entity stage (rho_i + rho_j), 1: EE (phi_i + psi_j)
+__global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
+                                                   const uint32_t* __restrict__ abits,
+                                                   const float* __restrict__ W, Off o, int Ne,
+                                                   const float* __restrict__ ra,
+                                                   const float* __restrict__ rb,
+                                                   float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float red[NW * 4 * H];
+  __shared__ float tot[4 * H];
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  const int i = t0 + lane;
+  const bool live = i < Ne;
+  const int ic = live ? i : Ne - 1;
+  const int WE = (Ne + 31) >> 5;
+  const float* xb = x + (size_t)b * Ne;
+  const float xi = xb[ic];
+  float wr[H], ur[H], dd[H], ri[H];
+  for (int k = 0; k < H; ++k) {
+    if constexpr (MODE == 0) {
+      const float w0 = W[o.E1_W1 + k], w2 = W[o.E1_W1 + 2 * H + k];
+      wr[k] = W[o.E1_W1 + H + k];
+      dd[k] = W[o.E1_W1 + 3 * H + k] - w2;
+      ur[k] = fmaf(xi, w0, w2 + W[o.E1_B1 + k]);
+    } else {
+      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
+      wr[k] = w;
+      dd[k] = W[o.EE_W12 + H + k] - w20;
+      ur[k] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
+    }
+    ri[k] = ra[((size_t)b * Ne + ic) * H + k];
+  }
+  float S1[H], S2[H], S3[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) { S1[k] = 0.f; S2[k] = 0.f; S3[k] = 0.f; }
+  const uint32_t* rowb = abits + ((size_t)b * Ne + ic) * WE;
+  const float* rbb = rb + (size_t)b * Ne * H;
+  sweep(Ne, t0, [&](int j, bool self) {
+    const float xj = xb[j];
+    const float af = bitf(rowb, j);
+    const bool on = live && !(self && j == i);
+    const float* rj = rbb + (size_t)j * H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const float zz = fmaf(af, dd[k], fmaf(xj, wr[k], ur[k]));
+      const float g = (on && zz > 0.f) ? ri[k] + rj[k] : 0.f;
+      S1[k] = fmaf(xj, g, S1[k]);
+      S2[k] += g;
+      S3[k] = fmaf(af, g, S3[k]);
+    }
+  });
+  float v[4 * H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    v[k] = xi * S2[k];
+    v[H + k] = S1[k];
+    v[2 * H + k] = S2[k];
+    v[3 * H + k] = S3[k];
+  }
+  block_sum<4 * H>(v, red, tot);
+  const int row = b * te + blockIdx.x;
+  const int t = threadIdx.x;
+  if (t < H) {
+    const float s0 = tot[t], s1 = tot[H + t], s2 = tot[2 * H + t], s3 = tot[3 * H + t];
+    if constexpr (MODE == 0) {
+      const Seg& s = sg.s[SG_E1W1];
+      put(part, s, t, row, s0);
+      put(part, s, H + t, row, s1);
+      put(part, s, 2 * H + t, row, s2 - s3);
+      put(part, s, 3 * H + t, row, s3);
+      put(part, s, 4 * H + t, row, s2);
+    } else {   // shared w1_1 sees both slices: sum dz (x_i + x_j)
+      const Seg& s = sg.s[SG_EEW11];
+      put(part, s, t, row, s0 + s1);
+      put(part, s, H + t, row, s2 - s3);
+      put(part, s, 2 * H + t, row, s3);
+      put(part, s, 3 * H + t, row, s2);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_ee_clsb  grid (te, B, 2): entity-edge classifier backward (model_4.py:286-304)
+//   dp_r[m] = dn[hid i'(r)][2+m] + dn[hid j'(r)][2+m];  dz1 = p0 p1 (dp1 - dp0) = -dz0
+//   g_ijk = [kappa'_ijk > 0] (U2'[k][1] - U2'[k][0]) dz1
+//   z = 0 column pass (lane = column j): dgam_j = sum_i g, classifier partial rows
+//   z = 1 row pass    (lane = row i)   : drho_i = sum_j g
+//   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_ee_clsb(
+    const uint32_t* __restrict__ abits, const int32_t* __restrict__ hidg,
+    const int32_t* __restrict__ nleng, const float* __restrict__ W, Off o,
+    const float* __restrict__ D, int Ne, int Nc, const float* __restrict__ rho,
+    const float* __restrict__ gmm, const float* __restrict__ dn, float* __restrict__ drho,
+    float* __restrict__ dgam, float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  extern __shared__ float dyn[];
+  __shared__ float buf[NW * TN * HP];
+  __shared__ float res[TN * HP];
+  __shared__ float red[NW * 41];
+  __shared__ float tot[41];
+  int* hl = reinterpret_cast<int*>(dyn);
+  float* dnl = dyn + Ne;
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+  const int lane = threadIdx.x & 63;
+  int n = nleng[b];
+  n = n < 0 ? 0 : (n > Ne ? Ne : n);
+  const int nrel = n >= 2 ? n * (n - 1) : 0;
+  for (int e = threadIdx.x; e < Ne; e += NT) {
+    const int h = hidg[(size_t)b * Ne + e];
+    hl[e] = (h >= 0 && h < Nc) ? h : -1;
+  }
+  for (int e = threadIdx.x; e < 2 * Nc; e += NT) dnl[e] = dn[((size_t)b * Nc + e / 2) * 4 + 2 + (e & 1)];
+  __syncthreads();
+  const int WE = (Ne + 31) >> 5;
+  const int nd = t0 + lane, ncl = nd < Ne ? nd : Ne - 1;
+  const float* rbase = (z ? rho : gmm) + (size_t)b * Ne * H;   // own operand
+  const float* obase = (z ? gmm : rho) + (size_t)b * Ne * H;   // swept operand
+  float ow[H], dl[H], cE[H], u0[H], u1[H], acc[H], zk[H], ag[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    ow[k] = rbase[(size_t)ncl * H + k];
+    dl[k] = D[D_EED + k];
+    cE[k] = D[D_EEC + k];
+    u0[k] = W[o.EC_W2 + 2 * k];
+    u1[k] = W[o.EC_W2 + 2 * k + 1];
+    acc[k] = 0.f;
+    zk[k] = 0.f;
+    ag[k] = 0.f;
+  }
+  const float b0 = W[o.EC_B2], b1 = W[o.EC_B2 + 1];
+  const int dn1 = n - 1 > 0 ? n - 1 : 1;
+  const float inv = 1.f / (float)dn1;
+  float sdl = 0.f;
+  // rows that hold relations r < nrel
+  const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
+  const int Nsw = z ? Ne : rows;             // swept index range
+  if (z == 1 && t0 >= rows) {                // whole tile of rows holds no relation
+  } else {
+    sweep(Nsw, t0, [&](int m, bool) {
+      const int i = z ? ncl : m, j = z ? m : ncl;
+      const int r = i * (Ne - 1) + j - (j > i ? 1 : 0);
+      const bool valid = nd < Ne && i != j && r < nrel;
+      float dp0 = 0.f, dp1 = 0.f;
+      if (valid) {
+        int ip, jj;
+        divmod24(r, dn1, inv, ip, jj);
+        const int jp = jj + (jj >= ip ? 1 : 0);
+        const int hs = hl[ip], ht = hl[jp];
+        if (hs >= 0) { dp0 += dnl[2 * hs]; dp1 += dnl[2 * hs + 1]; }
+        if (ht >= 0) { dp0 += dnl[2 * ht]; dp1 += dnl[2 * ht + 1]; }
+      }
+      const float af = bitf(abits + ((size_t)b * Ne + i) * WE, j);
+      const float* om = obase + (size_t)m * H;
+      float pre[H];
+      float z0 = b0, z1 = b1;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float rr = z ? ow[k] : om[k];   // rho_i + gam_j, same order as kw_ee_fwd
+        const float gg = z ? om[k] : ow[k];
+        pre[k] = fmaf(af, dl[k], rr + gg);
+        const float kk = relu(pre[k]);
+        z0 = fmaf(kk, u0[k], z0);
+        z1 = fmaf(kk, u1[k], z1);
+      }
+      const float mx = fmaxf(z0, z1);
+      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+      const float iv = 1.f / (e0 + e1);
+      const float p0 = e0 * iv, p1 = e1 * iv;
+      const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
+      sdl += d1;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float g = pre[k] > 0.f ? cE[k] * d1 : 0.f;
+        acc[k] += g;
+        zk[k] = fmaf(relu(pre[k]), d1, zk[k]);
+        ag[k] = fmaf(af, g, ag[k]);
+      }
+    });
+  }
+  combine4(acc, buf, res);
+  float* dout = (z ? drho : dgam) + (size_t)b * Ne * H;
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int nn = e / H, k = e - nn * H;
+    if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = res[nn * HP + k];
+  }
+  if (z == 1) return;   // block-uniform; partial rows come from the column pass
+  float v[41];
+#pragma unroll
+  for (int k = 0; k < H; ++k) { v[k] = zk[k]; v[H + k] = ag[k]; }
+  v[40] = sdl;
+  block_sum<41>(v, red, tot);
+  const int row = b * te + blockIdx.x;
+  const int t = threadIdx.x;
+  if (t < H) {
+    float sg_ = 0.f;   // sum of g over the tile = sum of the combined column sums
+    for (int nn = 0; nn < TN; ++nn) sg_ += (t0 + nn < Ne) ? res[nn * HP + t] : 0.f;
+    const Seg& sa = sg.s[SG_ECW1A];
+    const Seg& sb = sg.s[SG_ECB1];
+    put(part, sa, t, row, sg_ - tot[H + t]);          // P1[0] ([a = 0] input)
+    put(part, sa, H + t, row, tot[H + t]);            // P1[1] ([a = 1] input)
+    put(part, sb, t, row, sg_);                       // p1 bias
+    put(part, sb, H + 2 * t, row, -tot[t]);           // U2'[k][0]
+    put(part, sb, H + 2 * t + 1, row, tot[t]);        // U2'[k][1]
+  }
+  if (t == 0) {
+    const Seg& sb = sg.s[SG_ECB1];
+    put(part, sb, 3 * H, row, -tot[40]);
+    put(part, sb, 3 * H + 1, row, tot[40]);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_ee_nodeb  grid (te, B): dR = U1e' drho, dC = U1e' dgam;  phi = Q2 dR, psi = Q2 dC
+// (model_4.py:232-243 backward); partial rows of dU1e' (classifier rows 2..21),
+// dQ2 = sum R1 (x) dR + C1 (x) dC, dq2 = (Ne-1) sum (dR + dC)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void kw_ee_nodeb(
+    const float* __restrict__ W, Off o, int Ne, const float* __restrict__ R1,
+    const float* __restrict__ C1, const float* __restrict__ Rn, const float* __restrict__ Cn,
+    const float* __restrict__ drho, const float* __restrict__ dgam, float* __restrict__ phi,
+    float* __restrict__ psi, float* __restrict__ part, Segs sg) {
+  __shared__ float A[TN * HP], Bq[TN * HP], R1t[TN * HP], C1t[TN * HP], Rt[TN * HP],
+      Ct[TN * HP], dR[TN * HP], dC[TN * HP];
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
+  const size_t base = ((size_t)b * Ne + t0) * H;
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Ne;
+    A[n * HP + k] = in ? drho[base + e] : 0.f;
+    Bq[n * HP + k] = in ? dgam[base + e] : 0.f;
+    R1t[n * HP + k] = in ? R1[base + e] : 0.f;
+    C1t[n * HP + k] = in ? C1[base + e] : 0.f;
+    Rt[n * HP + k] = in ? Rn[base + e] : 0.f;
+    Ct[n * HP + k] = in ? Cn[base + e] : 0.f;
+  }
+  __syncthreads();
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, m = e - n * H;
+    float a = 0.f, c = 0.f;
+    for (int k = 0; k < H; ++k) {
+      const float u = W[o.EC_W1 + (2 + m) * H + k];
+      a = fmaf(u, A[n * HP + k], a);
+      c = fmaf(u, Bq[n * HP + k], c);
+    }
+    dR[n * HP + m] = a;
+    dC[n * HP + m] = c;
+  }
+  __syncthreads();
+  for (int e = t; e < TN * H; e += NT) {
+    const int n = e / H, l = e - n * H;
+    if (t0 + n >= Ne) continue;
+    float a = 0.f, c = 0.f;
+    for (int m = 0; m < H; ++m) {
+      const float q = W[o.EE_W2 + l * H + m];
+      a = fmaf(q, dR[n * HP + m], a);
+      c = fmaf(q, dC[n * HP + m], c);
+    }
+    phi[base + e] = a;
+    psi[base + e] = c;
+  }
+  const int row = b * te + blockIdx.x;
+  const Seg& s1 = sg.s[SG_ECW1E];
+  const Seg& s2 = sg.s[SG_EEW2];
+  const float Ne1 = (float)(Ne - 1);
+  for (int e = t; e < 400 + 420; e += NT) {
+    float a = 0.f;
+    if (e < 400) {
+      const int m = e / H, k = e - m * H;
+      for (int n = 0; n < TN; ++n)
+        a = fmaf(Rt[n * HP + m], A[n * HP + k], fmaf(Ct[n * HP + m], Bq[n * HP + k], a));
+      put(part, s1, e, row, a);
+    } else {
+      const int f = e - 400;
+      if (f < 400) {
+        const int l = f / H, m = f - l * H;
+        for (int n = 0; n < TN; ++n)
+          a = fmaf(R1t[n * HP + l], dR[n * HP + m], fmaf(C1t[n * HP + l], dC[n * HP + m], a));
+      } else {
+        const int m = f - 400;
+        for (int n = 0; n < TN; ++n) a += dR[n * HP + m] + dC[n * HP + m];
+        a *= Ne1;
+      }
+      put(part, s2, f, row, a);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_grad_reduce  grid (count): one wave per parameter p = p_begin + blockIdx.x; lanes
+// stride over the partial rows of p's segment in a fixed order, xor-butterfly total.
+// Parameters without a segment get 0 (data-independent: map_theta*, model_3's unused
+// entity-edge blocks).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ part, Segs sg,
+                                                     int p_begin, float* __restrict__ out) {
+  const int p = p_begin + blockIdx.x, lane = threadIdx.x;
+  float a = 0.f;
+  for (int s = 0; s < sg.count; ++s) {
+    const Seg& g = sg.s[s];
+    if (g.n > 0 && p >= g.p0 && p < g.p0 + g.n) {
+      const float* src = part + g.off + (long long)(p - g.p0) * g.rows;
+      for (int r = lane; r < g.rows; r += 64) a += src[r];
+      break;
+    }
+  }
+  a = wsum(a);
+  if (lane == 0) out[blockIdx.x] = a;
+}
+
+// transposed class bits: out[b][j][w] bit l = in[b][32w + l][j]
+__global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
+                                                uint32_t* __restrict__ out, int N) {
+  const int b = blockIdx.y, W_ = (N + 31) >> 5;
+  const uint32_t* ib = in + (size_t)b * N * W_;
+  for (int e = blockIdx.x * NT + threadIdx.x; e < N * W_; e += gridDim.x * NT) {
+    const int j = e / W_, w = e - j * W_;
+    uint32_t bits = 0;
+    for (int l = 0; l < 32; ++l) {
+      const int i = 32 * w + l;
+      if (i < N && i != j) bits |= ((ib[(size_t)i * W_ + (j >> 5)] >> (j & 31)) & 1u) << l;
+    }
+    out[(size_t)b * N * W_ + e] = bits;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------
+struct WideWork {
+  size_t xp, ov, P, Eb, hE, rhoE;                 // entity stage   [B][Ne](*H)
+  size_t R1, C1, Rn, Cn, rho, gmm, drho, dgam, phi, psi;   // EE     [B][Ne][H]
+  size_t ncacc;                                   // u64 [B][Nc][2]
+  size_t nvec, alpha, beta, G, Hh, sig, tau, Dsig, Dtau, dG, dH, Dal, Dbe, dn;   // hunk
+  size_t gam;                                     // [B][Nc][Nc]
+  size_t D;                                       // derived weights
+  size_t part;                                    // partial rows
+  Segs segs;
+  size_t total;
+};
+
+bool has_ent(int v) { return v == 2 || v == 4; }
+bool has_ee(int v) { return v == 4; }
+
+WideWork wide_layout(const hdg_shape* s) {
+  WideWork w;
+  memset(&w, 0, sizeof(w));
+  const size_t B = s->batch, Ne = s->ne, Nc = s->nc;
+  const int v = s->variant;
+  const Off o = param_offsets(v);
+  size_t off = 0;
+  auto take = [&](size_t n) { const size_t r = off; off += (n + 63) & ~(size_t)63; return r; };
+  const size_t NEH = B * Ne * H, NCH = B * Nc * H;
+  if (has_ent(v)) {
+    w.xp = take(B * Ne); w.ov = take(B * Ne);
+    w.P = take(NEH); w.Eb = take(NEH); w.hE = take(NEH); w.rhoE = take(NEH);
+  }
+  if (has_ee(v)) {
+    w.R1 = take(NEH); w.C1 = take(NEH); w.Rn = take(NEH); w.Cn = take(NEH);
+    w.rho = take(NEH); w.gmm = take(NEH); w.drho = take(NEH); w.dgam = take(NEH);
+    w.phi = take(NEH); w.psi = take(NEH);
+    w.ncacc = take(B * Nc * 4);
+  }
+  w.nvec = take(B * Nc * 4);
+  w.alpha = take(NCH); w.beta = take(NCH); w.G = take(NCH); w.Hh = take(NCH);
+  w.sig = take(NCH); w.tau = take(NCH); w.Dsig = take(NCH); w.Dtau = take(NCH);
+  w.dG = take(NCH); w.dH = take(NCH); w.Dal = take(NCH); w.Dbe = take(NCH);
+  w.dn = take(B * Nc * 4);
+  w.gam = take(B * Nc * Nc);
+  w.D = take(D_WORDS);
+  const int te = (int)((Ne + TN - 1) / TN), tc = (int)((Nc + TN - 1) / TN);
+  const int rc = (int)B * tc, re = (int)B * te;
+  auto seg = [&](int id, int p0, int n, int rows) {
+    w.segs.s[id].p0 = p0;
+    w.segs.s[id].n = n;
+    w.segs.s[id].rows = rows;
+    w.segs.s[id].off = (long long)take((size_t)n * rows);
+  };
+  seg(SG_CLS, o.H2_W2, 42, rc);
+  seg(SG_CE, o.NP, 1, rc);
+  seg(SG_CLSB_H2, o.H2_W1, 460, 2 * rc);
+  seg(SG_CLSB_H1, o.H1_W2, 420, 2 * rc);
+  seg(SG_MLPB, o.H1_W1, 220, 2 * rc);
+  if (has_ent(v)) {
+    seg(SG_E3, o.E3_W1, 461, re);
+    seg(SG_E1W5, o.E1_W5, 420, re);
+    seg(SG_E1W1, o.E1_W1, 100, re);
+  }
+  if (has_ee(v)) {
+    seg(SG_ECW1A, o.EC_W1, 40, re);
+    seg(SG_ECB1, o.EC_B1, 62, re);
+    seg(SG_ECW1E, o.EC_W1 + 40, 400, re);
+    seg(SG_EEW2, o.EE_W2, 420, re);
+    seg(SG_EEW11, o.EE_W11, 80, re);
+  }
+  w.segs.count = SG_COUNT;
+  w.part = 0;   // segment offsets are absolute (floats from the workspace base)
+  w.total = off;
+  return w;
+}
+
+#define WTRY(expr)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail((int)e_, "%s: %s", #expr, hipGetErrorString(e_));   \
+  } while (0)
+
+}  // namespace
+
+size_t wide_workspace_bytes(const hdg_shape* s) { return wide_layout(s).total * sizeof(float); }
+
+size_t wide_prep_bytes(const hdg_shape* s) {
+  const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
+  return (B * prep_layout(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
+}
+
+int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
+  WTRY(launch_prep_maps(s, bt, st));
+  uint32_t* aT = (uint32_t*)bt->prep + (size_t)s->batch * prep_layout(s->ne, s->nc).words;
+  uint32_t* yT = aT + (size_t)s->batch * s->ne * ((s->ne + 31) / 32);
+  hipLaunchKernelGGL(kw_prep_T, dim3(8, s->batch), dim3(NT), 0, st, bt->abits, aT, s->ne);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_prep_T, dim3(4, s->batch), dim3(NT), 0, st, bt->ybits, yT, s->nc);
+  WTRY(hipGetLastError());
+  return 0;
+}
+
+int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
+             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st) {
+  const int B = s->batch, Ne = s->ne, Nc = s->nc, v = s->variant;
+  const Off o = param_offsets(v);
+  const WideWork w = wide_layout(s);
+  float* ws = (float*)workspace;
+  const uint32_t* prep = (const uint32_t*)bt->prep;
+  const uint32_t* aT = prep + (size_t)B * prep_layout(Ne, Nc).words;
+  const uint32_t* yT = aT + (size_t)B * Ne * ((Ne + 31) / 32);
+  const int te = (Ne + TN - 1) / TN, tc = (Nc + TN - 1) / TN;
+  const bool ent = has_ent(v), ee = has_ee(v);
+  const int bg = s->batch_global > 0 ? s->batch_global : B;
+  const float ce_scale = 10.f / ((float)bg * (float)(Nc * (Nc - 1)));
+  float* D = ws + w.D;
+  float* part = ws;   // segment offsets are absolute
+  auto F = [&](size_t off) { return ws + off; };
+
+  hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D);
+  WTRY(hipGetLastError());
+  // ---- entity side ----
+  if (ent || ee) {
+    hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
+                       bt->abits, aT, params, o, Ne, ent ? 1 : 0, F(w.P), F(w.R1), F(w.C1));
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
+                       params, o, Ne, ent ? 1 : 0, F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp),
+                       F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.rho), F(w.gmm));
+    WTRY(hipGetLastError());
+  }
+  unsigned long long* ncacc = ee ? (unsigned long long*)F(w.ncacc) : nullptr;
+  if (ee) {
+    WTRY(hipMemsetAsync(ncacc, 0, (size_t)B * Nc * 2 * 8, st));
+    hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NT), (size_t)Nc * 16, st, bt->abits, bt->hid,
+                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), ncacc);
+    WTRY(hipGetLastError());
+  }
+  // ---- hunk side ----
+  hipLaunchKernelGGL(kw_cross_fwd, dim3((Nc + NW - 1) / NW, B), dim3(NT), 0, st, prep,
+                     ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncacc, F(w.nvec), F(w.alpha),
+                     F(w.beta));
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+                     F(w.alpha), F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
+  WTRY(hipGetLastError());
+  float* probs = out ? out->probs : nullptr;
+  float* logits = out ? out->logits : nullptr;
+  if (!train) {
+    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NT), 0, st, bt->ybits, params, o, D,
+                       Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
+    WTRY(hipGetLastError());
+    if (ce_sum) {
+      hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, ce_sum);
+      WTRY(hipGetLastError());
+    }
+    return 0;
+  }
+  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NT), 0, st, bt->ybits, params, o, D, Nc,
+                     F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, params, o, D,
+                     Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig), F(w.Dtau),
+                     F(w.dG), F(w.dH), part, w.segs);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+                     F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe), part,
+                     w.segs);
+  WTRY(hipGetLastError());
+  if (ent || ee) {
+    hipLaunchKernelGGL(kw_dn, dim3(tc, B), dim3(NT), 0, st, params, o, Nc, F(w.Dal), F(w.Dbe),
+                       F(w.dn));
+    WTRY(hipGetLastError());
+  }
+  if (ent) {
+    hipLaunchKernelGGL(kw_node_bwd, dim3(te, B), dim3(NT), 0, st, prep, bt->x, params, o, Ne, Nc,
+                       F(w.dn), F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part, w.segs);
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, params, o,
+                       Ne, F(w.rhoE), F(w.rhoE), part, w.segs);
+    WTRY(hipGetLastError());
+  }
+  if (ee) {
+    const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 2), dim3(NT), lds, st, bt->abits, bt->hid, bt->nlen,
+                       params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho), F(w.dgam),
+                       part, w.segs);
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
+                       F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, params, o,
+                       Ne, F(w.phi), F(w.psi), part, w.segs);
+    WTRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + 4), dim3(64), 0, st, part, w.segs, 0, grad);
+  WTRY(hipGetLastError());
+  return 0;
+}
+
+}  // namespace hdg

@@ -16,7 +16,11 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libhdgnn.so")
 
 class Shape(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("ne", ctypes.c_int32), ("nc", ctypes.c_int32),
-                ("variant", ctypes.c_int32), ("batch_global", ctypes.c_int32)]
+                ("variant", ctypes.c_int32), ("batch_global", ctypes.c_int32),
+                ("path", ctypes.c_int32)]
+
+
+PATH_AUTO, PATH_FUSED, PATH_GENERAL = 0, 1, 2
 
 
 class Batch(ctypes.Structure):
@@ -34,7 +38,7 @@ class Outputs(ctypes.Structure):
                 ("stats", ctypes.c_void_p)]
 
 
-EXPORTS = ["hdg_version", "hdg_last_error", "hdg_param_count", "hdg_grad_len",
+EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count", "hdg_grad_len",
            "hdg_workspace_bytes", "hdg_prep_bytes", "hdg_prepare", "hdg_fwd_bwd",
            "hdg_fwd_bwd_events", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
            "hdg_debug_step_stamps"]
@@ -56,6 +60,7 @@ def load(path=None):
     vp, f32, i32 = ctypes.c_void_p, ctypes.c_float, ctypes.c_int32
     lib.hdg_version.restype = ctypes.c_int
     lib.hdg_last_error.restype = ctypes.c_char_p
+    lib.hdg_resolve_path.argtypes = [P(Shape)]
     lib.hdg_param_count.argtypes = [i32]
     lib.hdg_grad_len.argtypes = [i32]
     lib.hdg_workspace_bytes.argtypes = [P(Shape)]

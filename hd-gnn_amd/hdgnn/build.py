@@ -15,13 +15,13 @@ ARCH = "gfx950"
 
 
 def build(verbose=False):
-    src = os.path.join(CSRC, "hdgnn.hip")
+    srcs = [os.path.join(CSRC, f) for f in ("hdgnn.hip", "wide.hip")]
     out = os.path.join(CSRC, "libhdgnn.so")
-    deps = [src, os.path.join(ROOT, "include", "hdgnn.h")]
+    deps = srcs + [os.path.join(CSRC, "hdgnn_internal.h"), os.path.join(ROOT, "include", "hdgnn.h")]
     if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp", src]
+           "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp"] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

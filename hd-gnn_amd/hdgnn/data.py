@@ -86,21 +86,26 @@ class CommitBatch:
             raise ValueError("nlen must be in [0, Ne]")
         return self
 
-    def to_device(self, device="cuda"):
-        return DeviceBatch.from_host(self, device)
+    def to_device(self, device="cuda", variant=2, path=0):
+        """Upload + hdg_prepare.  The prepared tables depend on the engine path the
+        (variant, path) pair resolves to, so pass the Engine's."""
+        return DeviceBatch.from_host(self, device, variant, path)
 
 
 class DeviceBatch:
     """The hdg_batch struct's device arrays (include/hdgnn.h), prepared on upload:
     hdg_prepare builds the per-commit sort / transposed-bit / count tables in `prep`."""
 
-    def __init__(self, x, abits, ybits, hid, nlen, Ne, Nc):
+    def __init__(self, x, abits, ybits, hid, nlen, Ne, Nc, variant=2, path=0):
         import torch
         from . import _lib
         self.x, self.abits, self.ybits, self.hid, self.nlen = x, abits, ybits, hid, nlen
         self.B, self.Ne, self.Nc = x.shape[0], Ne, Nc
         lib = _lib.load()
-        shape = _lib.Shape(self.B, Ne, Nc, 2, self.B)
+        shape = _lib.Shape(self.B, Ne, Nc, variant, self.B, path)
+        self.path = lib.hdg_resolve_path(ctypes.byref(shape))   # prep layout is per path
+        if self.path < 0:
+            raise ValueError(lib.hdg_last_error().decode())
         nbytes = lib.hdg_prep_bytes(ctypes.byref(shape))
         if nbytes == 0:
             raise ValueError(lib.hdg_last_error().decode())
@@ -110,7 +115,7 @@ class DeviceBatch:
                                    ctypes.c_void_p(stream)))
 
     @classmethod
-    def from_host(cls, cb, device="cuda"):
+    def from_host(cls, cb, device="cuda", variant=2, path=0):
         import torch
         cb.validate()
         t = lambda arr, dt: torch.from_numpy(np.ascontiguousarray(arr)).to(device=device, dtype=dt)
@@ -118,7 +123,7 @@ class DeviceBatch:
                    t(pack_bits(cb.a).view(np.int32), torch.int32),
                    t(pack_bits(cb.y).view(np.int32), torch.int32),
                    t(cb.hid.astype(np.int32), torch.int32),
-                   t(cb.nlen.astype(np.int32), torch.int32), cb.Ne, cb.Nc)
+                   t(cb.nlen.astype(np.int32), torch.int32), cb.Ne, cb.Nc, variant, path)
 
     def struct(self):
         from ._lib import Batch

@@ -16,9 +16,10 @@ from .layout import n_params
 
 class Engine:
     def __init__(self, ne, nc, batch, variant=2, device="cuda", batch_global=None, lr=3e-4,
-                 process_group=None):
-        if variant != 2:
-            raise NotImplementedError("the HIP engine implements model_2 (HD-GNN/S)")
+                 process_group=None, path=_lib.PATH_AUTO):
+        """variant: model_<variant>.py (1 HD-GNN/ES, 2 HD-GNN/S, 3 HD-GNN/E, 4 HD-GNN).
+        path: PATH_AUTO (fused kernel when it applies, else the general path),
+        PATH_FUSED or PATH_GENERAL (include/hdgnn.h)."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -27,7 +28,10 @@ class Engine:
         self.batch_global = batch_global or batch
         self.lr = lr
         self.pg = process_group
-        self.shape = _lib.Shape(batch, ne, nc, variant, self.batch_global)
+        self.shape = _lib.Shape(batch, ne, nc, variant, self.batch_global, path)
+        self.path = self.lib.hdg_resolve_path(ctypes.byref(self.shape))
+        if self.path < 0:
+            raise ValueError(self.lib.hdg_last_error().decode())
         self.np = self.lib.hdg_param_count(variant)
         assert self.np == n_params(variant)
         self.glen = self.lib.hdg_grad_len(variant)
@@ -68,8 +72,18 @@ class Engine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def fwd_bwd(self, dbatch, outputs=True):
+    def upload(self, cb):
+        """Host CommitBatch -> DeviceBatch prepared for this engine's path."""
+        return cb.to_device(self.device, self.variant, self.path)
+
+    def _check(self, dbatch):
         assert dbatch.B == self.batch and dbatch.Ne == self.ne and dbatch.Nc == self.nc
+        if dbatch.path != self.path:
+            raise ValueError("batch prepared for path %d, engine runs path %d (use "
+                             "Engine.upload)" % (dbatch.path, self.path))
+
+    def fwd_bwd(self, dbatch, outputs=True):
+        self._check(dbatch)
         b = dbatch.struct()
         out = self._out if outputs else None
         _lib.check(self.lib.hdg_fwd_bwd(ctypes.byref(self.shape), ctypes.byref(b),
@@ -104,7 +118,7 @@ class Engine:
             self.allreduce()
             self.adam()
             return
-        assert dbatch.B == self.batch and dbatch.Ne == self.ne and dbatch.Nc == self.nc
+        self._check(dbatch)
         b = dbatch.struct()
         out = self._out if outputs else None
         _lib.check(self.lib.hdg_train_step(ctypes.byref(self.shape), ctypes.byref(b),
@@ -136,7 +150,7 @@ class Engine:
 
     def forward(self, dbatch):
         """sess.run([loss_Hedge_mse, loss_map, C_edge_output2]) equivalent (test path)."""
-        assert dbatch.B == self.batch
+        self._check(dbatch)
         b = dbatch.struct()
         _lib.check(self.lib.hdg_forward(ctypes.byref(self.shape), ctypes.byref(b),
                                         ctypes.c_void_p(self.params.data_ptr()),

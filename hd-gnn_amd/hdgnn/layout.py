@@ -1,23 +1,39 @@
 """Flat parameter layout of the engine (tf.global_variables order, (in,out) weights).
 
 model_2.py:161-179 phi_E_O1, 190-205 phi_U_O1, 245-277 mlp_hunk_B2, 304-324 phi_U_R1,
-326-333 map_conv.  Offsets here match the m2:: constants in csrc/hdgnn.hip.
+326-333 map_conv; model_4.py:206-243 phi_E_R1, 286-304 phi_U_R1 (entity-edge blocks).
+Offsets match hdg::param_offsets in csrc/hdgnn.hip (and m2:: for model_2).
 """
 import numpy as np
 
-MODEL2 = [
-    ("phi_E_O1/r1_w1o:0", (4, 20)), ("phi_E_O1/r1_b1o:0", (20,)),
-    ("phi_E_O1/r1_w5o:0", (20, 20)), ("phi_E_O1/r1_b5o:0", (20,)),
-    ("phi_U_O1/o1_w1o:0", (21, 20)), ("phi_U_O1/o1_b1o:0", (20,)),
-    ("phi_U_O1/o1_w2o:0", (20, 1)), ("phi_U_O1/o1_b2o:0", (1,)),
-    ("mlp_hunk_B2/w1:0", (10, 20)), ("mlp_hunk_B2/b1:0", (20,)),
-    ("mlp_hunk_B2/r1_w2r:0", (20, 20)), ("mlp_hunk_B2/b2:0", (20,)),
-    ("phi_U_R1/C_edge_w1:0", (22, 20)), ("phi_U_R1/C_edge_b1:0", (20,)),
-    ("phi_U_R1/o1_w2r:0", (20, 2)), ("phi_U_R1/o1_b2r:0", (2,)),
-    ("map_conv/map_theta1:0", (1, 2, 1, 1)), ("map_conv/map_theta2:0", (1, 2, 1, 1)),
-]
-VARIANTS = {2: MODEL2}
-BIASES = {"r1_b1o", "r1_b5o", "o1_b1o", "o1_b2o", "b1", "b2", "C_edge_b1", "o1_b2r"}
+_E1 = [("phi_E_O1/r1_w1o:0", (4, 20)), ("phi_E_O1/r1_b1o:0", (20,)),
+       ("phi_E_O1/r1_w5o:0", (20, 20)), ("phi_E_O1/r1_b5o:0", (20,))]
+_E3 = [("phi_U_O1/o1_w1o:0", (21, 20)), ("phi_U_O1/o1_b1o:0", (20,)),
+       ("phi_U_O1/o1_w2o:0", (20, 1)), ("phi_U_O1/o1_b2o:0", (1,))]
+_EE = [("phi_E_R1/r1_w1r1:0", (1, 20)), ("phi_E_R1/r1_w1r2:0", (2, 20)),     # model_4.py:218-221
+       ("phi_E_R1/r1_b1r:0", (20,)), ("phi_E_R1/r1_w2r:0", (20, 20)), ("phi_E_R1/r1_b2r:0", (20,))]
+_EC = [("phi_U_R1/o1_w1r:0", (22, 20)), ("phi_U_R1/o1_b1r:0", (20,)),      # model_4.py:293-299
+       ("phi_U_R1/o1_w2r:0", (20, 2)), ("phi_U_R1/o1_b2r:0", (2,))]
+_H1 = [("mlp_hunk_B2/w1:0", (10, 20)), ("mlp_hunk_B2/b1:0", (20,)),
+       ("mlp_hunk_B2/r1_w2r:0", (20, 20)), ("mlp_hunk_B2/b2:0", (20,))]
+
+
+def _h2(scope):   # TF uniquifies the re-entered phi_U_R1 scope when EC opened it first
+    return [(scope + "/C_edge_w1:0", (22, 20)), (scope + "/C_edge_b1:0", (20,)),
+            (scope + "/o1_w2r:0", (20, 2)), (scope + "/o1_b2r:0", (2,))]
+
+
+_TH = [("map_conv/map_theta1:0", (1, 2, 1, 1)), ("map_conv/map_theta2:0", (1, 2, 1, 1))]
+
+MODEL2 = _E1 + _E3 + _H1 + _h2("phi_U_R1") + _TH
+VARIANTS = {
+    1: _H1 + _h2("phi_U_R1") + _TH,                        # model_1.py  HD-GNN/ES
+    2: MODEL2,                                              # model_2.py  HD-GNN/S
+    3: _EE + _EC + _H1 + _h2("phi_U_R1_1") + _TH,           # model_3.py  HD-GNN/E
+    4: _E1 + _E3 + _EE + _EC + _H1 + _h2("phi_U_R1_1") + _TH,   # model_4.py  HD-GNN
+}
+BIASES = {"r1_b1o", "r1_b5o", "o1_b1o", "o1_b2o", "b1", "b2", "C_edge_b1", "o1_b2r", "r1_b1r",
+          "r1_b2r", "o1_b1r"}
 
 
 def specs(variant=2):

@@ -36,17 +36,27 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 2
+#define HDG_ABI_VERSION 3
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
 typedef struct hdg_shape {
-    int32_t batch;      /* commits in this call (Mini_batch per rank)            */
-    int32_t ne;         /* entity nodes per commit   (main.py --Ne, 2 <= ne <= 256) */
-    int32_t nc;         /* hunk nodes per commit     (main.py --Nc, 2 <= nc <= 160) */
-    int32_t variant;    /* model_<variant>.py; this build implements 2            */
-    int32_t batch_global; /* commits summed by the CE mean across all ranks       */
+    int32_t batch;      /* commits in this call (Mini_batch per rank)              */
+    int32_t ne;         /* entity nodes per commit   (main.py --Ne, 2 <= ne <= 4096) */
+    int32_t nc;         /* hunk nodes per commit     (main.py --Nc, 2 <= nc <= 2048) */
+    int32_t variant;    /* model_<variant>.py: 1 HD-GNN/ES, 2 HD-GNN/S, 3 HD-GNN/E,
+                           4 HD-GNN                                      */
+    int32_t batch_global; /* commits summed by the CE mean across all ranks         */
+    int32_t path;       /* HDG_PATH_AUTO / _FUSED / _GENERAL (see below)           */
 } hdg_shape;
+
+/* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
+ * with ne <= 256, nc <= 160 (the benchmark shape).  GENERAL: one launch per phase, many
+ * blocks per commit, state in HBM; every variant and shape.  AUTO picks FUSED when it
+ * applies.  hdg_prep_bytes / hdg_workspace_bytes depend on the path. */
+#define HDG_PATH_AUTO 0
+#define HDG_PATH_FUSED 1
+#define HDG_PATH_GENERAL 2
 
 /* One batch of commits in compact device form (replaces the 12-tuple feed of
  * utils2.read_data, utils2.py:248-253, bit-exactly).       */
@@ -80,6 +90,8 @@ typedef struct hdg_outputs {
 
 int         hdg_version(void);
 const char* hdg_last_error(void);
+/* the path AUTO resolves to for this shape (HDG_PATH_FUSED / _GENERAL), or -1 */
+int         hdg_resolve_path(const hdg_shape* shape);
 int         hdg_param_count(int32_t variant);
 /* length of the gradient buffer hdg_fwd_bwd fills: param_count + 4 trailer slots
  * (slot P = CE sum over this call's relations); all-reduce the whole buffer.      */

@@ -1,0 +1,204 @@
+"""General engine path (csrc/wide.hip) vs the CPU oracle, every model variant.  GPU only.
+
+Variants: 1 model_1 HD-GNN/ES (hunk stage on B_1), 2 model_2 HD-GNN/S,
+3 model_3 HD-GNN/E (entity-edge stage computed, unused), 4 model_4 HD-GNN (entity-edge
+probabilities replace E_edge in B_2).  Same tolerances as tests/test_gpu_parity.py:
+logits 1e-4 |ref| + 1e-5 max(1, max|ref|); probs = softmax(logits) to 1e-6; CE rel 1e-5;
+gradients rtol 1e-3 + 1e-3 max|ref| per variable; weights after TF-Adam atol 2e-6.
+"""
+import numpy as np
+import pytest
+import torch
+
+from hdgnn import _lib, layout
+from hdgnn.data import CommitBatch
+from hdgnn.synth import synth_commits
+from oracle import layout as olayout
+from oracle import model_ref
+
+pytestmark = pytest.mark.gpu
+
+GEN = _lib.PATH_GENERAL
+
+
+def _keys(v):
+    return [k for k, _, _ in olayout.keyed_specs(v)]
+
+
+def _engine(B, ne, nc, v, path=GEN):
+    from hdgnn.engine import Engine
+    return Engine(ne, nc, B, variant=v, path=path)
+
+
+def _oracle(flat, cb, v):
+    params = model_ref.unflatten(np.asarray(flat, np.float64), v)
+    out, grads = model_ref.loss_and_grads(params, cb.x.astype(np.float64), cb.a, cb.y, cb.hid,
+                                          cb.nlen, variant=v)
+    return out, np.concatenate([grads[k].reshape(-1) for k in _keys(v)])
+
+
+def _reg_grad(flat):
+    """loss_para + 0.1 loss_map gradients (model_2.py:123-130, 326-333); thetas last."""
+    g = 0.001 * flat.astype(np.float64)
+    n = len(flat)
+    for off in (n - 4, n - 2):
+        th = flat[off:off + 2].astype(np.float64)
+        g[off:off + 2] += 0.001 * th / np.linalg.norm(th)
+    return g
+
+
+def _check_outputs(logits, probs, out):
+    ref = out["logits"].transpose(0, 2, 1)
+    scale = np.maximum(1.0, np.abs(ref).reshape(ref.shape[0], -1).max(1))[:, None, None]
+    tol = 1e-4 * np.abs(ref) + 1e-5 * scale
+    err = np.abs(logits - ref)
+    assert np.all(err <= tol), "logits: max err %.3g" % err.max()
+    sm = np.exp(logits - logits.max(1, keepdims=True))
+    sm /= sm.sum(1, keepdims=True)
+    np.testing.assert_allclose(probs, sm, atol=1e-6)
+
+
+def _grad_close(g_eng, g_ref, v):
+    bad = []
+    for name, (o, shape) in layout.offsets(v).items():
+        n = int(np.prod(shape))
+        a, r = g_eng[o:o + n], g_ref[o:o + n]
+        scale = max(np.abs(r).max(), 1e-12)
+        tol = 1e-3 * np.abs(r) + 1e-3 * scale + 1e-9
+        err = np.abs(a - r)
+        if not np.all(err <= tol):
+            bad.append("%s: max err %.3g, scale %.3g, %d/%d bad" % (
+                name, np.nanmax(err) if np.isfinite(err).any() else np.nan, scale,
+                int((~(err <= tol)).sum()), n))
+    assert not bad, "gradient mismatch:\n  " + "\n  ".join(bad)
+
+
+def _run_and_check(cb, v, seed, path=GEN):
+    B, ne, nc = cb.B, cb.Ne, cb.Nc
+    flat = layout.init_flat(seed, v)
+    eng = _engine(B, ne, nc, v, path)
+    eng.set_params(flat)
+    db = eng.upload(cb)
+    eng.fwd_bwd(db)
+    torch.cuda.synchronize()
+    out, g_ref = _oracle(flat, cb, v)
+    _check_outputs(eng.logits.cpu().numpy(), eng.probs.cpu().numpy(), out)
+    g = eng.grad.cpu().numpy().astype(np.float64)
+    np_ = len(flat)
+    _grad_close(g[:np_] + _reg_grad(flat), g_ref, v)
+    np.testing.assert_allclose(g[np_] / (B * nc * (nc - 1)), float(out["ce"]), rtol=1e-5)
+    probs, logits, ce_sum = eng.forward(db)          # test path (forward only)
+    torch.cuda.synchronize()
+    _check_outputs(logits.cpu().numpy(), probs.cpu().numpy(), out)
+    np.testing.assert_allclose(ce_sum.item() / (B * nc * (nc - 1)), float(out["ce"]), rtol=1e-5)
+    return eng
+
+
+SHAPES = [
+    (3, 7, 5, 0),       # tiny
+    (2, 37, 19, 1),     # ragged
+    (2, 64, 64, 2),     # exactly one tile
+    (2, 65, 70, 3),     # one past a tile on both graphs
+    (2, 200, 74, 4),    # glide step 2 (BASELINE config 1/2)
+    (1, 250, 114, 5),   # step=3 shapes (BASELINE config 3)
+]
+
+
+@pytest.mark.parametrize("v", [1, 2, 3, 4])
+@pytest.mark.parametrize("B,ne,nc,seed", SHAPES)
+def test_variant_matches_oracle(v, B, ne, nc, seed):
+    _run_and_check(synth_commits(B, ne, nc, seed), v, seed)
+
+
+@pytest.mark.parametrize("v", [2, 4])
+def test_stress_shape_matches_oracle(v):
+    """BASELINE config 5 shapes (Ne=1024, Nc=512): beyond the fused kernel's LDS budget."""
+    _run_and_check(synth_commits(1, 1024, 512, 9), v, 9)
+
+
+def test_general_equals_fused_model2():
+    B, ne, nc = 4, 200, 74
+    cb = synth_commits(B, ne, nc, 12)
+    flat = layout.init_flat(2)
+    outs = []
+    for path in (_lib.PATH_FUSED, GEN):
+        eng = _engine(B, ne, nc, 2, path)
+        eng.set_params(flat)
+        eng.fwd_bwd(eng.upload(cb))
+        torch.cuda.synchronize()
+        outs.append((eng.logits.cpu().numpy().astype(np.float64),
+                     eng.grad.cpu().numpy().astype(np.float64)))
+    (l1, g1), (l2, g2) = outs
+    scale = np.maximum(1.0, np.abs(l1).max())
+    assert np.abs(l1 - l2).max() <= 1e-4 * scale
+    _grad_close(g2[:2127], g1[:2127], 2)
+
+
+EDGE = {
+    "no_index_lines": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid * 0 - 1, cb.nlen * 0),
+    "one_index_line": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid, cb.nlen * 0 + 1),
+    "two_index_lines": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid, cb.nlen * 0 + 2),
+    "full_index_file": lambda cb: CommitBatch(cb.x, cb.a, cb.y, np.abs(cb.hid) % cb.Nc,
+                                              cb.nlen * 0 + cb.Ne),
+    "all_lines_one_hunk": lambda cb: CommitBatch(cb.x, cb.a, cb.y, cb.hid * 0, cb.nlen * 0 + cb.Ne),
+    "empty_adjacency": lambda cb: CommitBatch(cb.x, 0 * cb.a, 0 * cb.y, cb.hid, cb.nlen),
+    "full_adjacency": lambda cb: CommitBatch(cb.x, 1 - np.eye(cb.Ne, dtype=np.uint8)[None] + 0 * cb.a,
+                                             1 - np.eye(cb.Nc, dtype=np.uint8)[None] + 0 * cb.y,
+                                             cb.hid, cb.nlen),
+    "float_attributes": lambda cb: CommitBatch(
+        (np.random.default_rng(3).standard_normal(cb.x.shape) * 4).astype(np.float32),
+        cb.a, cb.y, cb.hid, cb.nlen),
+}
+
+
+@pytest.mark.parametrize("case", sorted(EDGE))
+def test_model4_edge_cases(case):
+    cb = EDGE[case](synth_commits(2, 70, 13, 7))
+    _run_and_check(cb, 4, 7)
+
+
+def test_model4_train_steps_match_oracle_adam():
+    B, ne, nc, seed, v = 2, 45, 17, 5, 4
+    cb = synth_commits(B, ne, nc, seed)
+    flat = layout.init_flat(seed, v)
+    eng = _engine(B, ne, nc, v)
+    eng.set_params(flat)
+    db = eng.upload(cb)
+    theta = flat.astype(np.float64)
+    opt = model_ref.AdamTF(len(flat))
+    for _ in range(3):
+        eng.train_step(db)
+        torch.cuda.synchronize()
+        out, g_ref = _oracle(theta.astype(np.float32), cb, v)
+        stats = eng.stats.cpu().numpy()
+        for i, k in enumerate(("ce", "loss_map", "loss_para", "total")):
+            np.testing.assert_allclose(stats[i], float(out[k]), rtol=1e-5)
+        theta = opt.step(theta, g_ref)
+        np.testing.assert_allclose(eng.get_params(), theta, rtol=0, atol=2e-6)
+
+
+def test_general_deterministic_bitwise():
+    cb = synth_commits(3, 200, 74, 11)
+    eng = _engine(3, 200, 74, 4)
+    eng.set_params(layout.init_flat(1, 4))
+    db = eng.upload(cb)
+    eng.fwd_bwd(db)
+    g1, p1 = eng.grad.clone(), eng.probs.clone()
+    eng.fwd_bwd(db)
+    assert torch.equal(g1, eng.grad) and torch.equal(p1, eng.probs)
+
+
+def test_general_graph_replay_equals_eager():
+    B, ne, nc, v = 3, 50, 30, 4
+    cb = synth_commits(B, ne, nc, 4)
+    flat = layout.init_flat(3, v)
+    e1, e2 = _engine(B, ne, nc, v), _engine(B, ne, nc, v)
+    e1.set_params(flat)
+    e2.set_params(flat)
+    db = e1.upload(cb)
+    e2.capture(db)
+    for _ in range(3):
+        e1.train_step(db)
+        e2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.probs, e2.probs)

@@ -208,9 +208,12 @@ def test_full_size_properties():
 
 
 def test_shape_errors_are_reported():
+    from hdgnn import _lib
     from hdgnn.engine import Engine
-    with pytest.raises(RuntimeError):
-        Engine(300, 74, 4)          # ne > 256
+    with pytest.raises(ValueError):
+        Engine(300, 74, 4, path=_lib.PATH_FUSED)    # ne > 256 on the fused kernel
+    with pytest.raises(ValueError):
+        Engine(5000, 74, 4)                          # beyond every path
 
 
 def test_graph_replay_equals_eager():

@@ -35,18 +35,33 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from hdgnn import _lib
     lib = _lib.load()
-    assert lib.hdg_version() == 2
-    assert lib.hdg_param_count(2) == 2127
-    assert lib.hdg_grad_len(2) == 2131
-    ok = _lib.Shape(100, 200, 74, 2, 100)
+    assert lib.hdg_version() == 3
+    for v, n in ((1, 1146), (2, 2127), (3, 2148), (4, 3129)):
+        assert lib.hdg_param_count(v) == n
+        assert lib.hdg_grad_len(v) == n + 4
+    assert lib.hdg_param_count(5) == -1
+    ok = _lib.Shape(100, 200, 74, 2, 100, 0)
+    assert lib.hdg_resolve_path(ctypes.byref(ok)) == _lib.PATH_FUSED
     assert lib.hdg_workspace_bytes(ctypes.byref(ok)) > 0
     assert lib.hdg_prep_bytes(ctypes.byref(ok)) > 0
-    for ne, nc in ((250, 114), (250, 150), (256, 160), (2, 2)):   # s3, s5, limits
-        sh = _lib.Shape(100, ne, nc, 2, 100)
+    for ne, nc in ((250, 114), (250, 150), (256, 160), (2, 2)):   # s3, s5, fused limits
+        sh = _lib.Shape(100, ne, nc, 2, 100, 0)
+        assert lib.hdg_resolve_path(ctypes.byref(sh)) == _lib.PATH_FUSED
         assert lib.hdg_workspace_bytes(ctypes.byref(sh)) > 0, lib.hdg_last_error()
-    bad = _lib.Shape(100, 300, 74, 2, 100)
+    # beyond the fused kernel (stress shape, other variants): the general path
+    for v, ne, nc in ((2, 1024, 512), (2, 300, 74), (1, 200, 74), (3, 200, 74), (4, 200, 74)):
+        sh = _lib.Shape(32, ne, nc, v, 256, 0)
+        assert lib.hdg_resolve_path(ctypes.byref(sh)) == _lib.PATH_GENERAL
+        assert lib.hdg_workspace_bytes(ctypes.byref(sh)) > 0, lib.hdg_last_error()
+        assert lib.hdg_prep_bytes(ctypes.byref(sh)) > 0
+    forced = _lib.Shape(4, 200, 74, 2, 4, _lib.PATH_GENERAL)
+    assert lib.hdg_resolve_path(ctypes.byref(forced)) == _lib.PATH_GENERAL
+    bad = _lib.Shape(100, 300, 74, 2, 100, _lib.PATH_FUSED)
+    assert lib.hdg_workspace_bytes(ctypes.byref(bad)) == 0
+    assert b"fused path" in lib.hdg_last_error()
+    bad = _lib.Shape(100, 5000, 74, 2, 100, 0)
     assert lib.hdg_workspace_bytes(ctypes.byref(bad)) == 0
     assert b"ne must be" in lib.hdg_last_error()
-    bad_v = _lib.Shape(4, 20, 10, 4, 4)
+    bad_v = _lib.Shape(4, 20, 10, 5, 4, 0)
     assert lib.hdg_workspace_bytes(ctypes.byref(bad_v)) == 0
     assert b"variant" in lib.hdg_last_error()
