@@ -27,14 +27,19 @@ FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA pea
 HBM_PEAK_GBS = 8000.0
 
 
-def flops_per_commit(ne, nc):
+def flops_per_commit(ne, nc, variant=2):
     """Algorithmic training FLOPs per commit, SURVEY 8(d) / BASELINE.md:
     3 * F_fwd(model_2), F_fwd = 1008 Pe + 880 Ne + 2200 Pc (the dense TF graph's pair
-    MLPs, sums, node MLPs and classifier; padding / recompute not counted).  The engine
-    executes far fewer operations (sorted-x entity sums), so this is
-    work-equivalent throughput; k_commit_step carries all of it (fwd + bwd)."""
+    MLPs, sums, node MLPs and classifier; padding / recompute not counted);
+    F_fwd(model_4) = F_fwd(model_2) + 1960 Pe; model_1 / model_3 (TF evaluates only the
+    fetched subgraph, so model_3's entity-edge stage is never run): 8 Pe + 2200 Pc.
+    The engine executes far fewer operations (sorted-x entity sums),
+    so this is work-equivalent throughput."""
     pe, pc = ne * (ne - 1), nc * (nc - 1)
-    return 3 * (1008 * pe + 880 * ne + 2200 * pc)
+    f = {1: 8 * pe + 2200 * pc, 3: 8 * pe + 2200 * pc,
+         2: 1008 * pe + 880 * ne + 2200 * pc,
+         4: 1008 * pe + 880 * ne + 2200 * pc + 1960 * pe}[variant]
+    return 3 * f
 
 
 def hbm_bytes_per_commit(ne, nc):
@@ -99,6 +104,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
+    ap.add_argument("--variant", type=int, default=2, choices=(1, 2, 3, 4),
+                    help="model_<variant>.py (the BASELINE metric is model_2)")
+    ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
+                    help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     args = ap.parse_args()
 
@@ -116,16 +125,16 @@ def main():
     from hdgnn.synth import seed_for, synth_commits
     from hdgnn import _lib
 
-    B, ne, nc = args.batch, args.ne, args.nc
+    B, ne, nc, v = args.batch, args.ne, args.nc, args.variant
     cb = synth_commits(B, ne, nc, seed_for(1, rank))
-    cb.to_device(dev)                            # warm the upload / prepare path once
+    eng = Engine(ne, nc, B, variant=v, device=dev, batch_global=B * world, path=args.path)
+    eng.set_params(layout.init_flat(0, v))
+    eng.upload(cb)                               # warm the upload / prepare path once
     torch.cuda.synchronize(dev)
     t_up = time.perf_counter()
-    db = cb.to_device(dev)                       # host arrays -> HBM + hdg_prepare
+    db = eng.upload(cb)                          # host arrays -> HBM + hdg_prepare
     torch.cuda.synchronize(dev)
     upload_ms = 1e3 * (time.perf_counter() - t_up)
-    eng = Engine(ne, nc, B, device=dev, batch_global=B * world)
-    eng.set_params(layout.init_flat(0))
 
     def barrier():
         if world > 1:
@@ -156,7 +165,8 @@ def main():
 
     # per-kernel durations (HIP events on the launch stream), separate instrumented pass
     ev = _lib.HipEvents(3)
-    names = ["k_commit_step", "k_grad_reduce"]
+    fused = eng.path == _lib.PATH_FUSED
+    names = ["k_commit_step", "k_grad_reduce"] if fused else ["general_fwd_bwd", "none"]
     acc = dict.fromkeys(names, 0.0)
     nev = max(10, min(args.steps, 50))
     import ctypes
@@ -179,14 +189,15 @@ def main():
         if world > 1:
             torch.distributed.destroy_process_group()
         return
-    dom = "k_commit_step"
-    flops_launch = flops_per_commit(ne, nc) * B
+    dom = names[0]
+    flops_launch = flops_per_commit(ne, nc, v) * B
     achieved = flops_launch / (kern_ms[dom] * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne:
+        if (tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne
+                and tj.get("nc") == nc and fused):
             traffic = tj.get("bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
@@ -194,16 +205,19 @@ def main():
                 "flops_per_launch": flops_launch, "avg_launch_ms": round(kern_ms[dom], 5),
                 "algorithmic_bytes_per_launch": hbm_bytes_per_commit(ne, nc) * B,
                 "note": "SURVEY 8(d) dense-graph FLOPs (3 F_fwd per commit) over the measured "
-                        "k_commit_step time; the engine executes fewer ops (DESIGN.md 3)"}
+                        "%s time; the engine executes fewer ops (DESIGN.md 3)" % dom}
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and v == 2:
         threads = min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(cb, args.cpu_steps, threads)
     line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)",
-            "config": {"workload": "model_2 (HD-GNN/S) train step: fwd+bwd+TF-Adam, glide step=2",
+            "config": {"workload": "model_%d (%s) train step: fwd+bwd+TF-Adam, %s" % (
+                           v, {1: "HD-GNN/ES", 2: "HD-GNN/S", 3: "HD-GNN/E", 4: "HD-GNN"}[v],
+                           "glide step=2" if (ne, nc) == (200, 74) else "Ne=%d Nc=%d" % (ne, nc)),
+                       "engine_path": "fused" if fused else "general",
                        "launch": "eager" if args.no_graph else "hipGraph replay per step",
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world},

@@ -1,4 +1,7 @@
-"""Drop-in for the reference's model_2.graph2graph (HD-GNN/S), backed by libhdgnn.so.
+"""Drop-in for the reference's model_N.graph2graph, backed by libhdgnn.so.
+
+graph2graph here is model_2 (HD-GNN/S, the reference main.py's import); hdgnn.model_1 /
+model_3 / model_4 export the same class for the other variants (variant attribute).
 
 Same constructor (model_2.py:16-33), same train(args) / test(args) flow, files and
 printed lines (model_2.py:336-407, 434-548); the TF graph + sess.run are replaced by
@@ -9,7 +12,7 @@ the engine (hdgnn.engine.Engine -> C ABI -> k_commit_step on MI355X):
     sess.run([loss, loss_map, C_edge_output2]) (486)  Engine.forward(DeviceBatch)
     read_data(self, Step) -> 12 dense arrays          reader(self, Step) -> the same tuple,
                                                       then data.compact_from_read_data
-    saver.save / restore (409-432)                    .npz of the 18 TF-named variables
+    saver.save / restore (409-432)                    .npz of the TF-named variables
 
 Reference behaviours kept on purpose: every batch feeds the maps
 of the first Mini_batch commits (B.2, also in test); remainder commits are dropped
@@ -27,7 +30,7 @@ import time
 import numpy as np
 
 from . import layout, metrics
-from .data import DeviceBatch, compact_from_read_data
+from .data import compact_from_read_data
 
 HS = 20   # De_e = De_er = h_size compiled into the engine
 
@@ -56,6 +59,8 @@ def _default_reader(model, step):
 
 
 class graph2graph(object):
+    variant = 2        # model_<variant>.py
+
     def __init__(self, sess, Ds, Ne, Nc, Ner, Ncr, Dr, De_e, De_er, Mini_batch, checkpoint_dir,
                  epoch, Ds_inter, Dr_inter, Step, Repo, *, reader=None, device=None, seed=0,
                  lr=3e-4, process_group=None):
@@ -89,8 +94,8 @@ class graph2graph(object):
                              % (self.mini_batch_num, self.world))
         self.local_batch = self.mini_batch_num // self.world
         dev = self.device or torch.device("cuda", torch.cuda.current_device())
-        self.engine = Engine(self.Ne, self.Nc, self.local_batch, device=dev,
-                             batch_global=self.mini_batch_num, lr=self.lr,
+        self.engine = Engine(self.Ne, self.Nc, self.local_batch, variant=self.variant,
+                             device=dev, batch_global=self.mini_batch_num, lr=self.lr,
                              process_group=self.pg)
         self._initialize()
         # fetchable attributes (filled by the last step, like sess.run results)
@@ -103,11 +108,11 @@ class graph2graph(object):
     def _initialize(self):
         """tf.global_variables_initializer(): truncated_normal(0.1) weights, zero biases,
         fresh Adam slots and beta powers."""
-        self.engine.set_params(layout.init_flat(self.seed))
+        self.engine.set_params(layout.init_flat(self.seed, self.variant))
 
     @property
     def vars(self):
-        return layout.split(self.engine.get_params())
+        return layout.split(self.engine.get_params(), self.variant)
 
     @property
     def theta(self):
@@ -125,7 +130,7 @@ class graph2graph(object):
         out = []
         for (c0, c1), (p0, p1) in shard_plan(part.B, self.mini_batch_num, self.world, self.rank):
             sh = part.slice(c0, c1).with_maps(maps.slice(p0, p1))
-            out.append(DeviceBatch.from_host(sh, self.engine.device))
+            out.append(self.engine.upload(sh))
         return out
 
     def _gather(self, arr):
@@ -183,8 +188,8 @@ class graph2graph(object):
                            " map MSE: " + str(tr_loss_map / nb if nb else 0.0)[0:6] + \
                            " theta: " + str(theta[0]) + ' ' + str(theta[1]) + '\n'
             if self.rank == 0:
-                filepath = r'outputSelf/{}/model_2/{}/result_{}.npy'.format(args.Repo, self.Step,
-                                                                              self.Step)
+                filepath = r'outputSelf/{}/model_{}/{}/result_{}.npy'.format(
+                    args.Repo, self.variant, self.Step, self.Step)
                 os.makedirs(os.path.dirname(filepath), exist_ok=True)
                 with open(filepath, "a", encoding='utf-8') as f:
                     f.write(resultString)
@@ -197,7 +202,7 @@ class graph2graph(object):
 
     # ------------------------------------------------------------------ checkpoints
     def _model_dir(self, checkpoint_dir):
-        return os.path.join(checkpoint_dir, "%s" % (self.Repo + '/model_2/' + str(self.Step)))
+        return os.path.join(checkpoint_dir, "%s/model_%d/%s" % (self.Repo, self.variant, self.Step))
 
     def save(self, checkpoint_dir, step):
         """g2g.model-<step>.npz holding the 18 variables under their TF names, the Adam
@@ -230,7 +235,7 @@ class graph2graph(object):
         import torch
         z = np.load(path, allow_pickle=False)
         flat = np.concatenate([np.asarray(z[n], np.float32).reshape(-1)
-                               for n, _ in layout.specs()])
+                               for n, _ in layout.specs(self.variant)])
         eng = self.engine
         eng.set_params(flat)
         if "_adam_m" in z:
@@ -272,7 +277,7 @@ class graph2graph(object):
                      else np.zeros((0, self.Dr, self.Ncr), np.float32))
         if self.rank != 0:
             return
-        step_dir = 'outputSelf/' + args.Repo + '/model_2/' + str(self.Step) + '/'
+        step_dir = 'outputSelf/%s/model_%d/%s/' % (args.Repo, self.variant, self.Step)
         os.makedirs(step_dir, exist_ok=True)
         np.save(step_dir + 'C_edge_t' + str(self.Ne) + '.npy', C_edge_t1)
         np.save(step_dir + 'C_edge_y' + str(self.Ne) + '.npy',

@@ -27,8 +27,19 @@ def _init_distributed():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
 
 
+def _variant(argv):
+    """--model N (1..4, default 2 = the reference main.py's `from model_2 import`): which
+    model_N.graph2graph to run.  An addition; every reference flag is unchanged."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument('--model', type=int, default=2, choices=(1, 2, 3, 4))
+    a, rest = p.parse_known_args(argv)
+    return a.model, rest
+
+
 def main(argv=None):
-    from hdgnn.model import graph2graph
+    import importlib
+    variant, argv = _variant(sys.argv[1:] if argv is None else argv)
+    graph2graph = importlib.import_module("hdgnn.model" + ("" if variant == 2 else "_%d" % variant)).graph2graph
     _init_distributed()
     steps = [2, 3, 5]
     entity_nodes = [200, 250, 250]

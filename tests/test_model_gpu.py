@@ -1,4 +1,4 @@
-"""hdgnn.model.graph2graph (the drop-in for model_2.graph2graph) end to end on the GPU:
+"""hdgnn.model[_N].graph2graph (the drop-ins for model_N.graph2graph) end to end on the GPU:
 train(args) for 2 epochs on the reference loader's golden 12-tuple (Ne=7, Nc=5,
 50 train / 50 test commits, Mini_batch=25 -> 2 steps per epoch) against the oracle
 driven through the same batch plan; then test(args) and its output files."""
@@ -26,8 +26,11 @@ def _tuple(golden_dir):
     return tuple(z[n] for n in NAMES), meta
 
 
-def test_graph2graph_train_and_test(golden_dir, tmp_path, monkeypatch):
-    from hdgnn.model import graph2graph
+@pytest.mark.parametrize("v", [1, 2, 3, 4])
+def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
+    import importlib
+    graph2graph = importlib.import_module("hdgnn.model" + ("" if v == 2 else "_%d" % v)).graph2graph
+    assert graph2graph.variant == v
     tup, meta = _tuple(golden_dir)
     ne, nc, mb = meta["Ne"], meta["Nc"], 25
     monkeypatch.chdir(tmp_path)
@@ -41,37 +44,38 @@ def test_graph2graph_train_and_test(golden_dir, tmp_path, monkeypatch):
 
     # oracle through the same plan: 2 epochs x 2 batches, maps of positions [:mb]
     train, test, maps = data.compact_from_read_data(tup, ne, nc, mb)
-    theta = layout.init_flat(7).astype(np.float64)
+    theta = layout.init_flat(7, v).astype(np.float64)
     opt = model_ref.AdamTF(theta.size)
     for _ in range(2):
         for j in range(2):
             sh = train.slice(j * mb, (j + 1) * mb).with_maps(maps)
-            P = model_ref.unflatten(theta.astype(np.float32).astype(np.float64))
+            P = model_ref.unflatten(theta.astype(np.float32).astype(np.float64), v)
             _, g = model_ref.loss_and_grads(P, sh.x.astype(np.float64), sh.a, sh.y, sh.hid,
-                                            sh.nlen)
+                                            sh.nlen, variant=v)
             from oracle import layout as olayout
-            keys = [k for k, _, _ in olayout.keyed_specs(2)]
+            keys = [k for k, _, _ in olayout.keyed_specs(v)]
             theta = opt.step(theta, np.concatenate([g[k].reshape(-1) for k in keys]))
     np.testing.assert_allclose(m.engine.get_params(), theta, rtol=0, atol=5e-6)
 
-    res = tmp_path / "outputSelf" / "tiny" / "model_2" / "2" / "result_2.npy"
+    res = tmp_path / "outputSelf" / "tiny" / ("model_%d" % v) / "2" / "result_2.npy"
     lines = res.read_text().splitlines()
     assert len(lines) == 2 and lines[0].startswith("Epoch 1 acc: ")
-    ck = tmp_path / "ckpt" / "tiny" / "model_2" / "2"
+    ck = tmp_path / "ckpt" / "tiny" / ("model_%d" % v) / "2"
     assert (ck / "checkpoint").exists() and (ck / "g2g.model-3.npz").exists()
     z = np.load(ck / "g2g.model-3.npz")
-    np.testing.assert_array_equal(z["phi_E_O1/r1_w1o:0"].reshape(-1),
-                                  m.engine.get_params()[:80])
+    first, shape = layout.specs(v)[0]
+    np.testing.assert_array_equal(z[first].reshape(-1),
+                                  m.engine.get_params()[:int(np.prod(shape))])
 
     # test(): checkpoint looked up under checkpoint_dir/Repo/Repo/... (reference quirk)
     m.test(args)
-    out = np.load(tmp_path / "outputSelf" / "tiny" / "model_2" / "2" / "C_edge_t7.npy")
+    out = np.load(tmp_path / "outputSelf" / "tiny" / ("model_%d" % v) / "2" / "C_edge_t7.npy")
     assert out.shape == (50, 2, nc * (nc - 1))
-    P0 = model_ref.unflatten(layout.init_flat(7).astype(np.float64))
+    P0 = model_ref.unflatten(layout.init_flat(7, v).astype(np.float64), v)
     ref = []
     for j in range(2):
         sh = test.slice(j * mb, (j + 1) * mb).with_maps(maps)
         o = model_ref.forward(model_ref.to_torch_params(P0, requires_grad=False),
-                              sh.x.astype(np.float64), sh.a, sh.y, sh.hid, sh.nlen)
+                              sh.x.astype(np.float64), sh.a, sh.y, sh.hid, sh.nlen, variant=v)
         ref.append(o["probs"].detach().numpy().transpose(0, 2, 1))
     np.testing.assert_allclose(out, np.concatenate(ref), atol=1e-5)
