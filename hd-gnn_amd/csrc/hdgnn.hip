@@ -471,19 +471,21 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
 //   n_c[0] = sum_I ks[c][I] x'_I,  n_c[1] = sum_J kt[c][J] x'_J,  n_c[2:4] = ncst[c]
 // ks[c][I] = #{r in Ne-row I : s_r = c} + #{r in Ne-row I : t_r = c}, kt over Ne-columns.
 // Integer LDS atomics (order-independent) over chunks of CH hunks.
+// The count arrays live at word offsets (o_ks, o_kt, o_ncst) of each commit's prep block
+// of `stride` words (fused layout: prep_layout; general path: its own layout).
 __global__ __launch_bounds__(1024) void k_prep_maps(const uint32_t* __restrict__ abits,
                                                     const int32_t* __restrict__ hidg,
                                                     const int32_t* __restrict__ nleng,
                                                     uint32_t* __restrict__ prep, int Ne, int Nc,
-                                                    int CH) {
+                                                    int CH, int stride, int o_ks, int o_kt,
+                                                    int o_ncst) {
   extern __shared__ uint32_t cnt[];   // [2][CH][Ne], then [Nc][2]
-  const PrepLayout L = prep_layout(Ne, Nc);
   const int b = blockIdx.x, t = threadIdx.x;
   const int WE = (Ne + 31) >> 5;
-  uint32_t* pb = prep + (size_t)b * L.words;
-  uint16_t* ks = (uint16_t*)(pb + L.ks);
-  uint16_t* kt = (uint16_t*)(pb + L.kt);
-  float* ncst = (float*)(pb + L.ncst);
+  uint32_t* pb = prep + (size_t)b * stride;
+  uint16_t* ks = (uint16_t*)(pb + o_ks);
+  uint16_t* kt = (uint16_t*)(pb + o_kt);
+  float* ncst = (float*)(pb + o_ncst);
   uint32_t* ncl = cnt + 2 * CH * Ne;
   const int32_t* hid = hidg + (size_t)b * Ne;
   const uint32_t* ab = abits + (size_t)b * Ne * WE;
@@ -1835,7 +1837,8 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
+hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,
+                            int o_kt, int o_ncst, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_prep_maps,
@@ -1847,7 +1850,7 @@ hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, hipStream_t
   const int ch = prep_chunk(s->ne, s->nc);
   const size_t lds = (size_t)(2 * ch * s->ne + 2 * s->nc) * 4;
   hipLaunchKernelGGL(k_prep_maps, dim3(s->batch), dim3(1024), lds, st, bt->abits, bt->hid,
-                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch);
+                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch, stride, o_ks, o_kt, o_ncst);
   return hipGetLastError();
 }
 
@@ -1992,7 +1995,8 @@ int hdg_prepare(const hdg_shape* s, const hdg_batch* bt, void* stream) {
   hipLaunchKernelGGL(k_prep_sort, dim3(s->batch), dim3(256), 0, st, bt->x, bt->abits,
                      (uint32_t*)bt->prep, s->ne, s->nc);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hdg::launch_prep_maps(s, bt, st));
+  const PrepLayout L = prep_layout(s->ne, s->nc);
+  HIP_TRY(hdg::launch_prep_maps(s, bt, L.words, L.ks, L.kt, L.ncst, st));
   return 0;
 }
 

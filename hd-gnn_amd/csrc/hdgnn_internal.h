@@ -28,8 +28,8 @@ constexpr int HS = 20;   // h_size = De_e = De_er (model_2.py:163, 192, 247, 306
 //   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
-// The general path uses only ks / kt / ncst of this block and appends, after all B
-// commits, the transposed class bits a^T [B][Ne][WE] and y^T [B][Nc][WC].
+// The general path has its own per-commit layout (wide.hip, GenPrep): ks / kt / ncst as
+// here, transposed class bits, and the sorted-x tables without the byte neighbour lists.
 // ------------------------------------------------------------------------------
 struct PrepLayout {
   int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, words;
@@ -80,7 +80,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
              hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st);
 
 // fused path pieces the general path reuses (hdgnn.hip)
-hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
+hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,
+                            int o_kt, int o_ncst, hipStream_t st);
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
 }  // namespace hdg

@@ -86,6 +86,34 @@ enum : int {
   D_WORDS = 544
 };
 
+// Prepared batch of the general path, per commit (words): cross-graph counts as in the
+// fused layout, then the sorted-x tables of the entity stages (k_prep_maps, kw_prep_sort):
+//   ks, kt [Nc][Ne] u16   ncst [Nc][2] f32   xsrt [NE4] x ascending   perm [NE4] node of slot
+//   xu [NE4] distinct values   cum [NE4+4] #nodes with x < xu[q]   pxd [NE4+4] f64 sums
+//   meta[4] = {nd}
+// followed, after all B commits, by a^T [B][Ne][WE] and y^T [B][Nc][WC] (kw_prep_T).
+struct GenPrep {
+  int ks, kt, ncst, xsrt, perm, xu, cum, pxd, meta, words;
+};
+
+__host__ __device__ inline GenPrep gen_prep(int Ne, int Nc) {
+  GenPrep G;
+  const int NE4 = (Ne + 3) & ~3;
+  const int kw = ((Nc * Ne + 1) / 2 + 3) & ~3;
+  int o = 0;
+  G.ks = o;   o += kw;
+  G.kt = o;   o += kw;
+  G.ncst = o; o += (2 * Nc + 3) & ~3;
+  G.xsrt = o; o += NE4;
+  G.perm = o; o += NE4;
+  G.xu = o;   o += NE4;
+  G.cum = o;  o += NE4 + 4;
+  G.pxd = o;  o += 2 * (NE4 + 4);     // every offset above is a multiple of 4: 8-B aligned
+  G.meta = o; o += 4;
+  G.words = (o + 63) & ~63;
+  return G;
+}
+
 // per-block partial gradient rows: segment s holds n consecutive parameters starting at
 // flat index p0, laid out [n][rows] at part + off
 constexpr int MAXSEG = 16;
@@ -202,93 +230,166 @@ __device__ __forceinline__ float bitf(const uint32_t* row, int m) {
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ent_fwd  grid (te, B, 1 + EE): z = 0 entity stage (if the variant has it) else EE
-//   E1 (model_2.py:161-188): pair (i,j) pre-activation u_i + x_j w1 + a_ij d with
-//     u = x w0 + w2 + b1, d = w3 - w2; P_i = sum_{j!=i} relu(z_ij) + relu(z_ji)
-//   EE (model_4.py:206-243, shared w1_1): z'_ij = (x_i + x_j) w + e + a_ij d',
-//     R1_i = sum_{j!=i} relu(z'_ij) (source side), C1_i = sum_{j!=i} relu(z'_ji)
+// Sorted-x entity sums.  For hidden unit k the a = 0 pre-activation of pair (i, j) is
+// affine in the scalar x_j, so {j : z_ij > 0} is a prefix or a suffix of the x-sorted
+// order: a binary search over the nd distinct values finds it, and the f64 prefix sums
+// give its relu sum (count * offset + slope * sum x).  The a = 1 pairs add
+// relu(z + d) - relu(z) over the set bits of the node's row (a) / column (a^T), and the
+// diagonal is removed once per side.  O(Ne H (log nd + deg)) per commit instead of
+// O(Ne^2 H).  Rounding contract (fp contract off): E1 row form z0 = fl(u_i + fl(x_j w1)),
+// EE z0 = fma(x_j, w, U_i); the searches, corrections and backward masks share it.
+// Thread map: wave g of the block owns hidden units [5g, 5g+5), lane = node of the tile.
 // ---------------------------------------------------------------------------------
-template <int MODE>
-__device__ __forceinline__ void ent_fwd_body(const float* __restrict__ x,
-                                             const uint32_t* __restrict__ abits,
-                                             const uint32_t* __restrict__ aT,
-                                             const float* __restrict__ W, const Off& o, int Ne,
-                                             float* __restrict__ out0, float* __restrict__ out1,
-                                             float* buf) {
-#pragma clang fp contract(off)
-  const int b = blockIdx.y, t0 = blockIdx.x * TN;
-  const int lane = threadIdx.x & 63;
-  const int i = t0 + lane, ic = i < Ne ? i : Ne - 1;
-  const int WE = (Ne + 31) >> 5;
-  const float* xb = x + (size_t)b * Ne;
-  const float xi = xb[ic];
-  float wr[H], wc[H], ur[H], uc[H], dd[H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    if constexpr (MODE == 0) {
-      const float w0 = W[o.E1_W1 + k], w1 = W[o.E1_W1 + H + k], w2 = W[o.E1_W1 + 2 * H + k];
-      const float c0 = w2 + W[o.E1_B1 + k];
-      dd[k] = W[o.E1_W1 + 3 * H + k] - w2;
-      wr[k] = w1;
-      wc[k] = w0;
-      ur[k] = fmaf(xi, w0, c0);
-      uc[k] = fmaf(xi, w1, c0);
-    } else {
-      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
-      dd[k] = W[o.EE_W12 + H + k] - w20;
-      wr[k] = w;
-      wc[k] = w;
-      ur[k] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
-      uc[k] = ur[k];
-    }
+constexpr int KPW = H / NW;   // hidden units per wave
+
+struct SortTabs {
+  const float* xu;
+  const int* cum;
+  const double* pxd;
+  int nd;
+};
+
+__device__ __forceinline__ SortTabs sort_tabs(const uint32_t* prep, const GenPrep& GP, int b) {
+  const uint32_t* pp = prep + (size_t)b * GP.words;
+  SortTabs T;
+  T.xu = reinterpret_cast<const float*>(pp + GP.xu);
+  T.cum = reinterpret_cast<const int*>(pp + GP.cum);
+  T.pxd = reinterpret_cast<const double*>(pp + GP.pxd);
+  T.nd = (int)pp[GP.meta];
+  return T;
+}
+
+__device__ __forceinline__ int top_pow2(int n) { return 1 << (31 - __builtin_clz((unsigned)n)); }
+
+// boundary q of the set {distinct values v : pred(v)} when pred is monotone: with
+// inc = pred increasing in v the set is [q, nd) (suffix), otherwise [0, q) (prefix)
+template <class P>
+__device__ __forceinline__ int set_bound(const SortTabs& T, bool inc, P pred) {
+  int q = 0;
+  for (int s = top_pow2(T.nd); s > 0; s >>= 1) {
+    const int m = q + s - 1;
+    if (m < T.nd && pred(T.xu[m]) != inc) q += s;
   }
-  float ar[H], ac[H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) { ar[k] = 0.f; ac[k] = 0.f; }
-  const uint32_t* rowb = abits + ((size_t)b * Ne + ic) * WE;
-  const uint32_t* colb = aT + ((size_t)b * Ne + ic) * WE;
-  sweep(Ne, t0, [&](int j, bool self) {
-    const float xj = xb[j];
-    const float fr = bitf(rowb, j), fc = bitf(colb, j);
-    const bool on = !(self && j == i);
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const float zr = fmaf(fr, dd[k], fmaf(xj, wr[k], ur[k]));
-      const float zc = fmaf(fc, dd[k], fmaf(xj, wc[k], uc[k]));
-      ar[k] += on ? relu(zr) : 0.f;
-      ac[k] += on ? relu(zc) : 0.f;
-    }
-  });
-  float* bufr = buf;
-  float* bufc = buf + NW * TN * HP;
-  float* resr = buf + 2 * NW * TN * HP;
-  float* resc = resr + TN * HP;
-  combine4(ar, bufr, resr);
-  combine4(ac, bufc, resc);
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
-    const int n = e / H, k = e - n * H;
-    if (t0 + n >= Ne) continue;
-    const size_t g = ((size_t)b * Ne + t0 + n) * H + k;
-    if constexpr (MODE == 0) {
-      out0[g] = resr[n * HP + k] + resc[n * HP + k];
-    } else {
-      out0[g] = resr[n * HP + k];
-      out1[g] = resc[n * HP + k];
+  return q;
+}
+
+// walk the set bits j != i of a bit row: f(j)
+template <class F>
+__device__ __forceinline__ void for_bits(const uint32_t* row, int WE, int i, F f) {
+  for (int w = 0; w < WE; ++w) {
+    uint32_t m = row[w];
+    if ((i >> 5) == w) m &= ~(1u << (i & 31));
+    while (m) {
+      const int j = 32 * w + __builtin_ctz(m);
+      m &= m - 1u;
+      f(j);
     }
   }
 }
 
+// MODE 0 (E1, model_2.py:161-188): P_i = sum_{j!=i} relu(z_ij) + relu(z_ji)
+// MODE 1 (EE, model_4.py:206-243): R1_i = sum_{j!=i} relu(z'_ij), C1_i = sum relu(z'_ji)
+template <int MODE>
+__device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
+                                               const uint32_t* __restrict__ abits,
+                                               const uint32_t* __restrict__ aT,
+                                               const uint32_t* __restrict__ prep,
+                                               const float* __restrict__ W, const Off& o, int Ne,
+                                               int Nc, float* __restrict__ out0,
+                                               float* __restrict__ out1) {
+#pragma clang fp contract(off)
+  const GenPrep GP = gen_prep(Ne, Nc);
+  const int b = blockIdx.y, t0 = blockIdx.x * TN;
+  const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
+  const int i = t0 + lane;
+  if (i >= Ne) return;   // no barriers below
+  const int WE = (Ne + 31) >> 5;
+  const SortTabs T = sort_tabs(prep, GP, b);
+  const float* xb = x + (size_t)b * Ne;
+  const float xi = xb[i];
+  const uint32_t* rowb = abits + ((size_t)b * Ne + i) * WE;
+  const uint32_t* colb = aT + ((size_t)b * Ne + i) * WE;
+  float u[KPW], v[KPW], s1[KPW], s2[KPW], c0[KPW], wa[KPW], wb[KPW], dd[KPW];
+  double dense[KPW], dense2[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    if constexpr (MODE == 0) {
+      const float w0 = W[o.E1_W1 + k], w1 = W[o.E1_W1 + H + k], w2 = W[o.E1_W1 + 2 * H + k];
+      c0[kk] = w2 + W[o.E1_B1 + k];
+      dd[kk] = W[o.E1_W1 + 3 * H + k] - w2;
+      wa[kk] = w0;
+      wb[kk] = w1;
+      u[kk] = fmaf(xi, w0, c0[kk]);
+      v[kk] = xi * w1;
+      const float uu = u[kk], vv = v[kk], cc = c0[kk];
+      const int br = set_bound(T, w1 >= 0.f, [&](float xq) { return (uu + xq * w1) > 0.f; });
+      const int bc = set_bound(T, w0 >= 0.f, [&](float xq) { return (fmaf(xq, w0, cc) + vv) > 0.f; });
+      const int rlo = w1 >= 0.f ? br : 0, rhi = w1 >= 0.f ? T.nd : br;
+      const int clo = w0 >= 0.f ? bc : 0, chi = w0 >= 0.f ? T.nd : bc;
+      double acc = (double)(T.cum[rhi] - T.cum[rlo]) * (double)uu +
+                   (double)w1 * (T.pxd[rhi] - T.pxd[rlo]);
+      acc += (double)(T.cum[chi] - T.cum[clo]) * ((double)vv + (double)cc) +
+             (double)w0 * (T.pxd[chi] - T.pxd[clo]);
+      acc -= 2.0 * (double)relu(uu + vv);
+      dense[kk] = acc;
+    } else {
+      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
+      dd[kk] = W[o.EE_W12 + H + k] - w20;
+      wa[kk] = w;
+      u[kk] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
+      const float uu = u[kk];
+      const int br = set_bound(T, w >= 0.f, [&](float xq) { return fmaf(xq, w, uu) > 0.f; });
+      const int lo = w >= 0.f ? br : 0, hi = w >= 0.f ? T.nd : br;
+      const double acc = (double)(T.cum[hi] - T.cum[lo]) * (double)uu +
+                         (double)w * (T.pxd[hi] - T.pxd[lo]) - (double)relu(fmaf(xi, w, uu));
+      dense[kk] = acc;
+      dense2[kk] = acc;
+    }
+    s1[kk] = 0.f;
+    s2[kk] = 0.f;
+  }
+  // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i))
+  for_bits(rowb, WE, i, [&](int j) {
+    const float xj = xb[j];
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = MODE == 0 ? u[kk] + xj * wb[kk] : fmaf(xj, wa[kk], u[kk]);
+      s1[kk] += relu(z0 + dd[kk]) - relu(z0);
+    }
+  });
+  for_bits(colb, WE, i, [&](int j) {
+    const float xj = xb[j];
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = MODE == 0 ? fmaf(xj, wa[kk], c0[kk]) + v[kk] : fmaf(xj, wa[kk], u[kk]);
+      s2[kk] += relu(z0 + dd[kk]) - relu(z0);
+    }
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const size_t gi = ((size_t)b * Ne + i) * H + g * KPW + kk;
+    if constexpr (MODE == 0) {
+      out0[gi] = (float)dense[kk] + (s1[kk] + s2[kk]);
+    } else {
+      out0[gi] = (float)dense[kk] + s1[kk];
+      out1[gi] = (float)dense2[kk] + s2[kk];
+    }
+  }
+}
+
+// grid (te, B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage
 __global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
                                                  const uint32_t* __restrict__ abits,
                                                  const uint32_t* __restrict__ aT,
+                                                 const uint32_t* __restrict__ prep,
                                                  const float* __restrict__ W, Off o, int Ne,
-                                                 int ent, float* __restrict__ P,
+                                                 int Nc, int ent, float* __restrict__ P,
                                                  float* __restrict__ R1, float* __restrict__ C1) {
-  __shared__ float buf[2 * NW * TN * HP + 2 * TN * HP];
   if (blockIdx.z == 0 && ent)
-    ent_fwd_body<0>(x, abits, aT, W, o, Ne, P, nullptr, buf);
+    ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
   else
-    ent_fwd_body<1>(x, abits, aT, W, o, Ne, R1, C1, buf);
+    ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
 }
 
 // ---------------------------------------------------------------------------------
@@ -483,7 +584,7 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
     const uint32_t* __restrict__ prep, const float* __restrict__ xv, const float* __restrict__ W,
     Off o, int Ne, int Nc, const unsigned long long* __restrict__ ncacc,
     float* __restrict__ nvec, float* __restrict__ alpha, float* __restrict__ beta) {
-  const PrepLayout PL = prep_layout(Ne, Nc);
+  const GenPrep PL = gen_prep(Ne, Nc);
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   const int c = blockIdx.x * NW + uni(threadIdx.x >> 6);
   if (c >= Nc) return;   // wave-uniform; no block barrier below
@@ -884,7 +985,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     float* __restrict__ rhoE, float* __restrict__ part, Segs sg) {
   __shared__ float dxq[NW * TN], xs[TN], dov[TN];
   __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
-  const PrepLayout PL = prep_layout(Ne, Nc);
+  const GenPrep PL = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
   const int lane = t & 63, w = t >> 6;
   const int I = t0 + lane;
@@ -974,88 +1075,185 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ent_bwd  grid (te, B): mlp_entity_B1 first layer backward (model_2.py:165-170):
-//   dz_ij = [z_ij > 0] (rho_i + rho_j);  dW1 = [sum x_i dz, sum x_j dz, sum (1-a) dz,
-//   sum a dz], db1 = sum dz.  Lane = row i, the j sweep split over the waves.
+// First-layer backward of the entity pair MLPs, sorted-x form.
+//   E1 (model_2.py:165-170):  dz_ij = [z_ij > 0] (rho_i + rho_j)         (r = q = rho = dP)
+//   EE (model_4.py:212-223):  dz'_ij = [z'_ij > 0] (phi_i + psi_j)       (r = phi, q = psi)
+//   S0 = sum x_i dz, S1 = sum x_j dz, S2 = sum dz, S3 = sum a dz over all pairs.
+// For node i the a = 0 set is the forward's prefix / suffix, so sum_{j in set} q_j and
+// sum x_j q_j are single reads of per-k scan tables over the x-sorted order (suffix
+// sums when the slope is >= 0, prefix sums otherwise; f64), built by kw_scan; the a = 1
+// pairs correct the mask over the set bits of row i; the diagonal is removed.
 // ---------------------------------------------------------------------------------
-template <int MODE>   // 0: entity stage (rho_i + rho_j), 1: EE (phi_i + psi_j)
+// kw_scan  grid (H, B, modes): tab[mode][b][k][2][Ne+1] (q sums, x q sums), f64
+__global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
+                                              const float* __restrict__ W, Off o, int Ne, int Nc,
+                                              int mode0, const float* __restrict__ q0,
+                                              const float* __restrict__ q1,
+                                              double* __restrict__ tab) {
+  __shared__ double c1[NT], c2[NT];
+  const GenPrep GP = gen_prep(Ne, Nc);
+  const int k = blockIdx.x, b = blockIdx.y, mode = mode0 + blockIdx.z, t = threadIdx.x;
+  const int B = gridDim.y;
+  const uint32_t* pp = prep + (size_t)b * GP.words;
+  const float* xsrt = reinterpret_cast<const float*>(pp + GP.xsrt);
+  const int* perm = reinterpret_cast<const int*>(pp + GP.perm);
+  const float slope = mode == 0 ? W[o.E1_W1 + H + k] : W[o.EE_W11 + k];
+  const bool suf = slope >= 0.f;
+  const float* q = (mode == 0 ? q0 : q1) + (size_t)b * Ne * H;
+  double* T = tab + (((size_t)mode * B + b) * H + k) * 2 * (Ne + 1);
+  const int C = (Ne + NT - 1) / NT;
+  const int p0 = t * C, p1 = p0 + C < Ne ? p0 + C : Ne;
+  double a1 = 0.0, a2 = 0.0;
+  for (int p = p0; p < p1; ++p) {            // p = position in scan order
+    const int m = suf ? Ne - 1 - p : p;
+    const double val = (double)q[(size_t)perm[m] * H + k];
+    a1 += val;
+    a2 += val * (double)xsrt[m];
+  }
+  c1[t] = a1;
+  c2[t] = a2;
+  __syncthreads();
+  if (t == 0) {
+    double r1 = 0.0, r2 = 0.0;
+    for (int u = 0; u < NT; ++u) {
+      const double e1 = c1[u], e2 = c2[u];
+      c1[u] = r1;
+      c2[u] = r2;
+      r1 += e1;
+      r2 += e2;
+    }
+  }
+  __syncthreads();
+  a1 = c1[t];
+  a2 = c2[t];
+  if (t == 0) {
+    T[suf ? Ne : 0] = 0.0;
+    T[Ne + 1 + (suf ? Ne : 0)] = 0.0;
+  }
+  for (int p = p0; p < p1; ++p) {
+    const int m = suf ? Ne - 1 - p : p;
+    const double val = (double)q[(size_t)perm[m] * H + k];
+    a1 += val;
+    a2 += val * (double)xsrt[m];
+    const int e = suf ? m : m + 1;           // suffix: sum over slots >= m; prefix: < m+1
+    T[e] = a1;
+    T[Ne + 1 + e] = a2;
+  }
+}
+
+template <int MODE>
 __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
                                                    const uint32_t* __restrict__ abits,
+                                                   const uint32_t* __restrict__ prep,
                                                    const float* __restrict__ W, Off o, int Ne,
-                                                   const float* __restrict__ ra,
+                                                   int Nc, const float* __restrict__ ra,
                                                    const float* __restrict__ rb,
+                                                   const double* __restrict__ tab,
                                                    float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ float red[NW * 4 * H];
-  __shared__ float tot[4 * H];
-  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
-  const int lane = threadIdx.x & 63;
+  const GenPrep GP = gen_prep(Ne, Nc);
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x, B = gridDim.y;
+  const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
   const int i = t0 + lane;
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
   const int WE = (Ne + 31) >> 5;
+  const SortTabs T = sort_tabs(prep, GP, b);
   const float* xb = x + (size_t)b * Ne;
   const float xi = xb[ic];
-  float wr[H], ur[H], dd[H], ri[H];
-  for (int k = 0; k < H; ++k) {
-    if constexpr (MODE == 0) {
-      const float w0 = W[o.E1_W1 + k], w2 = W[o.E1_W1 + 2 * H + k];
-      wr[k] = W[o.E1_W1 + H + k];
-      dd[k] = W[o.E1_W1 + 3 * H + k] - w2;
-      ur[k] = fmaf(xi, w0, w2 + W[o.E1_B1 + k]);
-    } else {
-      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
-      wr[k] = w;
-      dd[k] = W[o.EE_W12 + H + k] - w20;
-      ur[k] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
-    }
-    ri[k] = ra[((size_t)b * Ne + ic) * H + k];
-  }
-  float S1[H], S2[H], S3[H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) { S1[k] = 0.f; S2[k] = 0.f; S3[k] = 0.f; }
-  const uint32_t* rowb = abits + ((size_t)b * Ne + ic) * WE;
   const float* rbb = rb + (size_t)b * Ne * H;
-  sweep(Ne, t0, [&](int j, bool self) {
-    const float xj = xb[j];
-    const float af = bitf(rowb, j);
-    const bool on = live && !(self && j == i);
-    const float* rj = rbb + (size_t)j * H;
+  float S0[KPW], S1[KPW], S2[KPW], S3[KPW], u[KPW], wb[KPW], dd[KPW], ri[KPW];
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const float zz = fmaf(af, dd[k], fmaf(xj, wr[k], ur[k]));
-      const float g = (on && zz > 0.f) ? ri[k] + rj[k] : 0.f;
-      S1[k] = fmaf(xj, g, S1[k]);
-      S2[k] += g;
-      S3[k] = fmaf(af, g, S3[k]);
-    }
-  });
-  float v[4 * H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    v[k] = xi * S2[k];
-    v[H + k] = S1[k];
-    v[2 * H + k] = S2[k];
-    v[3 * H + k] = S3[k];
-  }
-  block_sum<4 * H>(v, red, tot);
-  const int row = b * te + blockIdx.x;
-  const int t = threadIdx.x;
-  if (t < H) {
-    const float s0 = tot[t], s1 = tot[H + t], s2 = tot[2 * H + t], s3 = tot[3 * H + t];
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    float slope;
     if constexpr (MODE == 0) {
-      const Seg& s = sg.s[SG_E1W1];
-      put(part, s, t, row, s0);
-      put(part, s, H + t, row, s1);
-      put(part, s, 2 * H + t, row, s2 - s3);
-      put(part, s, 3 * H + t, row, s3);
-      put(part, s, 4 * H + t, row, s2);
-    } else {   // shared w1_1 sees both slices: sum dz (x_i + x_j)
-      const Seg& s = sg.s[SG_EEW11];
-      put(part, s, t, row, s0 + s1);
-      put(part, s, H + t, row, s2 - s3);
-      put(part, s, 2 * H + t, row, s3);
-      put(part, s, 3 * H + t, row, s2);
+      const float w2 = W[o.E1_W1 + 2 * H + k];
+      slope = W[o.E1_W1 + H + k];
+      dd[kk] = W[o.E1_W1 + 3 * H + k] - w2;
+      u[kk] = fmaf(xi, W[o.E1_W1 + k], w2 + W[o.E1_B1 + k]);
+    } else {
+      const float w20 = W[o.EE_W12 + k];
+      slope = W[o.EE_W11 + k];
+      dd[kk] = W[o.EE_W12 + H + k] - w20;
+      u[kk] = fmaf(xi, slope, w20 + W[o.EE_B1 + k]);
+    }
+    wb[kk] = slope;
+    ri[kk] = ra[((size_t)b * Ne + ic) * H + k];
+    const float uu = u[kk];
+    const bool inc = slope >= 0.f;
+    const int br = MODE == 0
+        ? set_bound(T, inc, [&](float xq) { return (uu + xq * slope) > 0.f; })
+        : set_bound(T, inc, [&](float xq) { return fmaf(xq, slope, uu) > 0.f; });
+    const int lo = inc ? br : 0, hi = inc ? T.nd : br;
+    const double cnt = (double)(T.cum[hi] - T.cum[lo]);
+    const double sx = T.pxd[hi] - T.pxd[lo];
+    const double* Tk = tab + (((size_t)MODE * B + b) * H + k) * 2 * (Ne + 1);
+    const int bm = T.cum[br];
+    double gs = cnt * (double)ri[kk] + Tk[bm];
+    double gx = (double)ri[kk] * sx + Tk[Ne + 1 + bm];
+    const float zii = MODE == 0 ? uu + xi * slope : fmaf(xi, slope, uu);
+    if (zii > 0.f) {                              // remove j == i
+      const double gi = (double)ri[kk] + (double)rbb[(size_t)ic * H + k];
+      gs -= gi;
+      gx -= (double)xi * gi;
+    }
+    S2[kk] = (float)gs;
+    S1[kk] = (float)gx;
+    S0[kk] = 0.f;                                 // x_i-weighted corrections only
+    S3[kk] = 0.f;
+  }
+  float cs[KPW];                                  // sum of the corrections' dm
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) cs[kk] = 0.f;
+  if (live) {
+    for_bits(abits + ((size_t)b * Ne + i) * WE, WE, i, [&](int j) {
+      const float xj = xb[j];
+      const float* qj = rbb + (size_t)j * H + g * KPW;
+#pragma unroll
+      for (int kk = 0; kk < KPW; ++kk) {
+        const float z0 = MODE == 0 ? u[kk] + xj * wb[kk] : fmaf(xj, wb[kk], u[kk]);
+        const float z1 = z0 + dd[kk];
+        const float gg = ri[kk] + qj[kk];
+        const float m1 = z1 > 0.f ? gg : 0.f, m0 = z0 > 0.f ? gg : 0.f;
+        const float dm = m1 - m0;
+        cs[kk] += dm;
+        S1[kk] = fmaf(xj, dm, S1[kk]);
+        S3[kk] += m1;
+      }
+    });
+  }
+  float v[4 * KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const float s2 = live ? S2[kk] + cs[kk] : 0.f;
+    v[kk] = live ? xi * s2 : 0.f;                  // S0 = sum_i x_i (row sum of dz)
+    v[KPW + kk] = live ? S1[kk] : 0.f;
+    v[2 * KPW + kk] = s2;
+    v[3 * KPW + kk] = live ? S3[kk] : 0.f;
+  }
+  const int row = b * te + blockIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4 * KPW; ++q) v[q] = wsum(v[q]);
+  if (lane == 0) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int k = g * KPW + kk;
+      const float s0 = v[kk], s1 = v[KPW + kk], s2 = v[2 * KPW + kk], s3 = v[3 * KPW + kk];
+      if constexpr (MODE == 0) {
+        const Seg& s = sg.s[SG_E1W1];
+        put(part, s, k, row, s0);
+        put(part, s, H + k, row, s1);
+        put(part, s, 2 * H + k, row, s2 - s3);
+        put(part, s, 3 * H + k, row, s3);
+        put(part, s, 4 * H + k, row, s2);
+      } else {   // the shared w1_1 sees both slices: sum dz (x_i + x_j)
+        const Seg& s = sg.s[SG_EEW11];
+        put(part, s, k, row, s0 + s1);
+        put(part, s, H + k, row, s2 - s3);
+        put(part, s, 2 * H + k, row, s3);
+        put(part, s, 3 * H + k, row, s2);
+      }
     }
   }
 }
@@ -1289,6 +1487,53 @@ __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ p
   if (lane == 0) out[blockIdx.x] = a;
 }
 
+// kw_prep_sort  grid (B), 1024 threads, dynamic LDS 2 Ne floats: stable rank sort of x,
+// distinct values, counts below each distinct value and f64 prefix sums (any Ne)
+__global__ __launch_bounds__(1024) void kw_prep_sort(const float* __restrict__ x,
+                                                     uint32_t* __restrict__ prep, int Ne, int Nc) {
+  extern __shared__ float xl[];
+  float* xs = xl + Ne;
+  const GenPrep GP = gen_prep(Ne, Nc);
+  const int b = blockIdx.x, t = threadIdx.x;
+  uint32_t* pb = prep + (size_t)b * GP.words;
+  float* xsrt = reinterpret_cast<float*>(pb + GP.xsrt);
+  int* perm = reinterpret_cast<int*>(pb + GP.perm);
+  for (int i = t; i < Ne; i += 1024) xl[i] = x[(size_t)b * Ne + i];
+  __syncthreads();
+  for (int i = t; i < Ne; i += 1024) {
+    const float xi = xl[i];
+    int r = 0;
+    for (int j = 0; j < Ne; ++j) {
+      const float xj = xl[j];
+      r += (xj < xi || (xj == xi && j < i)) ? 1 : 0;
+    }
+    xs[r] = xi;
+    xsrt[r] = xi;
+    perm[r] = i;
+  }
+  __syncthreads();
+  if (t == 0) {   // serial over the sorted values, once per uploaded batch
+    float* xu = reinterpret_cast<float*>(pb + GP.xu);
+    int* cum = reinterpret_cast<int*>(pb + GP.cum);
+    double* pxd = reinterpret_cast<double*>(pb + GP.pxd);
+    int nd = 0;
+    double acc = 0.0;
+    for (int m = 0; m < Ne; ++m) {
+      const float v = xs[m];
+      if (m == 0 || v != xs[m - 1]) {
+        xu[nd] = v;
+        cum[nd] = m;
+        pxd[nd] = acc;
+        ++nd;
+      }
+      acc += (double)v;
+    }
+    cum[nd] = Ne;
+    pxd[nd] = acc;
+    pb[GP.meta] = (uint32_t)nd;
+  }
+}
+
 // transposed class bits: out[b][j][w] bit l = in[b][32w + l][j]
 __global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
                                                 uint32_t* __restrict__ out, int N) {
@@ -1315,6 +1560,7 @@ struct WideWork {
   size_t nvec, alpha, beta, G, Hh, sig, tau, Dsig, Dtau, dG, dH, Dal, Dbe, dn;   // hunk
   size_t gam;                                     // [B][Nc][Nc]
   size_t D;                                       // derived weights
+  size_t tab;                                     // f64 scan tables [2][B][H][2][Ne+1]
   size_t part;                                    // partial rows
   Segs segs;
   size_t total;
@@ -1349,6 +1595,7 @@ WideWork wide_layout(const hdg_shape* s) {
   w.dn = take(B * Nc * 4);
   w.gam = take(B * Nc * Nc);
   w.D = take(D_WORDS);
+  if (has_ent(v) || has_ee(v)) w.tab = take(2 * 2 * B * H * 2 * (Ne + 1));   // doubles
   const int te = (int)((Ne + TN - 1) / TN), tc = (int)((Nc + TN - 1) / TN);
   const int rc = (int)B * tc, re = (int)B * te;
   auto seg = [&](int id, int p0, int n, int rows) {
@@ -1392,12 +1639,16 @@ size_t wide_workspace_bytes(const hdg_shape* s) { return wide_layout(s).total * 
 
 size_t wide_prep_bytes(const hdg_shape* s) {
   const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
-  return (B * prep_layout(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
+  return (B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
 }
 
 int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
-  WTRY(launch_prep_maps(s, bt, st));
-  uint32_t* aT = (uint32_t*)bt->prep + (size_t)s->batch * prep_layout(s->ne, s->nc).words;
+  const GenPrep GP = gen_prep(s->ne, s->nc);
+  WTRY(launch_prep_maps(s, bt, GP.words, GP.ks, GP.kt, GP.ncst, st));
+  hipLaunchKernelGGL(kw_prep_sort, dim3(s->batch), dim3(1024), (size_t)2 * s->ne * 4, st, bt->x,
+                     (uint32_t*)bt->prep, s->ne, s->nc);
+  WTRY(hipGetLastError());
+  uint32_t* aT = (uint32_t*)bt->prep + (size_t)s->batch * GP.words;
   uint32_t* yT = aT + (size_t)s->batch * s->ne * ((s->ne + 31) / 32);
   hipLaunchKernelGGL(kw_prep_T, dim3(8, s->batch), dim3(NT), 0, st, bt->abits, aT, s->ne);
   WTRY(hipGetLastError());
@@ -1413,7 +1664,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   const WideWork w = wide_layout(s);
   float* ws = (float*)workspace;
   const uint32_t* prep = (const uint32_t*)bt->prep;
-  const uint32_t* aT = prep + (size_t)B * prep_layout(Ne, Nc).words;
+  const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const uint32_t* yT = aT + (size_t)B * Ne * ((Ne + 31) / 32);
   const int te = (Ne + TN - 1) / TN, tc = (Nc + TN - 1) / TN;
   const bool ent = has_ent(v), ee = has_ee(v);
@@ -1428,7 +1679,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   // ---- entity side ----
   if (ent || ee) {
     hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
-                       bt->abits, aT, params, o, Ne, ent ? 1 : 0, F(w.P), F(w.R1), F(w.C1));
+                       bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P), F(w.R1),
+                       F(w.C1));
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
                        params, o, Ne, ent ? 1 : 0, F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp),
@@ -1482,8 +1734,12 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_node_bwd, dim3(te, B), dim3(NT), 0, st, prep, bt->x, params, o, Ne, Nc,
                        F(w.dn), F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, params, o,
-                       Ne, F(w.rhoE), F(w.rhoE), part, w.segs);
+    hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 0,
+                       F(w.rhoE), nullptr, (double*)F(w.tab));
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, prep,
+                       params, o, Ne, Nc, F(w.rhoE), F(w.rhoE), (const double*)F(w.tab), part,
+                       w.segs);
     WTRY(hipGetLastError());
   }
   if (ee) {
@@ -1495,8 +1751,12 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
                        F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, params, o,
-                       Ne, F(w.phi), F(w.psi), part, w.segs);
+    hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
+                       nullptr, F(w.psi), (double*)F(w.tab));
+    WTRY(hipGetLastError());
+    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, prep,
+                       params, o, Ne, Nc, F(w.phi), F(w.psi), (const double*)F(w.tab), part,
+                       w.segs);
     WTRY(hipGetLastError());
   }
   hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + 4), dim3(64), 0, st, part, w.segs, 0, grad);
