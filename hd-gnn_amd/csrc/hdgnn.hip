@@ -175,9 +175,10 @@ __device__ __forceinline__ void pair_tile(
       const float af = (ABL & 1) ? 0.f : (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
       const p2 af2 = {af, af};
       float g = 0.f;
-      if constexpr (MODE == 2) {   // branch-free: clamped load, masked value
-        const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;
-        g = gam[ic * gld + jc] * ((iv && j < N && j != i) ? 1.f : 0.f);
+      if constexpr (MODE == 2) {   // branch-free: clamped load, selected (not multiplied:
+        const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;   // garbage * 0 can be NaN)
+        const float gl = gam[ic * gld + jc];
+        g = (iv && j < N && j != i) ? gl : 0.f;
       }
       const float* Bj = Bv + j * LD + k0;
 #pragma unroll
@@ -1228,7 +1229,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       if (prb) { prb[e] = p0; prb[Pc + e] = p1; }
       if (lgb) { lgb[e] = z0; lgb[Pc + e] = z1; }
       if constexpr (TRAIN) {
-        if (qq == p) gam[p * NC16 + p] = 0.f;     // defined diagonal (read masked in M8)
+        if (qq == p || (p == Nc1i && qq == Nc1i - 1))   // defined diagonal, every row
+          gam[p * NC16 + p] = 0.f;
         const float gmm = ce_scale * (p1 - yf);   // dL/dz1 = -dL/dz0
         gam[p * NC16 + q] = gmm;
         gsum += gmm;

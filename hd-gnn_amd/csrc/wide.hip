@@ -480,7 +480,9 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
 //   r < n(n-1) on the n-grid (utils2.py:121-137).  Relations outside that range feed
 //   nothing, so only they are evaluated.  Lanes walk index rows i' (one per lane), each
 //   wave a quarter of the j' range; relation r -> entity pair (i, j) on the Ne-grid is
-//   advanced incrementally.  Source bins: per-lane sums; target bins: wave sums.
+//   advanced incrementally.  Source bins: per-lane sums; target bins: wave sums, both
+//   added to the block's LDS bins in 2^-32 fixed point (integer adds: order-free), which
+//   go out as one partial row per tile.
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                 const int32_t* __restrict__ hidg,
@@ -489,16 +491,20 @@ __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abi
                                                 const float* __restrict__ D, int Ne, int Nc,
                                                 const float* __restrict__ rho,
                                                 const float* __restrict__ gmm,
-                                                unsigned long long* __restrict__ ncacc) {
+                                                unsigned long long* __restrict__ ncpart) {
 #pragma clang fp contract(off)
   extern __shared__ unsigned long long bins[];
   const int b = blockIdx.y, t0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  if (n < 2 || t0 >= n) return;   // block-uniform
   for (int c = threadIdx.x; c < 2 * Nc; c += NT) bins[c] = 0ull;
   __syncthreads();
+  if (n < 2 || t0 >= n) {         // block-uniform: this tile holds no index row
+    for (int c = threadIdx.x; c < 2 * Nc; c += NT) outp[c] = 0ull;
+    return;
+  }
   const int WE = (Ne + 31) >> 5;
   const int32_t* hid = hidg + (size_t)b * Ne;
   const int ip = t0 + lane;
@@ -569,8 +575,9 @@ __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abi
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * Nc; c += NT)
-    if (bins[c]) atomicAdd(&ncacc[(size_t)b * 2 * Nc + c], bins[c]);
+  // per-tile partial bins, summed in tile order by kw_cross_fwd (no global atomics: the
+  // L2s of the 8 XCDs are not coherent for device-scope atomics on coarse-grained memory)
+  for (int c = threadIdx.x; c < 2 * Nc; c += NT) outp[c] = bins[c];
 }
 
 // ---------------------------------------------------------------------------------
@@ -582,7 +589,7 @@ __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abi
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void kw_cross_fwd(
     const uint32_t* __restrict__ prep, const float* __restrict__ xv, const float* __restrict__ W,
-    Off o, int Ne, int Nc, const unsigned long long* __restrict__ ncacc,
+    Off o, int Ne, int Nc, const unsigned long long* __restrict__ ncpart, int nt,
     float* __restrict__ nvec, float* __restrict__ alpha, float* __restrict__ beta) {
   const GenPrep PL = gen_prep(Ne, Nc);
   const int b = blockIdx.y, lane = threadIdx.x & 63;
@@ -601,9 +608,15 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
   float nv[4];
   nv[0] = wsum(a0);
   nv[1] = wsum(a1);
-  if (ncacc) {
-    nv[2] = (float)((double)ncacc[((size_t)b * Nc + c) * 2] * (1.0 / FIX));
-    nv[3] = (float)((double)ncacc[((size_t)b * Nc + c) * 2 + 1] * (1.0 / FIX));
+  if (ncpart) {                    // EE aggregate: sum of the kw_ee_fwd tile partials
+    unsigned long long a2 = 0ull, a3 = 0ull;
+    for (int tl = 0; tl < nt; ++tl) {
+      const unsigned long long* pr = ncpart + ((size_t)b * nt + tl) * 2 * Nc;
+      a2 += pr[2 * c];
+      a3 += pr[2 * c + 1];
+    }
+    nv[2] = (float)((double)a2 * (1.0 / FIX));
+    nv[3] = (float)((double)a3 * (1.0 / FIX));
   } else {
     const float* ncst = reinterpret_cast<const float*>(pp + PL.ncst);
     nv[2] = ncst[2 * c];
@@ -624,20 +637,89 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
 }
 
 // ---------------------------------------------------------------------------------
+// Hunk pair passes (tile of 64 hunks = lanes, 8 waves split the swept index m).  The
+// swept side's node vectors are staged in LDS in chunks of CHM rows and read as
+// broadcast float4; hidden units run as packed fp32 pairs.  The self pair (n, n) is not
+// a relation: it is accumulated like any other and subtracted once with the identical
+// expression.
+// ---------------------------------------------------------------------------------
+constexpr int NTP = 512;
+constexpr int NWP = NTP / 64;
+constexpr int CHM = 128;
+constexpr int H2 = H / 2;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 ld2(const float* p) { return (f2){p[0], p[1]}; }
+
+// rows [c0, c1) of a [N][H] array -> LDS (float4 copies; rows are 80 B, 16-B aligned)
+__device__ __forceinline__ void stage_rows(float* dst, const float* src, int c0, int c1) {
+  const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)c0 * H);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  for (int e = threadIdx.x; e < (c1 - c0) * (H / 4); e += blockDim.x) d4[e] = s4[e];
+}
+
+// sum the NWP waves' packed accumulators of the 64 lane-nodes -> res[64][HP]
+__device__ __forceinline__ void combine8(const f2 (&acc)[H2], float* buf, float* res) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    buf[(w * TN + lane) * HP + 2 * kk] = acc[kk].x;
+    buf[(w * TN + lane) * HP + 2 * kk + 1] = acc[kk].y;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H;
+    float s = buf[n * HP + k];
+#pragma unroll
+    for (int q = 1; q < NWP; ++q) s += buf[(q * TN + n) * HP + k];
+    res[n * HP + k] = s;
+  }
+  __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum8(float (&v)[NV], float* red, float* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const float s = wsum(v[q]);
+    if (lane == 0) red[w * NV + q] = s;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NV; q += NTP) {
+    float s = red[q];
+    for (int u = 1; u < NWP; ++u) s += red[u * NV + q];
+    out[q] = s;
+  }
+  __syncthreads();
+}
+
+// the wave's share [lo, hi) of chunk [c0, c1)
+__device__ __forceinline__ void wave_share(int c0, int c1, int& lo, int& hi) {
+  const int w = uni(threadIdx.x >> 6), len = c1 - c0;
+  lo = c0 + (len * w) / NWP;
+  hi = c0 + (len * (w + 1)) / NWP;
+}
+
+// ---------------------------------------------------------------------------------
 // kw_hunk_fwd  grid (tc, B, 2): z = 0 row pass (G), 1 column pass (H)
 //   mlp_hunk_B2 first layer relu sums (model_2.py:257-275):
 //     G_p = sum_{q!=p} relu(alpha_p + beta_q + y_pq delta),  H_q = sum_{p!=q} (same)
 //   epilogue: sigma_p = G_p M + s0, tau_q = H_q M + t0 (classifier first layer, 304-318)
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_hunk_fwd(const uint32_t* __restrict__ ybits,
-                                                  const uint32_t* __restrict__ yT,
-                                                  const float* __restrict__ D, int Nc,
-                                                  const float* __restrict__ alpha,
-                                                  const float* __restrict__ beta,
-                                                  float* __restrict__ G, float* __restrict__ Hh,
-                                                  float* __restrict__ sig, float* __restrict__ tau) {
+__global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ ybits,
+                                                   const uint32_t* __restrict__ yT,
+                                                   const float* __restrict__ D, int Nc,
+                                                   const float* __restrict__ alpha,
+                                                   const float* __restrict__ beta,
+                                                   float* __restrict__ G, float* __restrict__ Hh,
+                                                   float* __restrict__ sig, float* __restrict__ tau) {
 #pragma clang fp contract(off)
-  __shared__ float buf[NW * TN * HP + TN * HP];
+  __shared__ __attribute__((aligned(16))) float os_[CHM * H];
+  __shared__ float buf[NWP * TN * HP];
+  __shared__ float res[TN * HP];
   const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63;
   const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
@@ -645,109 +727,148 @@ __global__ __launch_bounds__(NT) void kw_hunk_fwd(const uint32_t* __restrict__ y
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
   const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
-  float ow[H], dl[H], acc[H];
+  f2 ow[H2], dl[H2], acc[H2];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    ow[k] = own[ncl * H + k];
-    dl[k] = D[D_DLT + k];
-    acc[k] = 0.f;
+  for (int kk = 0; kk < H2; ++kk) {
+    ow[kk] = ld2(own + ncl * H + 2 * kk);
+    dl[kk] = ld2(D + D_DLT + 2 * kk);
+    acc[kk] = (f2){0.f, 0.f};
   }
-  sweep(Nc, t0, [&](int m, bool self) {
-    const float yf = bitf(brow, m);
-    const bool on = !(self && m == nd);
-    const float* om = oth + (size_t)m * H;
+  for (int c0 = 0; c0 < Nc; c0 += CHM) {
+    const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
+    __syncthreads();
+    stage_rows(os_, oth, c0, c1);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    int wi = -1;
+    uint32_t word = 0;
+    for (int m = lo; m < hi; ++m) {
+      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
+      const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+      const f2 y2 = {yf, yf};
+      const float4* o4 = reinterpret_cast<const float4*>(os_ + (m - c0) * H);
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const float v = relu(fmaf(yf, dl[k], ow[k] + om[k]));
-      acc[k] += on ? v : 0.f;
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 q = o4[v];
+        acc[2 * v] += relu2(fma2(y2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y}));
+        acc[2 * v + 1] += relu2(fma2(y2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w}));
+      }
     }
-  });
-  float* res = buf + NW * TN * HP;
-  combine4(acc, buf, res);
+  }
+  if ((threadIdx.x >> 6) == 0) {   // remove the self pair once
+    const float yf = bitf(brow, ncl);
+    const f2 y2 = {yf, yf};
+#pragma unroll
+    for (int kk = 0; kk < H2; ++kk)
+      acc[kk] -= relu2(fma2(y2, dl[kk], ow[kk] + ld2(oth + ncl * H + 2 * kk)));
+  }
+  combine8(acc, buf, res);
   float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
   float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
   const float* off = D + (z ? D_T0 : D_S0);
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
     const int n = e / H, k = e - n * H;
     if (t0 + n >= Nc) continue;
-    float s = 0.f;
-    for (int l = 0; l < H; ++l) s = fmaf(res[n * HP + l], D[D_M + l * H + k], s);
+    float sacc = 0.f;
+    for (int l = 0; l < H; ++l) sacc = fmaf(res[n * HP + l], D[D_M + l * H + k], sacc);
     gout[(t0 + n) * H + k] = res[n * HP + k];
-    sout[(t0 + n) * H + k] = s + off[k];
+    sout[(t0 + n) * H + k] = sacc + off[k];
   }
 }
 
 // ---------------------------------------------------------------------------------
-// kw_hunk_cls  grid (tc, B): lane = hunk column q, waves split the rows p
+// kw_hunk_cls  grid (tc, B): lane = hunk column q, the 8 waves split the rows p
 //   mlp_hunkedge_B2 (model_2.py:304-324) + softmax CE (115-118):
 //     kappa_pq = relu(sigma_p + tau_q + y_pq eps), z = kappa U2 + d2, CE = lse(z) - z_y
 //   TRAIN: gamma_pq = 10 / (B Pc) (p1 - y) = dL/dz1 (= -dL/dz0), parked for the backward;
 //   partial rows of dU2, dd2 and the CE sum
 // ---------------------------------------------------------------------------------
 template <bool TRAIN>
-__global__ __launch_bounds__(NT) void kw_hunk_cls(
+__global__ __launch_bounds__(NTP) void kw_hunk_cls(
     const uint32_t* __restrict__ ybits, const float* __restrict__ W, Off o,
     const float* __restrict__ D, int Nc, const float* __restrict__ sig,
     const float* __restrict__ tau, float* __restrict__ probs, float* __restrict__ logits,
     float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ float red[NW * 22];
+  __shared__ __attribute__((aligned(16))) float ss[CHM * H];
+  __shared__ float red[NWP * 22];
   __shared__ float tot[22];
   const int b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
-  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int q = t0 + lane;
   const bool live = q < Nc;
   const int qc = live ? q : Nc - 1;
   const int WC = (Nc + 31) >> 5;
   const int Pc = Nc * (Nc - 1);
-  float tq[H], ep[H], u0[H], u1[H];
+  const float* sgb = sig + (size_t)b * Nc * H;
+  f2 tq[H2], ep[H2], u2[H];   // u2[k] = (U2[k][0], U2[k][1])
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    tq[k] = tau[((size_t)b * Nc + qc) * H + k];
-    ep[k] = D[D_EPS + k];
-    u0[k] = W[o.H2_W2 + 2 * k];
-    u1[k] = W[o.H2_W2 + 2 * k + 1];
+  for (int kk = 0; kk < H2; ++kk) {
+    tq[kk] = ld2(tau + ((size_t)b * Nc + qc) * H + 2 * kk);
+    ep[kk] = ld2(D + D_EPS + 2 * kk);
   }
-  const float b0 = W[o.H2_B2], b1 = W[o.H2_B2 + 1];
+#pragma unroll
+  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.H2_W2 + 2 * k);
+  const f2 bb = ld2(W + o.H2_B2);
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
-  float acc[22];   // 0: CE, 1: sum gamma, 2..21: sum kappa_k gamma
+  float ce = 0.f, gs = 0.f;
+  f2 za[H2];
 #pragma unroll
-  for (int k = 0; k < 22; ++k) acc[k] = 0.f;
-  const int lo = (Nc * wv) / NW, hi = (Nc * (wv + 1)) / NW;
-  for (int p = lo; p < hi; ++p) {
-    const float* sp = sig + ((size_t)b * Nc + p) * H;
-    const float yf = bitf(ybits + ((size_t)b * Nc + p) * WC, qc);
-    float kk[H];
-    float z0 = b0, z1 = b1;
+  for (int kk = 0; kk < H2; ++kk) za[kk] = (f2){0.f, 0.f};
+  for (int c0 = 0; c0 < Nc; c0 += CHM) {
+    const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
+    __syncthreads();
+    stage_rows(ss, sgb, c0, c1);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    for (int p = lo; p < hi; ++p) {
+      const float yf = bitf(ybits + ((size_t)b * Nc + p) * WC, qc);
+      const f2 y2 = {yf, yf};
+      const float4* s4 = reinterpret_cast<const float4*>(ss + (p - c0) * H);
+      f2 kap[H2];
+      f2 zz = bb;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      kk[k] = relu(fmaf(yf, ep[k], sp[k] + tq[k]));
-      z0 = fmaf(kk[k], u0[k], z0);
-      z1 = fmaf(kk[k], u1[k], z1);
-    }
-    const bool valid = live && q != p;
-    if (valid) {
-      const float mx = fmaxf(z0, z1);
-      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
-      const float ssum = e0 + e1, inv = 1.f / ssum;
-      const float p0 = e0 * inv, p1 = e1 * inv;
-      const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
-      if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
-      if (lgb) { lgb[r] = z0; lgb[Pc + r] = z1; }
-      acc[0] += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
-      if constexpr (TRAIN) {
-        const float g = ce_scale * (p1 - yf);
-        gam[((size_t)b * Nc + p) * Nc + q] = g;
-        acc[1] += g;
-#pragma unroll
-        for (int k = 0; k < H; ++k) acc[2 + k] = fmaf(kk[k], g, acc[2 + k]);
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 sv = s4[v];
+        kap[2 * v] = relu2(fma2(y2, ep[2 * v], (f2){sv.x, sv.y} + tq[2 * v]));
+        kap[2 * v + 1] = relu2(fma2(y2, ep[2 * v + 1], (f2){sv.z, sv.w} + tq[2 * v + 1]));
       }
-    } else if (TRAIN && live) {
-      gam[((size_t)b * Nc + p) * Nc + q] = 0.f;   // defined diagonal, read by the passes
+#pragma unroll
+      for (int kk = 0; kk < H2; ++kk) {
+        zz = fma2((f2){kap[kk].x, kap[kk].x}, u2[2 * kk], zz);
+        zz = fma2((f2){kap[kk].y, kap[kk].y}, u2[2 * kk + 1], zz);
+      }
+      const float z0 = zz.x, z1 = zz.y;
+      if (live && q != p) {
+        const float mx = fmaxf(z0, z1);
+        const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+        const float ssum = e0 + e1, inv = 1.f / ssum;
+        const float p0 = e0 * inv, p1 = e1 * inv;
+        const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
+        if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
+        if (lgb) { lgb[r] = z0; lgb[Pc + r] = z1; }
+        ce += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+        if constexpr (TRAIN) {
+          const float g = ce_scale * (p1 - yf);
+          gam[((size_t)b * Nc + p) * Nc + q] = g;
+          gs += g;
+#pragma unroll
+          for (int kk = 0; kk < H2; ++kk) za[kk] = fma2(kap[kk], (f2){g, g}, za[kk]);
+        }
+      } else if (TRAIN && live) {
+        gam[((size_t)b * Nc + p) * Nc + q] = 0.f;   // defined diagonal, read by the passes
+      }
     }
   }
-  block_sum<22>(acc, red, tot);
+  float acc[22];
+  acc[0] = ce;
+  acc[1] = gs;
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) { acc[2 + 2 * kk] = za[kk].x; acc[3 + 2 * kk] = za[kk].y; }
+  block_sum8<22>(acc, red, tot);
   const int row = b * tc + blockIdx.x;
   if (threadIdx.x == 0) put(part, sg.s[SG_CE], 0, row, tot[0]);
   if constexpr (TRAIN) {
@@ -768,8 +889,10 @@ __global__ __launch_bounds__(NT) void kw_hunk_cls(
 //   column pass: Dtau_q = c (.) sum_p e_pq.  Epilogue: dG = Dsig M^T (dH = Dtau M^T) and
 //   the partial rows of dU1 (rows 0..1 from the row pass, rows 2..21 through
 //   X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p), dd1, dV2 and dc2 (model_2.py:265-275).
+//   The row pass reads gamma through a transposing LDS tile (coalesced global loads).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_hunk_clsb(
+constexpr int GTP = CHM + 1;   // gamma tile pitch
+__global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Nc,
     const float* __restrict__ sig, const float* __restrict__ tau, const float* __restrict__ gam,
@@ -777,7 +900,9 @@ __global__ __launch_bounds__(NT) void kw_hunk_clsb(
     float* __restrict__ Dtau, float* __restrict__ dG, float* __restrict__ dH,
     float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ float buf[NW * TN * HP];
+  __shared__ __attribute__((aligned(16))) float os_[CHM * H];
+  __shared__ float gt[TN * GTP];
+  __shared__ float buf[NWP * TN * HP];
   __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
   __shared__ float X[H * H], sumD[H], ysum[H];
   const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
@@ -788,31 +913,56 @@ __global__ __launch_bounds__(NT) void kw_hunk_clsb(
   const float* oth = (z ? sig : tau) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
   const float* gb = gam + (size_t)b * Nc * Nc;
-  float ow[H], ep[H], acc[H], ya[H];
+  f2 ow[H2], ep[H2], acc[H2], ya[H2];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    ow[k] = own[ncl * H + k];
-    ep[k] = D[D_EPS + k];
-    acc[k] = 0.f;
-    ya[k] = 0.f;
+  for (int kk = 0; kk < H2; ++kk) {
+    ow[kk] = ld2(own + ncl * H + 2 * kk);
+    ep[kk] = ld2(D + D_EPS + 2 * kk);
+    acc[kk] = (f2){0.f, 0.f};
+    ya[kk] = (f2){0.f, 0.f};
   }
-  sweep(Nc, t0, [&](int m, bool) {   // gamma's diagonal is 0: no self mask needed
-    const float yf = bitf(brow, m);
-    const float g = z ? gb[(size_t)m * Nc + ncl] : gb[(size_t)ncl * Nc + m];
-    const float* om = oth + (size_t)m * H;
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const float e = (fmaf(yf, ep[k], ow[k] + om[k]) > 0.f) ? g : 0.f;
-      acc[k] += e;
-      ya[k] = fmaf(yf, e, ya[k]);
+  for (int c0 = 0; c0 < Nc; c0 += CHM) {   // gamma's diagonal is 0: no self pair to remove
+    const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
+    __syncthreads();
+    stage_rows(os_, oth, c0, c1);
+    if (z == 0) {
+      const int len = c1 - c0;
+      for (int e = threadIdx.x; e < TN * len; e += NTP) {
+        const int r = e / len, c = e - r * len;
+        gt[r * GTP + c] = (t0 + r < Nc) ? gb[(size_t)(t0 + r) * Nc + c0 + c] : 0.f;
+      }
     }
-  });
-  combine4(acc, buf, res);
-  if (z == 0) combine4(ya, buf, yres);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    int wi = -1;
+    uint32_t word = 0;
+    for (int m = lo; m < hi; ++m) {
+      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
+      const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+      const f2 y2 = {yf, yf};
+      const float g = z ? gb[(size_t)m * Nc + ncl] : gt[lane * GTP + (m - c0)];
+      const float4* o4 = reinterpret_cast<const float4*>(os_ + (m - c0) * H);
+#pragma unroll
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 q = o4[v];
+        const f2 pa = fma2(y2, ep[2 * v], ow[2 * v] + (f2){q.x, q.y});
+        const f2 pb = fma2(y2, ep[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
+        const f2 ea = {pa.x > 0.f ? g : 0.f, pa.y > 0.f ? g : 0.f};
+        const f2 eb = {pb.x > 0.f ? g : 0.f, pb.y > 0.f ? g : 0.f};
+        acc[2 * v] += ea;
+        acc[2 * v + 1] += eb;
+        ya[2 * v] = fma2(y2, ea, ya[2 * v]);
+        ya[2 * v + 1] = fma2(y2, eb, ya[2 * v + 1]);
+      }
+    }
+  }
+  combine8(acc, buf, res);
+  if (z == 0) combine8(ya, buf, yres);
   const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
   float* dout = (z ? Dtau : Dsig) + (size_t)b * Nc * H;
   float* gout = (z ? dH : dG) + (size_t)b * Nc * H;
-  for (int e = threadIdx.x; e < TN * H; e += NT) {   // D = c (.) sums; padding rows -> 0
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {   // D = c (.) sums; padding rows -> 0
     const int n = e / H, k = e - n * H;
     const bool in = t0 + n < Nc;
     const float d = in ? res[n * HP + k] * D[D_CV + k] : 0.f;
@@ -822,27 +972,27 @@ __global__ __launch_bounds__(NT) void kw_hunk_clsb(
     if (in) dout[(t0 + n) * H + k] = d;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < TN * H; e += NT) {   // dG_n[l] = sum_k M[l][k] D_n[k]
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {   // dG_n[l] = sum_k M[l][k] D_n[k]
     const int n = e / H, l = e - n * H;
     if (t0 + n >= Nc) continue;
-    float s = 0.f;
-    for (int k = 0; k < H; ++k) s = fmaf(D[D_M + l * H + k], res[n * HP + k], s);
-    gout[(t0 + n) * H + l] = s;
+    float sacc = 0.f;
+    for (int k = 0; k < H; ++k) sacc = fmaf(D[D_M + l * H + k], res[n * HP + k], sacc);
+    gout[(t0 + n) * H + l] = sacc;
   }
-  for (int e = threadIdx.x; e < H * H; e += NT) {    // X_blk = sum_n G_n (x) D_n
+  for (int e = threadIdx.x; e < H * H; e += NTP) {    // X_blk = sum_n G_n (x) D_n
     const int l = e / H, k = e - l * H;
-    float s = 0.f;
-    for (int n = 0; n < TN; ++n) s = fmaf(Gt[n * HP + l], res[n * HP + k], s);
-    X[e] = s;
+    float sacc = 0.f;
+    for (int n = 0; n < TN; ++n) sacc = fmaf(Gt[n * HP + l], res[n * HP + k], sacc);
+    X[e] = sacc;
   }
   if (threadIdx.x < H) {
     const int k = threadIdx.x;
-    float s = 0.f, y = 0.f;
+    float sd = 0.f, y = 0.f;
     for (int n = 0; n < TN; ++n) {
-      s += res[n * HP + k];
+      sd += res[n * HP + k];
       if (z == 0) y += yres[n * HP + k];
     }
-    sumD[k] = s;
+    sumD[k] = sd;
     ysum[k] = y;
   }
   __syncthreads();
@@ -850,7 +1000,7 @@ __global__ __launch_bounds__(NT) void kw_hunk_clsb(
   const float Nc1 = (float)(Nc - 1);
   const Seg& s2 = sg.s[SG_CLSB_H2];
   const Seg& s1 = sg.s[SG_CLSB_H1];
-  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += NT) {
+  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += NTP) {
     if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
       const int m = e / H, k = e - m * H;
       float a = Nc1 * W[o.H1_B2 + m] * sumD[k];
@@ -887,14 +1037,16 @@ __global__ __launch_bounds__(NT) void kw_hunk_clsb(
 //   row pass: Dalpha_p = sum_q dz, sum y dz;  column pass: Dbeta_q = sum_p dz
 //   partial rows of dV1 (rows 0..3 / 4..7 / 8, 9) and dc1
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_hunk_mlpb(
+__global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
     const float* __restrict__ nvec, float* __restrict__ Dal, float* __restrict__ Dbe,
     float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ float buf[NW * TN * HP];
+  __shared__ __attribute__((aligned(16))) float os_[CHM * H];
+  __shared__ __attribute__((aligned(16))) float ws_[CHM * H];
+  __shared__ float buf[NWP * TN * HP];
   __shared__ float res[TN * HP], yres[TN * HP], nt[TN * 4];
   const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
   const int lane = threadIdx.x & 63;
@@ -905,43 +1057,73 @@ __global__ __launch_bounds__(NT) void kw_hunk_mlpb(
   const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
   const float* woth = (z ? dG : dH) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
-  float ow[H], wo[H], dl[H], acc[H], ya[H];
+  f2 ow[H2], wo[H2], dl[H2], acc[H2], ya[H2];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    ow[k] = own[ncl * H + k];
-    wo[k] = wown[ncl * H + k];
-    dl[k] = D[D_DLT + k];
-    acc[k] = 0.f;
-    ya[k] = 0.f;
+  for (int kk = 0; kk < H2; ++kk) {
+    ow[kk] = ld2(own + ncl * H + 2 * kk);
+    wo[kk] = ld2(wown + ncl * H + 2 * kk);
+    dl[kk] = ld2(D + D_DLT + 2 * kk);
+    acc[kk] = (f2){0.f, 0.f};
+    ya[kk] = (f2){0.f, 0.f};
   }
-  sweep(Nc, t0, [&](int m, bool self) {
-    const float yf = bitf(brow, m);
-    const bool on = !(self && m == nd);
-    const float* om = oth + (size_t)m * H;
-    const float* wm = woth + (size_t)m * H;
+  for (int c0 = 0; c0 < Nc; c0 += CHM) {
+    const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
+    __syncthreads();
+    stage_rows(os_, oth, c0, c1);
+    stage_rows(ws_, woth, c0, c1);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    int wi = -1;
+    uint32_t word = 0;
+    for (int m = lo; m < hi; ++m) {
+      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
+      const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+      const f2 y2 = {yf, yf};
+      const float4* o4 = reinterpret_cast<const float4*>(os_ + (m - c0) * H);
+      const float4* w4 = reinterpret_cast<const float4*>(ws_ + (m - c0) * H);
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const bool pos = on && fmaf(yf, dl[k], ow[k] + om[k]) > 0.f;
-      const float dz = pos ? wo[k] + wm[k] : 0.f;
-      acc[k] += dz;
-      ya[k] = fmaf(yf, dz, ya[k]);
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 q = o4[v], r = w4[v];
+        const f2 pa = fma2(y2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y});
+        const f2 pb = fma2(y2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
+        const f2 ga = wo[2 * v] + (f2){r.x, r.y}, gb2 = wo[2 * v + 1] + (f2){r.z, r.w};
+        const f2 da = {pa.x > 0.f ? ga.x : 0.f, pa.y > 0.f ? ga.y : 0.f};
+        const f2 db = {pb.x > 0.f ? gb2.x : 0.f, pb.y > 0.f ? gb2.y : 0.f};
+        acc[2 * v] += da;
+        acc[2 * v + 1] += db;
+        ya[2 * v] = fma2(y2, da, ya[2 * v]);
+        ya[2 * v + 1] = fma2(y2, db, ya[2 * v + 1]);
+      }
     }
-  });
-  combine4(acc, buf, res);
-  if (z == 0) combine4(ya, buf, yres);
+  }
+  if ((threadIdx.x >> 6) == 0) {   // remove the self pair once
+    const float yf = bitf(brow, ncl);
+    const f2 y2 = {yf, yf};
+#pragma unroll
+    for (int kk = 0; kk < H2; ++kk) {
+      const f2 pr = fma2(y2, dl[kk], ow[kk] + ld2(oth + ncl * H + 2 * kk));
+      const f2 gg = wo[kk] + ld2(woth + ncl * H + 2 * kk);
+      const f2 dz = {pr.x > 0.f ? gg.x : 0.f, pr.y > 0.f ? gg.y : 0.f};
+      acc[kk] -= dz;
+      ya[kk] -= y2 * dz;
+    }
+  }
+  combine8(acc, buf, res);
+  if (z == 0) combine8(ya, buf, yres);
   float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H;
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
     const int n = e / H, k = e - n * H;
     const bool in = t0 + n < Nc;
     if (!in) { res[n * HP + k] = 0.f; yres[n * HP + k] = 0.f; }
     else dout[(t0 + n) * H + k] = res[n * HP + k];
   }
-  for (int e = threadIdx.x; e < TN * 4; e += NT)
+  for (int e = threadIdx.x; e < TN * 4; e += NTP)
     nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
   __syncthreads();
   const int row = (b * tc + blockIdx.x) * 2 + z;
   const Seg& s = sg.s[SG_MLPB];
-  for (int e = threadIdx.x; e < 11 * H; e += NT) {   // rows 0..9 of V1, then c1
+  for (int e = threadIdx.x; e < 11 * H; e += NTP) {   // rows 0..9 of V1, then c1
     const int l = e / H, k = e - l * H;
     float a = 0.f;
     if (l < 8) {
@@ -1556,7 +1738,7 @@ __global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
 struct WideWork {
   size_t xp, ov, P, Eb, hE, rhoE;                 // entity stage   [B][Ne](*H)
   size_t R1, C1, Rn, Cn, rho, gmm, drho, dgam, phi, psi;   // EE     [B][Ne][H]
-  size_t ncacc;                                   // u64 [B][Nc][2]
+  size_t ncpart;                                  // u64 [B][te][Nc][2] EE partial bins
   size_t nvec, alpha, beta, G, Hh, sig, tau, Dsig, Dtau, dG, dH, Dal, Dbe, dn;   // hunk
   size_t gam;                                     // [B][Nc][Nc]
   size_t D;                                       // derived weights
@@ -1586,7 +1768,7 @@ WideWork wide_layout(const hdg_shape* s) {
     w.R1 = take(NEH); w.C1 = take(NEH); w.Rn = take(NEH); w.Cn = take(NEH);
     w.rho = take(NEH); w.gmm = take(NEH); w.drho = take(NEH); w.dgam = take(NEH);
     w.phi = take(NEH); w.psi = take(NEH);
-    w.ncacc = take(B * Nc * 4);
+    w.ncpart = take(B * ((Ne + TN - 1) / TN) * Nc * 4);
   }
   w.nvec = take(B * Nc * 4);
   w.alpha = take(NCH); w.beta = take(NCH); w.G = take(NCH); w.Hh = take(NCH);
@@ -1687,25 +1869,24 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.rho), F(w.gmm));
     WTRY(hipGetLastError());
   }
-  unsigned long long* ncacc = ee ? (unsigned long long*)F(w.ncacc) : nullptr;
+  unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
   if (ee) {
-    WTRY(hipMemsetAsync(ncacc, 0, (size_t)B * Nc * 2 * 8, st));
     hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NT), (size_t)Nc * 16, st, bt->abits, bt->hid,
-                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), ncacc);
+                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), ncpart);
     WTRY(hipGetLastError());
   }
   // ---- hunk side ----
   hipLaunchKernelGGL(kw_cross_fwd, dim3((Nc + NW - 1) / NW, B), dim3(NT), 0, st, prep,
-                     ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncacc, F(w.nvec), F(w.alpha),
+                     ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncpart, te, F(w.nvec), F(w.alpha),
                      F(w.beta));
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+  hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
                      F(w.alpha), F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
   WTRY(hipGetLastError());
   float* probs = out ? out->probs : nullptr;
   float* logits = out ? out->logits : nullptr;
   if (!train) {
-    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NT), 0, st, bt->ybits, params, o, D,
+    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NTP), 0, st, bt->ybits, params, o, D,
                        Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
     WTRY(hipGetLastError());
     if (ce_sum) {
@@ -1714,14 +1895,14 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
     return 0;
   }
-  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NT), 0, st, bt->ybits, params, o, D, Nc,
+  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, bt->ybits, params, o, D, Nc,
                      F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, params, o, D,
+  hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o, D,
                      Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig), F(w.Dtau),
                      F(w.dG), F(w.dH), part, w.segs);
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+  hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
                      F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe), part,
                      w.segs);
   WTRY(hipGetLastError());

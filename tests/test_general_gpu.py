@@ -202,3 +202,26 @@ def test_general_graph_replay_equals_eager():
         e2.replay()
     torch.cuda.synchronize()
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.probs, e2.probs)
+
+
+@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN), (1, GEN)])
+def test_workspace_garbage_does_not_leak(v, path):
+    """Every workspace word a step reads it wrote first: prefilling the caller's workspace,
+    gradient and outputs with NaN / Inf / huge values must not change one bit (a kernel that
+    masks an unwritten value by multiplying with 0 turns NaN garbage into NaN output)."""
+    B, ne, nc = 3, 60, 21
+    cb = synth_commits(B, ne, nc, 8)
+    ref = _engine(B, ne, nc, v, path)
+    ref.set_params(layout.init_flat(5, v))
+    db = ref.upload(cb)
+    ref.workspace.zero_()
+    ref.fwd_bwd(db)
+    g0, p0 = ref.grad.clone(), ref.probs.clone()
+    for fill in (float("nan"), float("inf"), -float("inf"), 1e30, -3e38):
+        e = _engine(B, ne, nc, v, path)
+        e.set_params(layout.init_flat(5, v))
+        for t in (e.workspace, e.grad, e.probs, e.logits):
+            t.fill_(fill)
+        e.fwd_bwd(db)
+        torch.cuda.synchronize()
+        assert torch.equal(e.grad, g0) and torch.equal(e.probs, p0), "fill %g" % fill

@@ -57,6 +57,8 @@ def test_rccl_step_matches_single_process(world1, v):
         dp.train_step(db)               # eager: hdg_fwd_bwd -> all_reduce -> hdg_adam_tf
         dg.replay()
     torch.cuda.synchronize()
+    for name, e in (("single", single), ("dp", dp), ("dg", dg)):
+        assert bool(torch.isfinite(e.params).all()), name
     assert torch.equal(dp.params, dg.params) and torch.equal(dp.stats, dg.stats)
     np.testing.assert_allclose(dp.get_params(), single.get_params(), rtol=0, atol=1e-7)
     np.testing.assert_allclose(dp.stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-6)
