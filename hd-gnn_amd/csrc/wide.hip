@@ -146,6 +146,11 @@ __device__ __forceinline__ void put(float* part, const Seg& s, int q, int row, f
   part[s.off + (long long)q * s.rows + row] = v;
 }
 
+// copy n floats of the parameter vector (or any global array) into LDS (no barrier)
+__device__ __forceinline__ void stage_w(float* dst, const float* src, int n) {
+  for (int e = threadIdx.x; e < n; e += blockDim.x) dst[e] = src[e];
+}
+
 // ---------------------------------------------------------------------------------
 // kw_derive: weight products every phase reads (1 block)
 // ---------------------------------------------------------------------------------
@@ -259,6 +264,33 @@ __device__ __forceinline__ SortTabs sort_tabs(const uint32_t* prep, const GenPre
   return T;
 }
 
+// the commit's sorted tables copied into LDS (dynamic, sort_lds_bytes); all threads
+__device__ __forceinline__ SortTabs stage_tabs(const uint32_t* prep, const GenPrep& GP, int b,
+                                               int Ne, void* lds) {
+  const SortTabs G = sort_tabs(prep, GP, b);
+  const int NE4 = (Ne + 3) & ~3;
+  double* pxd = reinterpret_cast<double*>(lds);
+  int* cum = reinterpret_cast<int*>(pxd + NE4 + 4);
+  float* xu = reinterpret_cast<float*>(cum + NE4 + 4);
+  for (int e = threadIdx.x; e <= G.nd; e += blockDim.x) {
+    pxd[e] = G.pxd[e];
+    cum[e] = G.cum[e];
+    if (e < G.nd) xu[e] = G.xu[e];
+  }
+  __syncthreads();
+  SortTabs T;
+  T.xu = xu;
+  T.cum = cum;
+  T.pxd = pxd;
+  T.nd = G.nd;
+  return T;
+}
+
+__host__ __device__ inline size_t sort_lds_bytes(int Ne) {
+  const size_t NE4 = (Ne + 3) & ~3;
+  return (NE4 + 4) * 8 + (NE4 + 4) * 4 + NE4 * 4;
+}
+
 __device__ __forceinline__ int top_pow2(int n) { return 1 << (31 - __builtin_clz((unsigned)n)); }
 
 // boundary q of the set {distinct values v : pred(v)} when pred is monotone: with
@@ -302,9 +334,10 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   const int b = blockIdx.y, t0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
   const int i = t0 + lane;
+  extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
+  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds);
   if (i >= Ne) return;   // no barriers below
   const int WE = (Ne + 31) >> 5;
-  const SortTabs T = sort_tabs(prep, GP, b);
   const float* xb = x + (size_t)b * Ne;
   const float xi = xb[i];
   const uint32_t* rowb = abits + ((size_t)b * Ne + i) * WE;
@@ -406,39 +439,46 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
     const float* __restrict__ C1, float* __restrict__ Rn, float* __restrict__ Cn,
     float* __restrict__ rho, float* __restrict__ gmm) {
   __shared__ float A[TN * HP], Bs[TN * HP], Cs[TN * HP], Ds[TN * HP];
+  __shared__ float Wl[896];                       // the block's weights, staged once
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x;
   const int nn = Ne - t0 < TN ? Ne - t0 : TN;
   const size_t base = ((size_t)b * Ne + t0) * H;
   const float Ne1 = (float)(Ne - 1);
   if (blockIdx.z == 0 && ent) {
+    const float *W5 = Wl, *B5 = Wl + 400, *W1e = Wl + 420, *B1e = Wl + 840, *W2e = Wl + 860;
+    stage_w(Wl, W + o.E1_W5, 420);                // W5 | b5
+    stage_w(Wl + 420, W + o.E3_W1, 461);          // W1' | b1' | w2' | b2'
     for (int e = t; e < nn * H; e += NT) A[(e / H) * HP + e % H] = P[base + e];
     __syncthreads();
     for (int e = t; e < nn * H; e += NT) {
       const int n = e / H, k = e - n * H;
       float acc = 0.f;
-      for (int m = 0; m < H; ++m) acc = fmaf(A[n * HP + m], W[o.E1_W5 + m * H + k], acc);
-      acc += (2.f * Ne1) * W[o.E1_B5 + k];
+      for (int m = 0; m < H; ++m) acc = fmaf(A[n * HP + m], W5[m * H + k], acc);
+      acc += (2.f * Ne1) * B5[k];
       Bs[n * HP + k] = acc;
       Eb[base + e] = acc;
     }
     __syncthreads();
     for (int e = t; e < nn * H; e += NT) {
       const int n = e / H, k = e - n * H;
-      float acc = x[(size_t)b * Ne + t0 + n] * W[o.E3_W1 + k];
-      for (int m = 0; m < H; ++m) acc = fmaf(Bs[n * HP + m], W[o.E3_W1 + (1 + m) * H + k], acc);
-      const float v = relu(acc + W[o.E3_B1 + k]);
+      float acc = x[(size_t)b * Ne + t0 + n] * W1e[k];
+      for (int m = 0; m < H; ++m) acc = fmaf(Bs[n * HP + m], W1e[(1 + m) * H + k], acc);
+      const float v = relu(acc + B1e[k]);
       Cs[n * HP + k] = v;
       hE[base + e] = v;
     }
     __syncthreads();
     for (int n = t; n < nn; n += NT) {
-      float acc = W[o.E3_B2];
-      for (int k = 0; k < H; ++k) acc = fmaf(Cs[n * HP + k], W[o.E3_W2 + k], acc);
+      float acc = Wl[880];
+      for (int k = 0; k < H; ++k) acc = fmaf(Cs[n * HP + k], W2e[k], acc);
       ov[(size_t)b * Ne + t0 + n] = acc;
       xp[(size_t)b * Ne + t0 + n] = relu(acc);
     }
     return;
   }
+  const float *Q2 = Wl, *q2 = Wl + 400, *P1 = Wl + 420, *p1b = Wl + 860;
+  stage_w(Wl, W + o.EE_W2, 420);                  // Q2 | q2
+  stage_w(Wl + 420, W + o.EC_W1, 460);            // U1' (22 x 20) | b1'
   for (int e = t; e < nn * H; e += NT) {
     A[(e / H) * HP + e % H] = R1[base + e];
     Bs[(e / H) * HP + e % H] = C1[base + e];
@@ -448,11 +488,11 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
     const int n = e / H, k = e - n * H;
     float ar = 0.f, ac = 0.f;
     for (int m = 0; m < H; ++m) {
-      const float q = W[o.EE_W2 + m * H + k];
+      const float q = Q2[m * H + k];
       ar = fmaf(A[n * HP + m], q, ar);
       ac = fmaf(Bs[n * HP + m], q, ac);
     }
-    const float qb = Ne1 * W[o.EE_B2 + k];
+    const float qb = Ne1 * q2[k];
     Cs[n * HP + k] = ar + qb;
     Ds[n * HP + k] = ac + qb;
     Rn[base + e] = ar + qb;
@@ -463,11 +503,11 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
     const int n = e / H, k = e - n * H;
     float ar = 0.f, ac = 0.f;
     for (int m = 0; m < H; ++m) {
-      const float q = W[o.EC_W1 + (2 + m) * H + k];
+      const float q = P1[(2 + m) * H + k];
       ar = fmaf(Cs[n * HP + m], q, ar);
       ac = fmaf(Ds[n * HP + m], q, ac);
     }
-    rho[base + e] = ar + (W[o.EC_W1 + k] + W[o.EC_B1 + k]);
+    rho[base + e] = ar + (P1[k] + p1b[k]);
     gmm[base + e] = ac;
   }
 }
@@ -720,10 +760,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
   __shared__ float buf[NWP * TN * HP];
   __shared__ float res[TN * HP];
+  __shared__ float Ml[H * H];
   const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63;
   const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
+  stage_w(Ml, D + D_M, H * H);                    // visible after the first chunk barrier
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
   const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
@@ -771,7 +813,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
     const int n = e / H, k = e - n * H;
     if (t0 + n >= Nc) continue;
     float sacc = 0.f;
-    for (int l = 0; l < H; ++l) sacc = fmaf(res[n * HP + l], D[D_M + l * H + k], sacc);
+    for (int l = 0; l < H; ++l) sacc = fmaf(res[n * HP + l], Ml[l * H + k], sacc);
     gout[(t0 + n) * H + k] = res[n * HP + k];
     sout[(t0 + n) * H + k] = sacc + off[k];
   }
@@ -905,6 +947,11 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   __shared__ float buf[NWP * TN * HP];
   __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
   __shared__ float X[H * H], sumD[H], ysum[H];
+  __shared__ float Wl[3 * H * H + H];
+  const float *Ml = Wl, *V2 = Wl + H * H, *c2 = Wl + 2 * H * H, *U1e = Wl + 2 * H * H + H;
+  stage_w(Wl, D + D_M, H * H);                    // visible after the first chunk barrier
+  stage_w(Wl + H * H, W + o.H1_W2, H * H + H);    // V2 | c2
+  stage_w(Wl + 2 * H * H + H, W + o.H2_W1 + 2 * H, H * H);
   const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
   const int lane = threadIdx.x & 63;
   const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
@@ -976,7 +1023,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     const int n = e / H, l = e - n * H;
     if (t0 + n >= Nc) continue;
     float sacc = 0.f;
-    for (int k = 0; k < H; ++k) sacc = fmaf(D[D_M + l * H + k], res[n * HP + k], sacc);
+    for (int k = 0; k < H; ++k) sacc = fmaf(Ml[l * H + k], res[n * HP + k], sacc);
     gout[(t0 + n) * H + l] = sacc;
   }
   for (int e = threadIdx.x; e < H * H; e += NTP) {    // X_blk = sum_n G_n (x) D_n
@@ -1003,18 +1050,18 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += NTP) {
     if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
       const int m = e / H, k = e - m * H;
-      float a = Nc1 * W[o.H1_B2 + m] * sumD[k];
-      for (int l = 0; l < H; ++l) a = fmaf(W[o.H1_W2 + l * H + m], X[l * H + k], a);
+      float a = Nc1 * c2[m] * sumD[k];
+      for (int l = 0; l < H; ++l) a = fmaf(V2[l * H + m], X[l * H + k], a);
       put(part, s2, (2 + m) * H + k, row, a);
     } else if (e < 2 * H * H) {   // dV2[l][m] = sum_k X[l][k] U1e[m][k]
       const int f = e - H * H, l = f / H, m = f - l * H;
       float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], W[o.H2_W1 + (2 + m) * H + k], a);
+      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], U1e[m * H + k], a);
       put(part, s1, f, row, a);
     } else if (e < 2 * H * H + H) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
       const int m = e - 2 * H * H;
       float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(W[o.H2_W1 + (2 + m) * H + k], sumD[k], a);
+      for (int k = 0; k < H; ++k) a = fmaf(U1e[m * H + k], sumD[k], a);
       put(part, s1, H * H + m, row, Nc1 * a);
     } else {                      // dU1[0], dU1[1], dd1 (row pass only)
       const int f = e - 2 * H * H - H;   // 0 .. 2H-1
@@ -1167,11 +1214,15 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     float* __restrict__ rhoE, float* __restrict__ part, Segs sg) {
   __shared__ float dxq[NW * TN], xs[TN], dov[TN];
   __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
+  __shared__ float Wl[864];
+  const float *W1e = Wl, *W2e = Wl + 440, *W5 = Wl + 464;   // W1' (21 x 20) | b1' | w2' | b2' | W5
   const GenPrep PL = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
   const int lane = t & 63, w = t >> 6;
   const int I = t0 + lane;
   const uint32_t* pp = prep + (size_t)b * PL.words;
+  stage_w(Wl, W + o.E3_W1, 461);
+  stage_w(Wl + 464, W + o.E1_W5, 400);
   {
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
@@ -1203,13 +1254,13 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   __syncthreads();
   for (int e = t; e < TN * H; e += NT) {
     const int n = e / H, k = e - n * H;
-    dq[n * HP + k] = ht[n * HP + k] > 0.f ? W[o.E3_W2 + k] * dov[n] : 0.f;
+    dq[n * HP + k] = ht[n * HP + k] > 0.f ? W2e[k] * dov[n] : 0.f;
   }
   __syncthreads();
   for (int e = t; e < TN * H; e += NT) {
     const int n = e / H, m = e - n * H;
     float a = 0.f;
-    for (int k = 0; k < H; ++k) a = fmaf(dq[n * HP + k], W[o.E3_W1 + (1 + m) * H + k], a);
+    for (int k = 0; k < H; ++k) a = fmaf(dq[n * HP + k], W1e[(1 + m) * H + k], a);
     dE[n * HP + m] = a;
   }
   __syncthreads();
@@ -1217,7 +1268,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     const int n = e / H, l = e - n * H;
     if (t0 + n >= Ne) continue;
     float a = 0.f;
-    for (int m = 0; m < H; ++m) a = fmaf(dE[n * HP + m], W[o.E1_W5 + l * H + m], a);
+    for (int m = 0; m < H; ++m) a = fmaf(dE[n * HP + m], W5[l * H + m], a);
     rhoE[base + e] = a;
   }
   const int row = b * te + blockIdx.x;
@@ -1292,22 +1343,20 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
     a1 += val;
     a2 += val * (double)xsrt[m];
   }
-  c1[t] = a1;
-  c2[t] = a2;
-  __syncthreads();
-  if (t == 0) {
-    double r1 = 0.0, r2 = 0.0;
-    for (int u = 0; u < NT; ++u) {
-      const double e1 = c1[u], e2 = c2[u];
-      c1[u] = r1;
-      c2[u] = r2;
-      r1 += e1;
-      r2 += e2;
-    }
+  // exclusive scan of the per-thread chunk sums: wave shuffles, then the 4 wave totals
+  const int lane = t & 63, w = t >> 6;
+  double i1 = a1, i2 = a2;
+#pragma unroll
+  for (int o2 = 1; o2 < 64; o2 <<= 1) {
+    const double u1 = __shfl_up(i1, o2), u2 = __shfl_up(i2, o2);
+    if (lane >= o2) { i1 += u1; i2 += u2; }
   }
+  if (lane == 63) { c1[w] = i1; c2[w] = i2; }
   __syncthreads();
-  a1 = c1[t];
-  a2 = c2[t];
+  double b1 = 0.0, b2 = 0.0;
+  for (int u = 0; u < w; ++u) { b1 += c1[u]; b2 += c2[u]; }
+  a1 = b1 + (i1 - a1);
+  a2 = b2 + (i2 - a2);
   if (t == 0) {
     T[suf ? Ne : 0] = 0.0;
     T[Ne + 1 + (suf ? Ne : 0)] = 0.0;
@@ -1340,7 +1389,8 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
   const int WE = (Ne + 31) >> 5;
-  const SortTabs T = sort_tabs(prep, GP, b);
+  extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
+  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds);
   const float* xb = x + (size_t)b * Ne;
   const float xi = xb[ic];
   const float* rbb = rb + (size_t)b * Ne * H;
@@ -1583,8 +1633,12 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     float* __restrict__ psi, float* __restrict__ part, Segs sg) {
   __shared__ float A[TN * HP], Bq[TN * HP], R1t[TN * HP], C1t[TN * HP], Rt[TN * HP],
       Ct[TN * HP], dR[TN * HP], dC[TN * HP];
+  __shared__ float Wl[800];
+  const float *U1e = Wl, *Q2 = Wl + 400;          // classifier rows 2..21 | EE second layer
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
   const size_t base = ((size_t)b * Ne + t0) * H;
+  stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
+  stage_w(Wl + 400, W + o.EE_W2, 400);
   for (int e = t; e < TN * H; e += NT) {
     const int n = e / H, k = e - n * H;
     const bool in = t0 + n < Ne;
@@ -1600,7 +1654,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     const int n = e / H, m = e - n * H;
     float a = 0.f, c = 0.f;
     for (int k = 0; k < H; ++k) {
-      const float u = W[o.EC_W1 + (2 + m) * H + k];
+      const float u = U1e[m * H + k];
       a = fmaf(u, A[n * HP + k], a);
       c = fmaf(u, Bq[n * HP + k], c);
     }
@@ -1613,7 +1667,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     if (t0 + n >= Ne) continue;
     float a = 0.f, c = 0.f;
     for (int m = 0; m < H; ++m) {
-      const float q = W[o.EE_W2 + l * H + m];
+      const float q = Q2[l * H + m];
       a = fmaf(q, dR[n * HP + m], a);
       c = fmaf(q, dC[n * HP + m], c);
     }
@@ -1856,11 +1910,22 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   float* part = ws;   // segment offsets are absolute
   auto F = [&](size_t off) { return ws + off; };
 
+  const size_t tlds = sort_lds_bytes(Ne);
+  static bool attr_set = false;   // > 64 KiB of dynamic LDS for Ne > 4000
+  if (!attr_set) {
+    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<0>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    attr_set = true;
+  }
   hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D);
   WTRY(hipGetLastError());
   // ---- entity side ----
   if (ent || ee) {
-    hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
+    hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st, bt->x,
                        bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P), F(w.R1),
                        F(w.C1));
     WTRY(hipGetLastError());
@@ -1918,7 +1983,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 0,
                        F(w.rhoE), nullptr, (double*)F(w.tab));
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, prep,
+    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), tlds, st, bt->x, bt->abits, prep,
                        params, o, Ne, Nc, F(w.rhoE), F(w.rhoE), (const double*)F(w.tab), part,
                        w.segs);
     WTRY(hipGetLastError());
@@ -1935,7 +2000,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
                        nullptr, F(w.psi), (double*)F(w.tab));
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), 0, st, bt->x, bt->abits, prep,
+    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), tlds, st, bt->x, bt->abits, prep,
                        params, o, Ne, Nc, F(w.phi), F(w.psi), (const double*)F(w.tab), part,
                        w.segs);
     WTRY(hipGetLastError());

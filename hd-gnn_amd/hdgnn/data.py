@@ -42,6 +42,15 @@ def pack_bits(cls):
     return np.ascontiguousarray(by).view("<u4").reshape(B, N, W)
 
 
+def onehot_relations(cls):
+    """(B, N, N) classes -> (B, 2, N(N-1)) float32 one-hot over relations in utils2's order:
+    the C_edge / E_edge arrays the reference feeds and scores (utils2.py:86-106)."""
+    cls = np.asarray(cls)
+    I, J = pair_index(cls.shape[1])
+    c = cls[:, I, J]
+    return np.stack([(c == 0), (c == 1)], 1).astype(np.float32)
+
+
 @dataclass
 class CommitBatch:
     """Host-side compact commits.  x f32 (B,Ne); a, y u8 class grids; hid i32 (B,Ne);

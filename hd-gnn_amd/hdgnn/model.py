@@ -30,7 +30,7 @@ import time
 import numpy as np
 
 from . import layout, metrics
-from .data import compact_from_read_data
+from .data import compact_from_read_data, onehot_relations
 
 HS = 20   # De_e = De_er = h_size compiled into the engine
 
@@ -63,7 +63,7 @@ class graph2graph(object):
 
     def __init__(self, sess, Ds, Ne, Nc, Ner, Ncr, Dr, De_e, De_er, Mini_batch, checkpoint_dir,
                  epoch, Ds_inter, Dr_inter, Step, Repo, *, reader=None, device=None, seed=0,
-                 lr=3e-4, process_group=None):
+                 lr=3e-4, process_group=None, loader="utils2", data_root="."):
         self.sess = sess                       # accepted and ignored (no TF session)
         self.Ds, self.Ne, self.Nc, self.Ner, self.Ncr, self.Dr = Ds, Ne, Nc, Ner, Ncr, Dr
         self.Ds_inter, self.Dr_inter = Ds_inter, Dr_inter
@@ -73,6 +73,9 @@ class graph2graph(object):
         self.checkpoint_dir = checkpoint_dir
         self.Step, self.Repo = Step, Repo
         self.reader = reader or _default_reader
+        if loader not in ("utils2", "fast"):
+            raise ValueError("loader must be 'utils2' (the reference read_data) or 'fast'")
+        self.loader, self.data_root = loader, data_root
         self.seed, self.lr, self.pg = seed, lr, process_group
         self.device = device
         if (Ds, Dr, De_e, De_er) != (1, 2, HS, HS):
@@ -120,9 +123,17 @@ class graph2graph(object):
 
     # ------------------------------------------------------------------ data
     def _compact(self):
+        """-> (C_edge_train, C_edge_test, train, test, maps).  'utils2': the reference's
+        read_data 12-tuple through the bit-exact adapter; 'fast': hdgnn.loader reads the same
+        files straight into the compact form (no dense arrays, no progress-bar sleeps)."""
+        if self.loader == "fast":
+            from .loader import read_compact
+            train, test, maps = read_compact(self.Repo, self.Step, self.Ne, self.Nc,
+                                             self.mini_batch_num, root=self.data_root)
+            return onehot_relations(train.y), onehot_relations(test.y), train, test, maps
         tup = self.reader(self, self.Step)
         train, test, maps = compact_from_read_data(tup, self.Ne, self.Nc, self.mini_batch_num)
-        return tup, train, test, maps
+        return np.asarray(tup[4]), np.asarray(tup[5]), train, test, maps
 
     def _device_batches(self, part, maps):
         """Per reference batch j: this rank's shard of commits j*mb .. (j+1)*mb with the
@@ -155,8 +166,7 @@ class graph2graph(object):
     def train(self, args):
         import torch
         self._initialize()
-        tup, train, _, maps = self._compact()
-        C_edge_train = np.asarray(tup[4])
+        C_edge_train, _, train, _, maps = self._compact()
         batches = self._device_batches(train, maps)
         nb = len(batches)
         counter = 1
@@ -246,8 +256,7 @@ class graph2graph(object):
 
     # ------------------------------------------------------------------ test
     def test(self, args):
-        tup, _, test, maps = self._compact()
-        C_edge_test = np.asarray(tup[5])
+        _, C_edge_test, _, test, maps = self._compact()
         self._initialize()
         checkpoint_dir = os.path.join(self.checkpoint_dir, self.Repo)
         if self.load(checkpoint_dir):

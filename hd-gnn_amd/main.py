@@ -28,17 +28,20 @@ def _init_distributed():
 
 
 def _variant(argv):
-    """--model N (1..4, default 2 = the reference main.py's `from model_2 import`): which
-    model_N.graph2graph to run.  An addition; every reference flag is unchanged."""
+    """Additions to the reference's flags (every reference flag is unchanged):
+    --model N (1..4, default 2 = the reference main.py's `from model_2 import`): which
+    model_N.graph2graph to run; --loader utils2|fast: the reference's read_data (default)
+    or hdgnn.loader reading the same dataset files straight into the compact form."""
     p = argparse.ArgumentParser(add_help=False)
     p.add_argument('--model', type=int, default=2, choices=(1, 2, 3, 4))
+    p.add_argument('--loader', default='utils2', choices=('utils2', 'fast'))
     a, rest = p.parse_known_args(argv)
-    return a.model, rest
+    return a.model, a.loader, rest
 
 
 def main(argv=None):
     import importlib
-    variant, argv = _variant(sys.argv[1:] if argv is None else argv)
+    variant, loader, argv = _variant(sys.argv[1:] if argv is None else argv)
     graph2graph = importlib.import_module("hdgnn.model" + ("" if variant == 2 else "_%d" % variant)).graph2graph
     _init_distributed()
     steps = [2, 3, 5]
@@ -84,7 +87,7 @@ def main(argv=None):
                             epoch=args.epoch,
                             Ds_inter=args.Ds_inter, Dr_inter=args.Dr_inter,
                             Step=args.Step,
-                            Repo=args.Repo)
+                            Repo=args.Repo, loader=loader)
         if args.Type == 'train':
             model.train(args)
         if args.Type == 'test':

@@ -79,3 +79,34 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
                               sh.x.astype(np.float64), sh.a, sh.y, sh.hid, sh.nlen, variant=v)
         ref.append(o["probs"].detach().numpy().transpose(0, 2, 1))
     np.testing.assert_allclose(out, np.concatenate(ref), atol=1e-5)
+
+
+def test_graph2graph_fast_loader_equals_reference_loader(golden_dir, tmp_path, monkeypatch):
+    """loader='fast' (hdgnn.loader on the dataset files) trains to the same weights and
+    writes the same test outputs as the reference loader's 12-tuple."""
+    from hdgnn.model import graph2graph
+    from test_loader import _tree
+    tup, meta = _tuple(golden_dir)
+    z = np.load(os.path.join(golden_dir, "loader_tiny.npz"))
+    ne, nc, mb = meta["Ne"], meta["Nc"], 25
+    data_root = tmp_path / "data"
+    data_root.mkdir()
+    repo, step = _tree(str(data_root), z, meta)
+    outs = {}
+    for kind in ("utils2", "fast"):
+        run = tmp_path / kind
+        run.mkdir()
+        monkeypatch.chdir(run)
+        args = types.SimpleNamespace(Repo=repo, checkpoint_dir=str(run / "ckpt"))
+        kw = dict(reader=lambda model, s: tup) if kind == "utils2" else dict(
+            loader="fast", data_root=str(data_root))
+        m = graph2graph(None, Ds=1, Ne=ne, Nc=nc, Ner=ne * (ne - 1), Ncr=nc * (nc - 1), Dr=2,
+                        De_e=20, De_er=20, Mini_batch=mb, checkpoint_dir=args.checkpoint_dir,
+                        epoch=2, Ds_inter=1, Dr_inter=2, Step=step, Repo=repo, seed=3, **kw)
+        m.train(args)
+        m.test(args)
+        d = run / "outputSelf" / repo / "model_2" / str(step)
+        outs[kind] = (m.engine.get_params(), np.load(d / ("C_edge_t%d.npy" % ne)),
+                      np.load(d / ("C_edge_y%d.npy" % ne)))
+    for a, b in zip(outs["utils2"], outs["fast"]):
+        np.testing.assert_array_equal(a, b)
