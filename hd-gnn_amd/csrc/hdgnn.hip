@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M7: edge classifier + softmax CE per hunk pair (model_2.py:304-324, 115-118) ----
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
-  float ce_acc = 0.f, gsum = 0.f;
+  float ce_acc = 0.f, gsum = 0.f, corr = 0.f;
   float zacc[HS];          // sum relu(kappa_k) gamma  (dU2, model_2.py:318-321)
 #pragma unroll
   for (int k = 0; k < HS; ++k) zacc[k] = 0.f;
@@ -1226,6 +1226,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const float inv = 1.f / ssum;
       const float p0 = e0 * inv, p1 = e1 * inv;
       ce_acc += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+      corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
       if (prb) { prb[e] = p0; prb[Pc + e] = p1; }
       if (lgb) { lgb[e] = z0; lgb[Pc + e] = z1; }
       if constexpr (TRAIN) {
@@ -1247,7 +1248,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   {
     const float s0 = wave_sum(ce_acc);
-    if (lane == 0) red[wv * 32] = s0;
+    const float sc = wave_sum(corr);
+    if (lane == 0) { red[wv * 32] = s0; red[wv * 32 + 2 + HS] = sc; }
     if constexpr (TRAIN) {
       const float s1 = wave_sum(gsum);
       if (lane == 0) red[wv * 32 + 1] = s1;
@@ -1261,13 +1263,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  if (t < 2 + HS) {
+  if (t < 3 + HS) {
     float s = 0.f;
     for (int w = 0; w < NT_MID / 64; ++w) s += red[w * 32 + t];
     if (t == 0) pb[NP] = s;
+    if (t == 2 + HS) pb[NP + 1] = s;        // correct-prediction count (integer, exact)
     if constexpr (TRAIN) {
       if (t == 1) { pb[H2_B2] = -s; pb[H2_B2 + 1] = s; }
-      if (t >= 2) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
+      if (t >= 2 && t < 2 + HS) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
     }
   }
   if constexpr (!TRAIN) return;   // uniform exit: forward-only launch
@@ -1570,7 +1573,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     pb[lane < HS ? E3_W2 + lane : E3_B2] = acc;
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
-  if (t < 4) pb[NP + 1 + t] = 0.f;                  // trailer / pad
+  if (t < 3) pb[NP + 2 + t] = 0.f;                  // trailer / pad
   __syncthreads();
   MID_STAMP();
 

@@ -127,7 +127,7 @@ struct Segs {
 };
 enum : int {
   SG_CLS = 0,   // H2_W2 .. H2_B2 (42)                 kw_hunk_cls
-  SG_CE,        // CE sum slot NP                      kw_hunk_cls
+  SG_CE,        // CE sum, correct count (slots NP, NP+1) kw_hunk_cls
   SG_CLSB_H2,   // H2_W1 .. H2_B1 (460)                kw_hunk_clsb (2 passes)
   SG_CLSB_H1,   // H1_W2 .. H1_B2 (420)                kw_hunk_clsb (2 passes)
   SG_MLPB,      // H1_W1 .. H1_B1 (220)                kw_hunk_mlpb (2 passes)
@@ -834,8 +834,8 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float ss[CHM * H];
-  __shared__ float red[NWP * 22];
-  __shared__ float tot[22];
+  __shared__ float red[NWP * 23];
+  __shared__ float tot[23];
   const int b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
   const int lane = threadIdx.x & 63;
   const int q = t0 + lane;
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   const f2 bb = ld2(W + o.H2_B2);
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
-  float ce = 0.f, gs = 0.f;
+  float ce = 0.f, gs = 0.f, corr = 0.f;
   f2 za[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) za[kk] = (f2){0.f, 0.f};
@@ -893,6 +893,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
         if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
         if (lgb) { lgb[r] = z0; lgb[Pc + r] = z1; }
         ce += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+        corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
         if constexpr (TRAIN) {
           const float g = ce_scale * (p1 - yf);
           gam[((size_t)b * Nc + p) * Nc + q] = g;
@@ -905,14 +906,18 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
       }
     }
   }
-  float acc[22];
+  float acc[23];
   acc[0] = ce;
   acc[1] = gs;
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) { acc[2 + 2 * kk] = za[kk].x; acc[3 + 2 * kk] = za[kk].y; }
-  block_sum8<22>(acc, red, tot);
+  acc[22] = corr;
+  block_sum8<23>(acc, red, tot);
   const int row = b * tc + blockIdx.x;
-  if (threadIdx.x == 0) put(part, sg.s[SG_CE], 0, row, tot[0]);
+  if (threadIdx.x == 0) {
+    put(part, sg.s[SG_CE], 0, row, tot[0]);
+    put(part, sg.s[SG_CE], 1, row, tot[22]);
+  }
   if constexpr (TRAIN) {
     const int t = threadIdx.x;
     if (t < H) {
@@ -1841,7 +1846,7 @@ WideWork wide_layout(const hdg_shape* s) {
     w.segs.s[id].off = (long long)take((size_t)n * rows);
   };
   seg(SG_CLS, o.H2_W2, 42, rc);
-  seg(SG_CE, o.NP, 1, rc);
+  seg(SG_CE, o.NP, 2, rc);
   seg(SG_CLSB_H2, o.H2_W1, 460, 2 * rc);
   seg(SG_CLSB_H1, o.H1_W2, 420, 2 * rc);
   seg(SG_MLPB, o.H1_W1, 220, 2 * rc);

@@ -21,8 +21,9 @@ so normally evaluates freshly initialised weights (B.8).
 
 Data parallel: when torch.distributed is initialised with world W > 1, every batch of
 Mini_batch commits is split into W contiguous shards (Mini_batch % W == 0); the flat
-gradient is all-reduced once per step (Engine.allreduce) and the epoch accuracy is an
-all-reduced correct count.  Outputs written to disk are gathered on rank 0.
+gradient is all-reduced once per step (Engine.allreduce).  The epoch accuracy's correct
+count is computed on the device and travels in the gradient trailer, so the same
+all-reduce sums it.  Outputs written to disk are gathered on rank 0.
 """
 import os
 import time
@@ -166,7 +167,7 @@ class graph2graph(object):
     def train(self, args):
         import torch
         self._initialize()
-        C_edge_train, _, train, _, maps = self._compact()
+        _, _, train, _, maps = self._compact()
         batches = self._device_batches(train, maps)
         nb = len(batches)
         counter = 1
@@ -178,19 +179,20 @@ class graph2graph(object):
             correct = 0
             for j, db in enumerate(batches):
                 eng.train_step(db)
-                stats = eng.stats.cpu().numpy()            # pre-update, like sess.run
-                probs = eng.probs.cpu().numpy()
-                tr_loss_Hedge += float(stats[0])
-                tr_loss_map += float(stats[1])
-                self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(stats[0]),
-                                                                      float(stats[1]),
-                                                                      float(stats[2]))
-                self.C_edge_output2 = probs
-                self.C_edge_output2_logits = eng.logits.cpu().numpy()
-                lo = j * self.mini_batch_num + self.rank * self.local_batch
-                correct += metrics.top_acc_count(C_edge_train[lo:lo + self.local_batch], probs)
+                # one small copy per step: pre-update losses (like sess.run) and the
+                # on-device top_ACC numerator (gradient trailer slot P+1; already summed
+                # over ranks by the data-parallel all-reduce)
+                host = torch.cat([eng.stats, eng.grad[eng.np:eng.np + 2]]).cpu().numpy()
+                tr_loss_Hedge += float(host[0])
+                tr_loss_map += float(host[1])
+                self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[0]),
+                                                                      float(host[1]),
+                                                                      float(host[2]))
+                self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
+                self.C_edge_output2_logits = eng.logits
+                correct += int(round(float(host[5])))
             torch.cuda.synchronize(eng.device)
-            acc_top = self._allsum(correct) / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
+            acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
             theta = self.theta.reshape([2])
             resultString = "Epoch " + str(i + 1) + \
                            " acc: " + str(acc_top)[0:6] + \

@@ -94,7 +94,9 @@ const char* hdg_last_error(void);
 int         hdg_resolve_path(const hdg_shape* shape);
 int         hdg_param_count(int32_t variant);
 /* length of the gradient buffer hdg_fwd_bwd fills: param_count + 4 trailer slots
- * (slot P = CE sum over this call's relations); all-reduce the whole buffer.      */
+ * (slot P = CE sum over this call's relations, slot P+1 = number of relations whose
+ * argmax prediction equals the label, the numerator of EvaluationFuncs.top_ACC with
+ * np.argmax's tie rule, exact); all-reduce the whole buffer.                       */
 int         hdg_grad_len(int32_t variant);
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
 /* bytes of batch->prep for this shape (0 on a shape error) */

@@ -225,3 +225,19 @@ def test_workspace_garbage_does_not_leak(v, path):
         e.fwd_bwd(db)
         torch.cuda.synchronize()
         assert torch.equal(e.grad, g0) and torch.equal(e.probs, p0), "fill %g" % fill
+
+
+@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN)])
+def test_on_device_correct_count(v, path):
+    """Gradient trailer slot P+1 = EvaluationFuncs.top_ACC numerator on the returned probs
+    (np.argmax tie rule), exactly; forward-only leaves the CE slot intact."""
+    from hdgnn import metrics
+    from hdgnn.data import onehot_relations
+    B, ne, nc = 5, 70, 33
+    cb = synth_commits(B, ne, nc, 2)
+    eng = _engine(B, ne, nc, v, path)
+    eng.set_params(layout.init_flat(1, v))
+    eng.fwd_bwd(eng.upload(cb))
+    torch.cuda.synchronize()
+    want = metrics.top_acc_count(onehot_relations(cb.y), eng.probs.cpu().numpy())
+    assert eng.grad[eng.np + 1].item() == want
