@@ -234,6 +234,68 @@ __device__ __forceinline__ float bitf(const uint32_t* row, int m) {
   return ((row[m >> 5] >> (m & 31)) & 1u) ? 1.f : 0.f;
 }
 
+// ---- 8-wave pass helpers (hunk and entity-edge classifier passes) ----
+constexpr int NTP = 512;
+constexpr int NWP = NTP / 64;
+constexpr int CHM = 128;
+constexpr int H2 = H / 2;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 ld2(const float* p) { return (f2){p[0], p[1]}; }
+
+// rows [c0, c1) of a [N][H] array -> LDS (float4 copies; rows are 80 B, 16-B aligned)
+__device__ __forceinline__ void stage_rows(float* dst, const float* src, int c0, int c1) {
+  const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)c0 * H);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  for (int e = threadIdx.x; e < (c1 - c0) * (H / 4); e += blockDim.x) d4[e] = s4[e];
+}
+
+// sum the NWP waves' packed accumulators of the 64 lane-nodes -> res[64][HP]
+__device__ __forceinline__ void combine8(const f2 (&acc)[H2], float* buf, float* res) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    buf[(w * TN + lane) * HP + 2 * kk] = acc[kk].x;
+    buf[(w * TN + lane) * HP + 2 * kk + 1] = acc[kk].y;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H;
+    float s = buf[n * HP + k];
+#pragma unroll
+    for (int q = 1; q < NWP; ++q) s += buf[(q * TN + n) * HP + k];
+    res[n * HP + k] = s;
+  }
+  __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum8(float (&v)[NV], float* red, float* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const float s = wsum(v[q]);
+    if (lane == 0) red[w * NV + q] = s;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NV; q += NTP) {
+    float s = red[q];
+    for (int u = 1; u < NWP; ++u) s += red[u * NV + q];
+    out[q] = s;
+  }
+  __syncthreads();
+}
+
+// the wave's share [lo, hi) of chunk [c0, c1)
+__device__ __forceinline__ void wave_share(int c0, int c1, int& lo, int& hi) {
+  const int w = uni(threadIdx.x >> 6), len = c1 - c0;
+  lo = c0 + (len * w) / NWP;
+  hi = c0 + (len * (w + 1)) / NWP;
+}
+
+
 // ---------------------------------------------------------------------------------
 // Sorted-x entity sums.  For hidden unit k the a = 0 pre-activation of pair (i, j) is
 // affine in the scalar x_j, so {j : z_ij > 0} is a prefix or a suffix of the x-sorted
@@ -524,47 +586,53 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
 //   added to the block's LDS bins in 2^-32 fixed point (integer adds: order-free), which
 //   go out as one partial row per tile.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abits,
-                                                const int32_t* __restrict__ hidg,
-                                                const int32_t* __restrict__ nleng,
-                                                const float* __restrict__ W, Off o,
-                                                const float* __restrict__ D, int Ne, int Nc,
-                                                const float* __restrict__ rho,
-                                                const float* __restrict__ gmm,
-                                                unsigned long long* __restrict__ ncpart) {
+constexpr int EE_GAM_LDS_MAX = 800;   // Ne up to which the commit's gam table sits in LDS
+
+__global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
+                                                 const int32_t* __restrict__ hidg,
+                                                 const int32_t* __restrict__ nleng,
+                                                 const float* __restrict__ W, Off o,
+                                                 const float* __restrict__ D, int Ne, int Nc,
+                                                 const float* __restrict__ rho,
+                                                 const float* __restrict__ gmm,
+                                                 unsigned long long* __restrict__ ncpart) {
 #pragma clang fp contract(off)
-  extern __shared__ unsigned long long bins[];
+  extern __shared__ __attribute__((aligned(16))) unsigned long long bins[];   // [Nc][2] | gam
   const int b = blockIdx.y, t0 = blockIdx.x * TN;
   const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  for (int c = threadIdx.x; c < 2 * Nc; c += NT) bins[c] = 0ull;
-  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * Nc; c += NTP) bins[c] = 0ull;
   if (n < 2 || t0 >= n) {         // block-uniform: this tile holds no index row
-    for (int c = threadIdx.x; c < 2 * Nc; c += NT) outp[c] = 0ull;
+    for (int c = threadIdx.x; c < 2 * Nc; c += NTP) outp[c] = 0ull;
     return;
   }
+  const float* gb = gmm + (size_t)b * Ne * H;
+  const bool gl = Ne <= EE_GAM_LDS_MAX;
+  float* gs = reinterpret_cast<float*>(bins + ((2 * Nc + 1) & ~1));
+  if (gl) stage_rows(gs, gb, 0, Ne);
+  const float* gt = gl ? gs : gb;
+  __syncthreads();
   const int WE = (Ne + 31) >> 5;
   const int32_t* hid = hidg + (size_t)b * Ne;
   const int ip = t0 + lane;
   const bool live = ip < n;
   const int ipc = live ? ip : 0;
-  const int jlo = (n * wv) / NW, jhi = (n * (wv + 1)) / NW;
+  const int jlo = (n * wv) / NWP, jhi = (n * (wv + 1)) / NWP;
   const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
   int ei = r0 / (Ne - 1), ejj = r0 - ei * (Ne - 1);
-  float rh[H], dl[H], u0[H], u1[H];
   const float* rb = rho + (size_t)b * Ne * H;
-  const float* gb = gmm + (size_t)b * Ne * H;
+  f2 rh[H2], dl[H2], u2[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    rh[k] = rb[(ei < Ne ? ei : Ne - 1) * H + k];
-    dl[k] = D[D_EED + k];
-    u0[k] = W[o.EC_W2 + 2 * k];
-    u1[k] = W[o.EC_W2 + 2 * k + 1];
+  for (int kk = 0; kk < H2; ++kk) {
+    rh[kk] = ld2(rb + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
+    dl[kk] = ld2(D + D_EED + 2 * kk);
   }
+#pragma unroll
+  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.EC_W2 + 2 * k);
   int cur = ei;
-  const float b0 = W[o.EC_B2], b1 = W[o.EC_B2 + 1];
+  const f2 bb = ld2(W + o.EC_B2);
   float s0 = 0.f, s1 = 0.f;
   for (int jp = jlo; jp < jhi; ++jp) {
     const bool valid = live && jp != ip;
@@ -573,26 +641,25 @@ __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abi
       const int ej = ejj + (ejj >= ei ? 1 : 0);
       if (ei != cur) {
 #pragma unroll
-        for (int k = 0; k < H; ++k) rh[k] = rb[ei * H + k];
+        for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + ei * H + 2 * kk);
         cur = ei;
       }
       const float af = bitf(abits + ((size_t)b * Ne + ei) * WE, ej);
-      const float4* g4 = reinterpret_cast<const float4*>(gb + (size_t)ej * H);
-      float z0 = b0, z1 = b1;
+      const f2 a2 = {af, af};
+      const float4* g4 = reinterpret_cast<const float4*>(gt + (size_t)ej * H);
+      f2 zz = bb;
 #pragma unroll
-      for (int v = 0; v < H / 4; ++v) {
+      for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j (kw_ee_clsb forms the same sum)
         const float4 q = g4[v];
-        const float qq[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = 4 * v + u;
-          const float kk = relu(fmaf(af, dl[k], rh[k] + qq[u]));
-          z0 = fmaf(kk, u0[k], z0);
-          z1 = fmaf(kk, u1[k], z1);
-        }
+        const f2 ka = relu2(fma2(a2, dl[2 * v], rh[2 * v] + (f2){q.x, q.y}));
+        const f2 kb = relu2(fma2(a2, dl[2 * v + 1], rh[2 * v + 1] + (f2){q.z, q.w}));
+        zz = fma2((f2){ka.x, ka.x}, u2[4 * v], zz);
+        zz = fma2((f2){ka.y, ka.y}, u2[4 * v + 1], zz);
+        zz = fma2((f2){kb.x, kb.x}, u2[4 * v + 2], zz);
+        zz = fma2((f2){kb.y, kb.y}, u2[4 * v + 3], zz);
       }
-      const float mx = fmaxf(z0, z1);
-      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+      const float mx = fmaxf(zz.x, zz.y);
+      const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
       const float inv = 1.f / (e0 + e1);
       p0 = e0 * inv;
       p1 = e1 * inv;
@@ -617,7 +684,7 @@ __global__ __launch_bounds__(NT) void kw_ee_fwd(const uint32_t* __restrict__ abi
   __syncthreads();
   // per-tile partial bins, summed in tile order by kw_cross_fwd (no global atomics: the
   // L2s of the 8 XCDs are not coherent for device-scope atomics on coarse-grained memory)
-  for (int c = threadIdx.x; c < 2 * Nc; c += NT) outp[c] = bins[c];
+  for (int c = threadIdx.x; c < 2 * Nc; c += NTP) outp[c] = bins[c];
 }
 
 // ---------------------------------------------------------------------------------
@@ -683,66 +750,6 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
 // a relation: it is accumulated like any other and subtracted once with the identical
 // expression.
 // ---------------------------------------------------------------------------------
-constexpr int NTP = 512;
-constexpr int NWP = NTP / 64;
-constexpr int CHM = 128;
-constexpr int H2 = H / 2;
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 ld2(const float* p) { return (f2){p[0], p[1]}; }
-
-// rows [c0, c1) of a [N][H] array -> LDS (float4 copies; rows are 80 B, 16-B aligned)
-__device__ __forceinline__ void stage_rows(float* dst, const float* src, int c0, int c1) {
-  const float4* s4 = reinterpret_cast<const float4*>(src + (size_t)c0 * H);
-  float4* d4 = reinterpret_cast<float4*>(dst);
-  for (int e = threadIdx.x; e < (c1 - c0) * (H / 4); e += blockDim.x) d4[e] = s4[e];
-}
-
-// sum the NWP waves' packed accumulators of the 64 lane-nodes -> res[64][HP]
-__device__ __forceinline__ void combine8(const f2 (&acc)[H2], float* buf, float* res) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int kk = 0; kk < H2; ++kk) {
-    buf[(w * TN + lane) * HP + 2 * kk] = acc[kk].x;
-    buf[(w * TN + lane) * HP + 2 * kk + 1] = acc[kk].y;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < TN * H; e += NTP) {
-    const int n = e / H, k = e - n * H;
-    float s = buf[n * HP + k];
-#pragma unroll
-    for (int q = 1; q < NWP; ++q) s += buf[(q * TN + n) * HP + k];
-    res[n * HP + k] = s;
-  }
-  __syncthreads();
-}
-
-template <int NV>
-__device__ __forceinline__ void block_sum8(float (&v)[NV], float* red, float* out) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int q = 0; q < NV; ++q) {
-    const float s = wsum(v[q]);
-    if (lane == 0) red[w * NV + q] = s;
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < NV; q += NTP) {
-    float s = red[q];
-    for (int u = 1; u < NWP; ++u) s += red[u * NV + q];
-    out[q] = s;
-  }
-  __syncthreads();
-}
-
-// the wave's share [lo, hi) of chunk [c0, c1)
-__device__ __forceinline__ void wave_share(int c0, int c1, int& lo, int& hi) {
-  const int w = uni(threadIdx.x >> 6), len = c1 - c0;
-  lo = c0 + (len * w) / NWP;
-  hi = c0 + (len * (w + 1)) / NWP;
-}
-
 // ---------------------------------------------------------------------------------
 // kw_hunk_fwd  grid (tc, B, 2): z = 0 row pass (G), 1 column pass (H)
 //   mlp_hunk_B2 first layer relu sums (model_2.py:257-275):
@@ -1501,60 +1508,66 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 //   g_ijk = [kappa'_ijk > 0] (U2'[k][1] - U2'[k][0]) dz1
 //   z = 0 column pass (lane = column j): dgam_j = sum_i g, classifier partial rows
 //   z = 1 row pass    (lane = row i)   : drho_i = sum_j g
+//   8 waves; the swept side's operand rows staged in LDS, packed fp32, the class bits read
+//   from the lane's own row of a (row pass) or a^T (column pass).
 //   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_ee_clsb(
-    const uint32_t* __restrict__ abits, const int32_t* __restrict__ hidg,
-    const int32_t* __restrict__ nleng, const float* __restrict__ W, Off o,
-    const float* __restrict__ D, int Ne, int Nc, const float* __restrict__ rho,
-    const float* __restrict__ gmm, const float* __restrict__ dn, float* __restrict__ drho,
-    float* __restrict__ dgam, float* __restrict__ part, Segs sg) {
+struct EEBwdSmem {
+  float* os_;
+  float* buf;
+  float* res;
+  float* red;
+  float* tot;
+  int* hl;
+  float* dnl;
+};
+
+template <int Z>
+__device__ __forceinline__ void ee_clsb_body(
+    const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
+    const float* __restrict__ W, const Off& o, const float* __restrict__ D, int Ne, int nrel,
+    int dn1, const float* __restrict__ rho, const float* __restrict__ gmm,
+    float* __restrict__ drho, float* __restrict__ dgam, float* __restrict__ part, const Segs& sg,
+    const EEBwdSmem& sm) {
 #pragma clang fp contract(off)
-  extern __shared__ float dyn[];
-  __shared__ float buf[NW * TN * HP];
-  __shared__ float res[TN * HP];
-  __shared__ float red[NW * 41];
-  __shared__ float tot[41];
-  int* hl = reinterpret_cast<int*>(dyn);
-  float* dnl = dyn + Ne;
-  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
   const int lane = threadIdx.x & 63;
-  int n = nleng[b];
-  n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  const int nrel = n >= 2 ? n * (n - 1) : 0;
-  for (int e = threadIdx.x; e < Ne; e += NT) {
-    const int h = hidg[(size_t)b * Ne + e];
-    hl[e] = (h >= 0 && h < Nc) ? h : -1;
-  }
-  for (int e = threadIdx.x; e < 2 * Nc; e += NT) dnl[e] = dn[((size_t)b * Nc + e / 2) * 4 + 2 + (e & 1)];
-  __syncthreads();
   const int WE = (Ne + 31) >> 5;
   const int nd = t0 + lane, ncl = nd < Ne ? nd : Ne - 1;
-  const float* rbase = (z ? rho : gmm) + (size_t)b * Ne * H;   // own operand
-  const float* obase = (z ? gmm : rho) + (size_t)b * Ne * H;   // swept operand
-  float ow[H], dl[H], cE[H], u0[H], u1[H], acc[H], zk[H], ag[H];
+  const float* obase = (Z ? gmm : rho) + (size_t)b * Ne * H;   // swept operand
+  const float* own = (Z ? rho : gmm) + ((size_t)b * Ne + ncl) * H;
+  const uint32_t* brow = (Z ? abits : aT) + ((size_t)b * Ne + ncl) * WE;
+  f2 ow[H2], dl[H2], cE[H2], acc[H2], zk[H2], ag[H2], u2[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    ow[k] = rbase[(size_t)ncl * H + k];
-    dl[k] = D[D_EED + k];
-    cE[k] = D[D_EEC + k];
-    u0[k] = W[o.EC_W2 + 2 * k];
-    u1[k] = W[o.EC_W2 + 2 * k + 1];
-    acc[k] = 0.f;
-    zk[k] = 0.f;
-    ag[k] = 0.f;
+  for (int kk = 0; kk < H2; ++kk) {
+    ow[kk] = ld2(own + 2 * kk);
+    dl[kk] = ld2(D + D_EED + 2 * kk);
+    cE[kk] = ld2(D + D_EEC + 2 * kk);
+    acc[kk] = (f2){0.f, 0.f};
+    zk[kk] = acc[kk];
+    ag[kk] = acc[kk];
   }
-  const float b0 = W[o.EC_B2], b1 = W[o.EC_B2 + 1];
-  const int dn1 = n - 1 > 0 ? n - 1 : 1;
+#pragma unroll
+  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.EC_W2 + 2 * k);
+  const f2 bb = ld2(W + o.EC_B2);
   const float inv = 1.f / (float)dn1;
   float sdl = 0.f;
   // rows that hold relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
-  const int Nsw = z ? Ne : rows;             // swept index range
-  if (z == 1 && t0 >= rows) {                // whole tile of rows holds no relation
-  } else {
-    sweep(Nsw, t0, [&](int m, bool) {
-      const int i = z ? ncl : m, j = z ? m : ncl;
+  const int Nsw = (Z == 1 && t0 >= rows) ? 0 : (Z ? Ne : rows);   // block-uniform
+  for (int c0 = 0; c0 < Nsw; c0 += CHM) {
+    const int c1 = c0 + CHM < Nsw ? c0 + CHM : Nsw;
+    __syncthreads();
+    stage_rows(sm.os_, obase, c0, c1);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    int wi = -1;
+    uint32_t word = 0;
+    for (int m = lo; m < hi; ++m) {
+      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
+      const float af = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+      const int i = Z ? ncl : m, j = Z ? m : ncl;
       const int r = i * (Ne - 1) + j - (j > i ? 1 : 0);
       const bool valid = nd < Ne && i != j && r < nrel;
       float dp0 = 0.f, dp1 = 0.f;
@@ -1562,68 +1575,113 @@ __global__ __launch_bounds__(NT) void kw_ee_clsb(
         int ip, jj;
         divmod24(r, dn1, inv, ip, jj);
         const int jp = jj + (jj >= ip ? 1 : 0);
-        const int hs = hl[ip], ht = hl[jp];
-        if (hs >= 0) { dp0 += dnl[2 * hs]; dp1 += dnl[2 * hs + 1]; }
-        if (ht >= 0) { dp0 += dnl[2 * ht]; dp1 += dnl[2 * ht + 1]; }
+        const int hs = sm.hl[ip], ht = sm.hl[jp];
+        if (hs >= 0) { dp0 += sm.dnl[2 * hs]; dp1 += sm.dnl[2 * hs + 1]; }
+        if (ht >= 0) { dp0 += sm.dnl[2 * ht]; dp1 += sm.dnl[2 * ht + 1]; }
       }
-      const float af = bitf(abits + ((size_t)b * Ne + i) * WE, j);
-      const float* om = obase + (size_t)m * H;
-      float pre[H];
-      float z0 = b0, z1 = b1;
+      const f2 a2 = {af, af};
+      const float4* o4 = reinterpret_cast<const float4*>(sm.os_ + (m - c0) * H);
+      f2 pre[H2];
+      f2 zz = bb;
 #pragma unroll
-      for (int k = 0; k < H; ++k) {
-        const float rr = z ? ow[k] : om[k];   // rho_i + gam_j, same order as kw_ee_fwd
-        const float gg = z ? om[k] : ow[k];
-        pre[k] = fmaf(af, dl[k], rr + gg);
-        const float kk = relu(pre[k]);
-        z0 = fmaf(kk, u0[k], z0);
-        z1 = fmaf(kk, u1[k], z1);
+      for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j: the same sum kw_ee_fwd forms
+        const float4 q = o4[v];
+        pre[2 * v] = fma2(a2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y});
+        pre[2 * v + 1] = fma2(a2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
       }
-      const float mx = fmaxf(z0, z1);
-      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
+#pragma unroll
+      for (int kk = 0; kk < H2; ++kk) {
+        const f2 kp = relu2(pre[kk]);
+        zz = fma2((f2){kp.x, kp.x}, u2[2 * kk], zz);
+        zz = fma2((f2){kp.y, kp.y}, u2[2 * kk + 1], zz);
+      }
+      const float mx = fmaxf(zz.x, zz.y);
+      const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
       const float iv = 1.f / (e0 + e1);
       const float p0 = e0 * iv, p1 = e1 * iv;
       const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
-      sdl += d1;
+      const f2 d2 = {d1, d1};
 #pragma unroll
-      for (int k = 0; k < H; ++k) {
-        const float g = pre[k] > 0.f ? cE[k] * d1 : 0.f;
-        acc[k] += g;
-        zk[k] = fmaf(relu(pre[k]), d1, zk[k]);
-        ag[k] = fmaf(af, g, ag[k]);
+      for (int kk = 0; kk < H2; ++kk) {
+        const f2 cd = cE[kk] * d2;
+        const f2 g = {pre[kk].x > 0.f ? cd.x : 0.f, pre[kk].y > 0.f ? cd.y : 0.f};
+        acc[kk] += g;
+        if constexpr (Z == 0) {
+          zk[kk] = fma2(relu2(pre[kk]), d2, zk[kk]);
+          ag[kk] = fma2(a2, g, ag[kk]);
+        }
       }
-    });
+      if constexpr (Z == 0) sdl += d1;
+    }
   }
-  combine4(acc, buf, res);
-  float* dout = (z ? drho : dgam) + (size_t)b * Ne * H;
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
+  combine8(acc, sm.buf, sm.res);
+  float* dout = (Z ? drho : dgam) + (size_t)b * Ne * H;
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
     const int nn = e / H, k = e - nn * H;
-    if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = res[nn * HP + k];
+    if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = sm.res[nn * HP + k];
   }
-  if (z == 1) return;   // block-uniform; partial rows come from the column pass
-  float v[41];
+  if constexpr (Z == 0) {   // classifier partial rows
+    float v[41];
 #pragma unroll
-  for (int k = 0; k < H; ++k) { v[k] = zk[k]; v[H + k] = ag[k]; }
-  v[40] = sdl;
-  block_sum<41>(v, red, tot);
-  const int row = b * te + blockIdx.x;
-  const int t = threadIdx.x;
-  if (t < H) {
-    float sg_ = 0.f;   // sum of g over the tile = sum of the combined column sums
-    for (int nn = 0; nn < TN; ++nn) sg_ += (t0 + nn < Ne) ? res[nn * HP + t] : 0.f;
-    const Seg& sa = sg.s[SG_ECW1A];
-    const Seg& sb = sg.s[SG_ECB1];
-    put(part, sa, t, row, sg_ - tot[H + t]);          // P1[0] ([a = 0] input)
-    put(part, sa, H + t, row, tot[H + t]);            // P1[1] ([a = 1] input)
-    put(part, sb, t, row, sg_);                       // p1 bias
-    put(part, sb, H + 2 * t, row, -tot[t]);           // U2'[k][0]
-    put(part, sb, H + 2 * t + 1, row, tot[t]);        // U2'[k][1]
+    for (int kk = 0; kk < H2; ++kk) {
+      v[2 * kk] = zk[kk].x; v[2 * kk + 1] = zk[kk].y;
+      v[H + 2 * kk] = ag[kk].x; v[H + 2 * kk + 1] = ag[kk].y;
+    }
+    v[40] = sdl;
+    block_sum8<41>(v, sm.red, sm.tot);
+    const int row = b * te + blockIdx.x;
+    const int t = threadIdx.x;
+    if (t < H) {
+      float sg_ = 0.f;   // sum of g over the tile = sum of the combined column sums
+      for (int nn = 0; nn < TN; ++nn) sg_ += (t0 + nn < Ne) ? sm.res[nn * HP + t] : 0.f;
+      const Seg& sa = sg.s[SG_ECW1A];
+      const Seg& sb = sg.s[SG_ECB1];
+      put(part, sa, t, row, sg_ - sm.tot[H + t]);       // P1[0] ([a = 0] input)
+      put(part, sa, H + t, row, sm.tot[H + t]);         // P1[1] ([a = 1] input)
+      put(part, sb, t, row, sg_);                       // p1 bias
+      put(part, sb, H + 2 * t, row, -sm.tot[t]);        // U2'[k][0]
+      put(part, sb, H + 2 * t + 1, row, sm.tot[t]);     // U2'[k][1]
+    }
+    if (t == 0) {
+      const Seg& sb = sg.s[SG_ECB1];
+      put(part, sb, 3 * H, row, -sm.tot[40]);
+      put(part, sb, 3 * H + 1, row, sm.tot[40]);
+    }
   }
-  if (t == 0) {
-    const Seg& sb = sg.s[SG_ECB1];
-    put(part, sb, 3 * H, row, -tot[40]);
-    put(part, sb, 3 * H + 1, row, tot[40]);
+}
+
+__global__ __launch_bounds__(NTP) void kw_ee_clsb(
+    const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
+    const int32_t* __restrict__ hidg, const int32_t* __restrict__ nleng,
+    const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
+    const float* __restrict__ rho, const float* __restrict__ gmm, const float* __restrict__ dn,
+    float* __restrict__ drho, float* __restrict__ dgam, float* __restrict__ part, Segs sg) {
+  extern __shared__ float dyn[];
+  __shared__ __attribute__((aligned(16))) float os_[CHM * H];
+  __shared__ float buf[NWP * TN * HP];
+  __shared__ float res[TN * HP];
+  __shared__ float red[NWP * 41];
+  __shared__ float tot[41];
+  const int b = blockIdx.y;
+  int n = nleng[b];
+  n = n < 0 ? 0 : (n > Ne ? Ne : n);
+  const int nrel = n >= 2 ? n * (n - 1) : 0;
+  EEBwdSmem sm;
+  sm.os_ = os_; sm.buf = buf; sm.res = res; sm.red = red; sm.tot = tot;
+  sm.hl = reinterpret_cast<int*>(dyn);
+  sm.dnl = dyn + Ne;
+  for (int e = threadIdx.x; e < Ne; e += NTP) {
+    const int h = hidg[(size_t)b * Ne + e];
+    sm.hl[e] = (h >= 0 && h < Nc) ? h : -1;
   }
+  for (int e = threadIdx.x; e < 2 * Nc; e += NTP)
+    sm.dnl[e] = dn[((size_t)b * Nc + e / 2) * 4 + 2 + (e & 1)];
+  __syncthreads();
+  const int dn1 = n - 1 > 0 ? n - 1 : 1;
+  if (blockIdx.z == 0)
+    ee_clsb_body<0>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
+  else
+    ee_clsb_body<1>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1924,6 +1982,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             96 * 1024));
     attr_set = true;
   }
   hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D);
@@ -1941,7 +2001,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
   if (ee) {
-    hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NT), (size_t)Nc * 16, st, bt->abits, bt->hid,
+    const size_t elds = (size_t)((2 * Nc + 1) & ~1) * 8 +
+                        (Ne <= EE_GAM_LDS_MAX ? (size_t)Ne * H * 4 : 0);
+    hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NTP), elds, st, bt->abits, bt->hid,
                        bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), ncpart);
     WTRY(hipGetLastError());
   }
@@ -1995,9 +2057,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   if (ee) {
     const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
-    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 2), dim3(NT), lds, st, bt->abits, bt->hid, bt->nlen,
-                       params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho), F(w.dgam),
-                       part, w.segs);
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 2), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
+                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
+                       F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
                        F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
