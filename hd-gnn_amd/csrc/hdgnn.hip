@@ -84,6 +84,17 @@ __device__ __forceinline__ float wave_sum(float v) { return xrow_sum4(row16_sum(
 
 __device__ __forceinline__ float reluf(float v) { return fmaxf(v, 0.f); }
 
+typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
+
+// [z > 0] for two lanes of a packed pair in ONE VALU op: clamp(z * 2^126, 0, 1) on
+// v_pk_mul_f32 (exact for every normal z; -0, NaN -> 0).  Used as step2(z) * w, which
+// needs w finite wherever z <= 0 (padding rows / columns are kept finite).
+__device__ __forceinline__ f2 step2(f2 z) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(z), "v"((f2){0x1p126f, 0x1p126f}));
+  return r;
+}
+
 __device__ __forceinline__ uint32_t getbit(const uint32_t* rowbits, int j) {
   return (rowbits[j >> 5] >> (j & 31)) & 1u;
 }
@@ -195,7 +206,7 @@ __device__ __forceinline__ void pair_tile(
           } else {
             w = (p2){g, g};
           }
-          e = (p2){z.x > 0.f ? w.x : 0.f, z.y > 0.f ? w.y : 0.f};
+          e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
         }
         racc2[p] += e;
@@ -324,9 +335,8 @@ __device__ __forceinline__ void for_each_nbr(const uint8_t* list, const int d, c
   }
 }
 
-typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
-
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+
 
 // inclusive scan over the 64 lanes of a wave with DPP only (GFX9 row_shr + row_bcast):
 // no LDS round trips.  Lanes shifted in from outside a row read 0 (bound_ctrl).
@@ -1375,7 +1385,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     if (l < HS) {
       float* dst = which ? dH : dG;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[(row0 + 4 * (lane >> 4) + q) * HS + l] = c[q];
+      for (int q = 0; q < 4; ++q) {   // padding rows (from -inf sigma / tau) kept finite
+        const int pr = row0 + 4 * (lane >> 4) + q;
+        dst[pr * HS + l] = pr < Nc ? c[q] : 0.f;
+      }
     }
   }
   __syncthreads();
