@@ -12,7 +12,7 @@ the engine (hdgnn.engine.Engine -> C ABI -> k_commit_step on MI355X):
     sess.run([loss, loss_map, C_edge_output2]) (486)  Engine.forward(DeviceBatch)
     read_data(self, Step) -> 12 dense arrays          reader(self, Step) -> the same tuple,
                                                       then data.compact_from_read_data
-    saver.save / restore (409-432)                    .npz of the TF-named variables
+    saver.save / restore (427-451)                    TF V2 bundle, TF variable names
 
 Reference behaviours kept on purpose: every batch feeds the maps
 of the first Mini_batch commits (B.2, also in test); remainder commits are dropped
@@ -30,7 +30,7 @@ import time
 
 import numpy as np
 
-from . import layout, metrics
+from . import layout, metrics, tfckpt
 from .data import compact_from_read_data, onehot_relations
 
 HS = 20   # De_e = De_er = h_size compiled into the engine
@@ -217,43 +217,48 @@ class graph2graph(object):
         return os.path.join(checkpoint_dir, "%s/model_%d/%s" % (self.Repo, self.variant, self.Step))
 
     def save(self, checkpoint_dir, step):
-        """g2g.model-<step>.npz holding the 18 variables under their TF names, the Adam
-        slots and beta powers (enough to resume), plus a TF-style 'checkpoint' index."""
+        """saver.save(sess, <dir>/g2g.model, global_step=step) (model_2.py:427-437): a TF V2
+        bundle g2g.model-<step>.index / .data-00000-of-00001 under the TF variable names
+        (hdgnn.tfckpt), plus TF1 Adam's slots and beta powers so training can resume, and
+        the 'checkpoint' state file tf.train.get_checkpoint_state reads."""
         if self.rank != 0:
             return
         d = self._model_dir(checkpoint_dir)
         os.makedirs(d, exist_ok=True)
         eng = self.engine
         name = "g2g.model-%d" % step
-        state = dict(self.vars)
-        state["_adam_m"] = eng.m.cpu().numpy()
-        state["_adam_v"] = eng.v.cpu().numpy()
-        state["_beta_pow"] = eng.beta_pow.cpu().numpy()
-        np.savez(os.path.join(d, name + ".npz"), **state)
-        with open(os.path.join(d, "checkpoint"), "w") as f:
-            f.write('model_checkpoint_path: "%s"\n' % name)
+        tfckpt.write(os.path.join(d, name),
+                     tfckpt.state_tensors(eng.get_params(), self.variant, eng.m.cpu().numpy(),
+                                          eng.v.cpu().numpy(), eng.beta_pow.cpu().numpy()))
+        tfckpt.write_state_file(d, name)
 
     def load(self, checkpoint_dir):
+        """get_checkpoint_state + saver.restore (model_2.py:439-451).  Reads TF V2 bundles
+        (this framework's or the reference's own; the latter carry no Adam slots, so the
+        optimizer state is left as initialised) and this framework's older .npz files."""
         print(" [*] Reading checkpoint...")
         d = self._model_dir(checkpoint_dir)
-        idx = os.path.join(d, "checkpoint")
-        if not os.path.exists(idx):
+        name = tfckpt.latest(d)
+        if not name:
             return False
-        with open(idx) as f:
-            name = f.read().split('"')[1]
-        path = os.path.join(d, name + ".npz")
-        if not os.path.exists(path):
+        path = os.path.join(d, name)
+        if os.path.exists(path + ".index"):
+            flat, m, v, bp = tfckpt.engine_state(tfckpt.read(path), self.variant)
+        elif os.path.exists(path + ".npz"):
+            z = np.load(path + ".npz", allow_pickle=False)
+            flat = np.concatenate([np.asarray(z[n], np.float32).reshape(-1)
+                                   for n, _ in layout.specs(self.variant)])
+            m, v, bp = ((z["_adam_m"], z["_adam_v"], z["_beta_pow"]) if "_adam_m" in z
+                        else (None, None, None))
+        else:
             return False
         import torch
-        z = np.load(path, allow_pickle=False)
-        flat = np.concatenate([np.asarray(z[n], np.float32).reshape(-1)
-                               for n, _ in layout.specs(self.variant)])
         eng = self.engine
         eng.set_params(flat)
-        if "_adam_m" in z:
-            eng.m.copy_(torch.from_numpy(z["_adam_m"]))
-            eng.v.copy_(torch.from_numpy(z["_adam_v"]))
-            eng.beta_pow.copy_(torch.from_numpy(z["_beta_pow"]))
+        if m is not None:
+            eng.m.copy_(torch.from_numpy(np.asarray(m, np.float32)))
+            eng.v.copy_(torch.from_numpy(np.asarray(v, np.float32)))
+            eng.beta_pow.copy_(torch.from_numpy(np.asarray(bp, np.float32)))
         return True
 
     # ------------------------------------------------------------------ test

@@ -61,11 +61,23 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
     lines = res.read_text().splitlines()
     assert len(lines) == 2 and lines[0].startswith("Epoch 1 acc: ")
     ck = tmp_path / "ckpt" / "tiny" / ("model_%d" % v) / "2"
-    assert (ck / "checkpoint").exists() and (ck / "g2g.model-3.npz").exists()
-    z = np.load(ck / "g2g.model-3.npz")
+    assert (ck / "checkpoint").exists() and (ck / "g2g.model-3.index").exists()
+    assert (ck / "g2g.model-3.data-00000-of-00001").exists()
+    from hdgnn import tfckpt
+    z = tfckpt.read(str(ck / "g2g.model-3"))
     first, shape = layout.specs(v)[0]
-    np.testing.assert_array_equal(z[first].reshape(-1),
+    np.testing.assert_array_equal(z[first.split(":")[0]].reshape(-1),
                                   m.engine.get_params()[:int(np.prod(shape))])
+    # resume: a fresh model restores weights, Adam slots and beta powers bit-exactly
+    m2 = graph2graph(None, Ds=1, Ne=ne, Nc=nc, Ner=ne * (ne - 1), Ncr=nc * (nc - 1), Dr=2,
+                     De_e=20, De_er=20, Mini_batch=mb, checkpoint_dir=args.checkpoint_dir,
+                     epoch=2, Ds_inter=1, Dr_inter=2, Step=2, Repo="tiny",
+                     reader=lambda model, step: tup, seed=99)
+    m2._initialize()
+    assert m2.load(args.checkpoint_dir)
+    for a, b in ((m2.engine.params, m.engine.params), (m2.engine.m, m.engine.m),
+                 (m2.engine.v, m.engine.v), (m2.engine.beta_pow, m.engine.beta_pow)):
+        assert torch.equal(a, b)
 
     # test(): checkpoint looked up under checkpoint_dir/Repo/Repo/... (reference quirk)
     m.test(args)

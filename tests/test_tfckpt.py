@@ -1,0 +1,168 @@
+"""TF V2 checkpoint reader / writer (hdgnn.tfckpt).  CPU only.
+
+Parity against TF-written files is unpinned (no TensorFlow here and no checkpoint in the
+reference snapshot); the container format is pinned piece by piece: CRC-32C known answers
+(RFC 3720 B.4), a Snappy stream and an SSTable assembled by hand from the published
+formats, then round trips and corruption detection.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from hdgnn import layout, tfckpt
+
+
+@pytest.mark.parametrize("data,want", [
+    (b"123456789", 0xE3069283),
+    (bytes(32), 0x8A9136AA),
+    (b"\xff" * 32, 0x62A8AB43),
+    (bytes(range(32)), 0x46DD794E),
+    (bytes(range(31, -1, -1)), 0x113FDB5C),
+])
+def test_crc32c_known_answers(data, want):
+    assert tfckpt.crc32c(data) == want
+
+
+def test_mask_is_rotate_plus_delta():
+    assert tfckpt.mask_crc(0) == 0xA282EAD8
+    c = 0x12345678
+    assert tfckpt.mask_crc(c) == ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def test_snappy_hand_assembled():
+    # len 12; literal "abc" (tag (3-1)<<2); copy-1 len 9 off 3 (tag (9-4)<<2 | 1)
+    assert tfckpt.snappy_decompress(bytes([12, 0x08]) + b"abc" + bytes([0x15, 0x03])) == b"abc" * 4
+    # copy-2: len 6 off 2 over "xy" -> overlapping copy
+    assert tfckpt.snappy_decompress(bytes([8, 0x04]) + b"xy" + bytes([(6 - 1) << 2 | 2, 2, 0])) == b"xy" * 4
+    # 61-byte literal needs the 1-extra-byte length form (tag 60 << 2)
+    lit = bytes(range(61))
+    assert tfckpt.snappy_decompress(bytes([61, 60 << 2, 60]) + lit) == lit
+    with pytest.raises(tfckpt.CheckpointError):
+        tfckpt.snappy_decompress(bytes([4, 0x0d, 0x05]))     # copy before any output
+
+
+def _blk(contents, ctype=0):
+    tail = bytes([ctype])
+    return contents + tail + struct.pack("<I", tfckpt.mask_crc(tfckpt.crc32c(contents + tail)))
+
+
+def _hand_table(compress=False):
+    """Two-entry data block with prefix compression, empty meta block, one-entry index."""
+    data = (bytes([0, 1, 1]) + b"a1" +            # shared 0, key "a", value "1"
+            bytes([1, 1, 2]) + b"b22" +           # shared 1 -> key "ab", value "22"
+            struct.pack("<II", 0, 1))
+    stored = data
+    if compress:                                   # one snappy literal
+        stored = bytes([len(data), (len(data) - 1) << 2]) + data
+    out = _blk(stored, 1 if compress else 0)
+    h_data = bytes([0, len(stored)])
+    meta = struct.pack("<II", 0, 1)
+    h_meta = bytes([len(out), len(meta)])
+    out += _blk(meta)
+    index = bytes([0, 2, 2]) + b"ab" + h_data + struct.pack("<II", 0, 1)
+    h_index = bytes([len(out), len(index)])
+    out += _blk(index)
+    foot = h_meta + h_index
+    return out + foot + bytes(40 - len(foot)) + struct.pack("<Q", 0xdb4775248b80fb57)
+
+
+@pytest.mark.parametrize("compress", [False, True])
+def test_read_hand_assembled_table(compress):
+    assert tfckpt.read_table(_hand_table(compress)) == [(b"a", b"1"), (b"ab", b"22")]
+
+
+def test_table_writer_matches_hand_layout():
+    assert tfckpt.write_table([(b"a", b"1"), (b"ab", b"22")]) == _hand_table()
+
+
+def test_table_detects_corruption():
+    t = bytearray(_hand_table())
+    t[4] ^= 0x01
+    with pytest.raises(tfckpt.CheckpointError, match="checksum"):
+        tfckpt.read_table(bytes(t))
+    t = bytearray(_hand_table())
+    t[-1] ^= 0xFF
+    with pytest.raises(tfckpt.CheckpointError, match="magic"):
+        tfckpt.read_table(bytes(t))
+
+
+def test_large_table_many_blocks_roundtrip():
+    rng = np.random.default_rng(0)
+    keys = sorted({("scope_%03d/var_%d" % (rng.integers(1000), i)).encode() for i in range(700)})
+    ents = [(k, rng.bytes(int(rng.integers(0, 40)))) for k in keys]
+    img = tfckpt.write_table(ents, block_size=512)
+    assert tfckpt.read_table(img) == ents
+
+
+def test_entry_proto_fields():
+    msg = tfckpt.encode_entry(1, (22, 20), 0, 1760, 1760, 0xDEADBEEF)
+    # dtype=1 varint, shape dims {size=22}{size=20}, offset, size, fixed32 crc
+    assert msg[:2] == bytes([0x08, 0x01])
+    assert msg[2:12] == bytes([0x12, 0x08, 0x12, 0x02, 0x08, 22, 0x12, 0x02, 0x08, 20])
+    e = tfckpt.decode_entry(msg)
+    assert (e["dtype"], e["shape"], e["offset"], e["size"], e["crc32c"]) == (1, [22, 20], 1760, 1760, 0xDEADBEEF)
+    h = tfckpt.decode_header(tfckpt.encode_header(1))
+    assert (h["num_shards"], h["endianness"], h["producer"]) == (1, 0, 1)
+
+
+def test_bundle_roundtrip_and_tamper(tmp_path):
+    rng = np.random.default_rng(1)
+    t = {"phi_E_O1/r1_w1o": rng.standard_normal((4, 20)).astype(np.float32),
+         "map_conv/map_theta1": rng.standard_normal((1, 2, 1, 1)).astype(np.float32),
+         "beta1_power": np.float32(0.729).reshape(()),
+         "global_step": np.int64(7).reshape(()),
+         "d": rng.standard_normal(5)}
+    pre = str(tmp_path / "g2g.model-3")
+    tfckpt.write(pre, t)
+    r = tfckpt.read(pre)
+    assert set(r) == set(t)
+    for k in t:
+        assert r[k].dtype == np.asarray(t[k]).dtype and r[k].shape == np.asarray(t[k]).shape
+        np.testing.assert_array_equal(r[k], t[k])
+    with open(pre + ".data-00000-of-00001", "r+b") as f:
+        f.seek(3)
+        b = f.read(1)
+        f.seek(3)
+        f.write(bytes([b[0] ^ 0x40]))
+    with pytest.raises(tfckpt.CheckpointError, match="checksum"):
+        tfckpt.read(pre)
+
+
+@pytest.mark.parametrize("v", [1, 2, 3, 4])
+def test_engine_state_tf_names(v, tmp_path):
+    rng = np.random.default_rng(v)
+    n = layout.n_params(v)
+    flat, m, vv = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+    bp = np.array([0.9 ** 4, 0.999 ** 4], np.float32)
+    pre = str(tmp_path / "g2g.model-1")
+    tfckpt.write(pre, tfckpt.state_tensors(flat, v, m, vv, bp))
+    tens = tfckpt.read(pre)
+    names = [s.split(":")[0] for s, _ in layout.specs(v)]
+    assert set(tens) == set(names) | {x + "/Adam" for x in names} | \
+        {x + "/Adam_1" for x in names} | {"beta1_power", "beta2_power"}
+    f2, m2, v2, bp2 = tfckpt.engine_state(tens, v)
+    for a, b in ((f2, flat), (m2, m), (v2, vv), (bp2, bp)):
+        np.testing.assert_array_equal(a, b)
+    # a reference-style checkpoint (Saver built before the optimizer): weights only
+    ref = {k: tens[k] for k in names}
+    f3, m3, _, _ = tfckpt.engine_state(ref, v)
+    np.testing.assert_array_equal(f3, flat)
+    assert m3 is None
+    ref.pop(names[0])
+    with pytest.raises(tfckpt.CheckpointError, match="lacks"):
+        tfckpt.engine_state(ref, v)
+    bad = dict(tens)
+    bad[names[-1]] = np.zeros((2, 1, 1, 1), np.float32)
+    with pytest.raises(tfckpt.CheckpointError, match="shape"):
+        tfckpt.engine_state(bad, v)
+
+
+def test_checkpoint_state_file(tmp_path):
+    tfckpt.write_state_file(str(tmp_path), "g2g.model-12")
+    assert tfckpt.latest(str(tmp_path)) == "g2g.model-12"
+    (tmp_path / "checkpoint").write_text(
+        'model_checkpoint_path: "./checkpoint40/glide/glide/model_2/2/g2g.model-5"\n'
+        'all_model_checkpoint_paths: "./checkpoint40/glide/glide/model_2/2/g2g.model-5"\n')
+    assert tfckpt.latest(str(tmp_path)) == "g2g.model-5"
+    assert tfckpt.latest(str(tmp_path / "nope")) is None
