@@ -636,6 +636,45 @@ __device__ __forceinline__ f4v mfma_tile16(FA fa, FB fb, const int K, const int 
   return c0 + c1;
 }
 
+// The same tile with strided operands: lane l supplies row r = l & 15 of A as
+// pa[k * sa] and column r of B as pb[k * sb], k < K.  A row / column outside the matrix
+// passes a pointer to a 0.f word with stride 0 (a row of ones: a 1.f word, stride 0), so
+// the K loop carries no bounds logic: one LDS read and one address add per operand.
+__device__ __forceinline__ f4v mfma_tile16_p(const float* pa, const int sa, const float* pb,
+                                             const int sb, const int K, const int lane) {
+  const int q = lane >> 4;
+  const float* a = pa + q * sa;
+  const float* b = pb + q * sb;
+  const int sa4 = 4 * sa, sb4 = 4 * sb;
+  f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  int k = 0;
+  for (; k + 16 <= K; k += 16) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      av[u] = a[u * sa4];
+      bv[u] = b[u * sb4];
+    }
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c1, 0, 0, 0);
+    a += 4 * sa4;
+    b += 4 * sb4;
+  }
+  for (; k + 4 <= K; k += 4) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c0, 0, 0, 0);
+    a += sa4;
+    b += sb4;
+  }
+  if (k < K) {                       // K % 4 tail: entries k + q >= K are selected to zero
+    const bool ok = k + q < K;       // (callers' arrays are padded, the read stays in LDS)
+    const float av = ok ? a[0] : 0.f, bv = ok ? b[0] : 0.f;
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, c0, 0, 0, 0);
+  }
+  return c0 + c1;
+}
+
 // first layer of mlp_entity_B1 for hidden unit kk (model_2.py:165-170):
 //   W1^T [x_i, x_j, [a=0], [a=1]] + b1 = u_i + v_j + a_ij d,
 //   u = fma(x, W1[0], W1[2] + b1), v = x * W1[1], d = W1[3] - W1[2]
@@ -887,6 +926,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* s0v = ysumv + HS;          // sigma offset
   float* t0v = s0v + HS;            // tau offset
   float* sumD = t0v + HS;
+  float* kzero = sumD + HS;         // 0.f, 1.f: stride-0 operand rows of mfma_tile16_p
+  const float* kone = kzero + 1;
   float* Mm = lds + L.Mm;
   float* Xm = lds + L.Xm;
   float* red = lds + L.red;
@@ -942,6 +983,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if (lfit)
     for (int w = t; w < lwords; w += NT_MID) U[NE4 * HS + w] = __builtin_bit_cast(float, pp[PL.lists + w]);
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
+  if (t == 0) { kzero[0] = 0.f; kzero[1] = 1.f; }
   __syncthreads();
   if (aux && b == 0 && t == 0) {           // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
     float s2 = 0.f;
@@ -979,15 +1021,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   const int ntm_e = (Ne + 15) >> 4;
   for (int rb = wv; rb < ntm_e; rb += NT_MID / 64) {          // wave-uniform
     const int row0 = rb * 16;
+    const int ir = row0 + (lane & 15);                         // this lane's A row
+    const bool rv = ir < Ne;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int col0 = cb * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? Ps[i * HS + k] : 0.f; },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k < HS && m < HS) ? Ws[E1_W5 + k * HS + m] : 0.f;
-          }, HS, lane);
+      const int mc = col0 + (lane & 15);                       // this lane's B column
+      const f4v c = mfma_tile16_p(rv ? Ps + ir * HS : kzero, rv ? 1 : 0,
+                                  mc < HS ? Ws + E1_W5 + mc : kzero, mc < HS ? HS : 0, HS, lane);
       const int m = col0 + (lane & 15);
       if (m < HS) {
         const float bias = twoNe1 * Ws[E1_B5 + m];
@@ -1003,24 +1044,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {   // same wave: its E_bar rows are complete (LDS in order)
-      const int col0 = cb * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) {
-            const int i = row0 + r;
-            return (i < Ne && k <= HS) ? (k == 0 ? xs[i] : Eb[i * HS + k - 1]) : 0.f;
-          },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k <= HS && m < HS) ? Ws[E3_W1 + k * HS + m] : 0.f;
-          }, HS + 1, lane);
+      const int col0 = cb * 16;        // [x, E_bar] W1' = E_bar W1'[1:] (MFMA) + x W1'[0]
+      const int mc = col0 + (lane & 15);
+      const f4v c = mfma_tile16_p(rv ? Eb + ir * HS : kzero, rv ? 1 : 0,
+                                  mc < HS ? Ws + E3_W1 + HS + mc : kzero, mc < HS ? HS : 0, HS, lane);
       const int m = col0 + (lane & 15);
       if (m < HS) {
-        const float bias = Ws[E3_B1 + m];
+        const float bias = Ws[E3_B1 + m], w0 = Ws[E3_W1 + m];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = row0 + 4 * (lane >> 4) + q;
           if (i < Ne) {
-            const float v = reluf(c[q] + bias);
+            const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
             hE[i * HS + m] = v;
             hEG[i * HS + m] = v;
           }
@@ -1155,10 +1190,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {
     const int which = tile & 1, row0 = ((tile >> 2)) * 16, col0 = ((tile >> 1) & 1) * 16;
     const float* src = which ? Hh : G;
-    const f4v c = mfma_tile16(
-        [&](int r, int k) { const int p = row0 + r; return (p < Nc && k < HS) ? src[p * HS + k] : 0.f; },
-        [&](int k, int j) { const int m = col0 + j; return (k < HS && m < HS) ? Mm[k * HS + m] : 0.f; },
-        HS, lane);
+    const int pr = row0 + (lane & 15), mc = col0 + (lane & 15);
+    const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
+                                mc < HS ? Mm + mc : kzero, mc < HS ? HS : 0, HS, lane);
     const int m = col0 + (lane & 15);
     if (m < HS) {
       const float off = which ? t0v[m] : s0v[m], ek = eps[m];
@@ -1377,10 +1411,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {   // dG = Dsig M^T, dH = Dtau M^T
     const int which = tile & 1, row0 = (tile >> 2) * 16, col0 = ((tile >> 1) & 1) * 16;
     const float* src = which ? Dtau : Dsig;
-    const f4v c = mfma_tile16(
-        [&](int r, int k) { const int p = row0 + r; return (p < Nc && k < HS) ? src[p * HS + k] : 0.f; },
-        [&](int k, int j) { const int l = col0 + j; return (k < HS && l < HS) ? Mm[l * HS + k] : 0.f; },
-        HS, lane);
+    const int pr = row0 + (lane & 15), lc = col0 + (lane & 15);
+    const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
+                                lc < HS ? Mm + lc * HS : kzero, lc < HS ? 1 : 0, HS, lane);
     const int l = col0 + (lane & 15);
     if (l < HS) {
       float* dst = which ? dH : dG;
@@ -1409,12 +1442,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if (wv < 4) {         // dV1 rows 0..7 and dc1: [n^T; 1] . Dalpha, n^T . Dbeta  (MFMA)
     const int side = wv >> 1, col0 = (wv & 1) * 16;
     const float* D = side ? Dbe : Dal;
-    const f4v c = mfma_tile16(
-        [&](int r, int p) {
-          return (p < Nc) ? (r < 4 ? nb[4 * p + r] : ((r == 4 && side == 0) ? 1.f : 0.f)) : 0.f;
-        },
-        [&](int p, int j) { const int m = col0 + j; return (p < Nc && m < HS) ? D[p * HS + m] : 0.f; },
-        Nc, lane);
+    const int r = lane & 15, mc = col0 + (lane & 15);
+    const float* pa = r < 4 ? nb + r : ((r == 4 && side == 0) ? kone : kzero);
+    const f4v c = mfma_tile16_p(pa, r < 4 ? 4 : 0, mc < HS ? D + mc : kzero, mc < HS ? HS : 0, Nc,
+                                lane);
     const int m = col0 + (lane & 15);
     if (m < HS) {
       if (lane < 16) {
@@ -1502,15 +1533,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       }
       dw2p[rb * 21 + lane] = acc;
     }
+    const int ir = row0 + (lane & 15);
+    const bool rv = ir < Ne;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int col0 = cb * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k < HS && m < HS) ? Ws[E3_W1 + (1 + m) * HS + k] : 0.f;
-          }, HS, lane);
+      const int mc = col0 + (lane & 15);
+      const f4v c = mfma_tile16_p(rv ? dq + ir * HS : kzero, rv ? 1 : 0,
+                                  mc < HS ? Ws + E3_W1 + (1 + mc) * HS : kzero, mc < HS ? 1 : 0,
+                                  HS, lane);
       const int m = col0 + (lane & 15);
       if (m < HS) {
 #pragma unroll
@@ -1523,12 +1554,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int col0 = cb * 16;
-      const f4v c = mfma_tile16(
-          [&](int r, int k) { const int i = row0 + r; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
-          [&](int k, int j) {
-            const int m = col0 + j;
-            return (k < HS && m < HS) ? Ws[E1_W5 + m * HS + k] : 0.f;
-          }, HS, lane);
+      const int mc = col0 + (lane & 15);
+      const f4v c = mfma_tile16_p(rv ? dE + ir * HS : kzero, rv ? 1 : 0,
+                                  mc < HS ? Ws + E1_W5 + mc * HS : kzero, mc < HS ? 1 : 0, HS, lane);
       const int m = col0 + (lane & 15);
       if (m < HS) {
 #pragma unroll
@@ -1545,14 +1573,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8)
   if (wv < 4) {
     const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
-    const f4v c = mfma_tile16(
-        [&](int r, int i) {
-          const int l = row0 + r;
-          if (i >= Ne) return 0.f;
-          return l == 0 ? xs[i] : (l <= HS ? Eb[i * HS + l - 1] : (l == HS + 1 ? 1.f : 0.f));
-        },
-        [&](int i, int j) { const int k = col0 + j; return (i < Ne && k < HS) ? dq[i * HS + k] : 0.f; },
-        Ne, lane);
+    const int lr = row0 + (lane & 15), kc = col0 + (lane & 15);
+    const float* pa = lr == 0 ? xs : (lr <= HS ? Eb + lr - 1 : (lr == HS + 1 ? kone : kzero));
+    const int sa = lr == 0 ? 1 : (lr <= HS ? HS : 0);
+    const f4v c = mfma_tile16_p(pa, sa, kc < HS ? dq + kc : kzero, kc < HS ? HS : 0, Ne, lane);
     const int k = col0 + (lane & 15);
     if (k < HS) {
 #pragma unroll
@@ -1564,13 +1588,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
   } else if (wv < 8) {
     const int row0 = ((wv - 4) >> 1) * 16, col0 = ((wv - 4) & 1) * 16;
-    const f4v c = mfma_tile16(
-        [&](int r, int i) {
-          const int l = row0 + r;
-          return i < Ne ? (l < HS ? Ps[i * HS + l] : (l == HS ? 1.f : 0.f)) : 0.f;
-        },
-        [&](int i, int j) { const int k = col0 + j; return (i < Ne && k < HS) ? dE[i * HS + k] : 0.f; },
-        Ne, lane);
+    const int lr = row0 + (lane & 15), kc = col0 + (lane & 15);
+    const f4v c = mfma_tile16_p(lr < HS ? Ps + lr : (lr == HS ? kone : kzero), lr < HS ? HS : 0,
+                                kc < HS ? dE + kc : kzero, kc < HS ? HS : 0, Ne, lane);
     const int k = col0 + (lane & 15);
     if (k < HS) {
 #pragma unroll
@@ -1716,6 +1736,10 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
   using namespace m2;
   __shared__ float sh[RED_PH][64];
   const int p = blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool upd = (threadIdx.x >> 6) == 0 && p < NP;
+  // the update's operands are fetched before the reduction so both latencies overlap
+  const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
+  const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
   const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh);
   if ((threadIdx.x >> 6) != 0) return;
   if (p < GRAD_LEN) grad[p] = g;
@@ -1728,14 +1752,12 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
       stats[3] = 10.f * ce + 0.1f * aux[1] + aux[0];
     }
   }
-  if (p < NP) {
+  if (upd) {
     const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
-    const float lr_t = lr * aux[4];
-    const float w = params[p];
     float gg = g + 0.001f * w;
-    if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / aux[2];
-    if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / aux[3];
-    float m = mm[p], v = vv[p];
+    if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / n1;
+    if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / n2;
+    float m = m0, v = v0;
     m += (gg - m) * (1.f - b1);
     v += (gg * gg - v) * (1.f - b2);
     mm[p] = m;
