@@ -312,27 +312,43 @@ __device__ __forceinline__ T wave_incl_scan(T v, int lane) {
 // its x once; the group reads (j, x_j) back with ds_bpermute (LDS pipe, not VALU), four
 // neighbours per trip so their bpermutes are in flight together.  All lanes of a group
 // share the trip count, so bpermute sources are active.  list may point to LDS or HBM.
+// (ds_bpermute byte addresses are formed once per trip; the 4 reads use the immediate
+// offset field, so a neighbour costs no address arithmetic.)
 template <int GL, bool NEED_J, class F>
 __device__ __forceinline__ void for_each_nbr(const uint8_t* list, const int d, const int gbase,
                                              const int r, const float* xs, F f) {
   for (int c0 = 0; c0 < d; c0 += GL) {
     const int jl = (c0 + r < d) ? (int)list[c0 + r] : 0;
-    const float xl = xs[jl];
+    const int xl = __builtin_bit_cast(int, xs[jl]);
     const int nn = (d - c0 < GL) ? d - c0 : GL;
     int n = 0;
     for (; n + 4 <= nn; n += 4) {
+      const int a0 = (gbase + n) << 2;
       float x[4];
       int j[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        x[q] = __shfl(xl, gbase + n + q);
-        j[q] = NEED_J ? __shfl(jl, gbase + n + q) : 0;
+        x[q] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(a0 + 4 * q, xl));
+        j[q] = NEED_J ? __builtin_amdgcn_ds_bpermute(a0 + 4 * q, jl) : 0;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) f(j[q], x[q]);
     }
-    for (; n < nn; ++n) f(NEED_J ? __shfl(jl, gbase + n) : 0, __shfl(xl, gbase + n));
+    for (; n < nn; ++n) {
+      const int a0 = (gbase + n) << 2;
+      f(NEED_J ? __builtin_amdgcn_ds_bpermute(a0, jl) : 0,
+        __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(a0, xl)));
+    }
   }
+}
+
+// clamp(x * a + b, 0, 1) on both halves of a packed pair, x broadcast: ONE v_pk_fma_f32
+__device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) {
+  f2 xx;
+  xx.x = x;
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(r) : "v"(xx), "v"(a), "v"(b));
+  return r;
 }
 
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
@@ -548,6 +564,9 @@ __global__ __launch_bounds__(1024) void k_prep_maps(const uint32_t* __restrict__
 constexpr int NG_MID = NT_MID / 256;            // 4 pair-tile groups, one k-chunk each
 // hunk node buffers [NC16][HS]: alpha beta G H sigma tau (+ tau+eps when it fits)
 __host__ __device__ constexpr int nbuf_h(int smaxc) { return smaxc <= 8 ? 7 : 6; }
+// the classifier's dL/dz1 matrix gamma [NC16][NC16] lives in LDS (after the pair-tile
+// scratch) when Nc <= 80; larger hunk graphs keep it in the workspace
+__host__ __device__ constexpr bool gam_lds(int smaxc) { return smaxc <= 5; }
 constexpr int NSL = NT_MID / HS;                // 51 node slices for (k, slice) matvecs
 
 struct StepLayout {   // offsets in 4-byte words into the dynamic LDS arena
@@ -583,7 +602,8 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.Xm = o;   o += HS * HS;           // sum_p G_p (x) Dsig_p + H_p (x) Dtau_p
   L.red = o;  o += (NT_MID / 64) * 32;
   int u = 3 * NE4 * HS;                                            // P | E_bar | h
-  const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred;        // hunk phases
+  const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred +      // hunk phases
+                 (gam_lds(smaxc) ? NC16 * NC16 : 0);
   int ueb = 5 * NE4 * HS;                         // E3 bwd: P | E_bar | dq | dE | h/rho
   const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2 + rho
   if (ue2 > ueb) ueb = ue2;
@@ -731,8 +751,8 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
         const float xr = xu[mr < nd ? mr : nd - 1], xc = xu[mc < nd ? mc : nd - 1];
         const bool fr = (u[h] + xr * w1[h]) > 0.f;
         const bool fc = (fmaf(xc, w0[h], c0[h]) + v[h]) > 0.f;
-        br[h] = ((mr < nd) && (fr != ra[h])) ? br[h] + s : br[h];
-        bc[h] = ((mc < nd) && (fc != ca[h])) ? bc[h] + s : bc[h];
+        br[h] = ((mr < nd) & (fr != ra[h])) ? br[h] + s : br[h];   // '&': no branch around
+        bc[h] = ((mc < nd) & (fc != ca[h])) ? bc[h] + s : bc[h];   // the clamped loads
       }
     }
     double tot[2] = {0.0, 0.0};
@@ -749,28 +769,31 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
         tot[h] = acc;
       }
     }
-    // a = 1 corrections relu(z0 + d) - relu(z0) = med3(s z0 + t, 0, d) with (s, t) =
-    // (1, d) for d >= 0 and (-1, 0) for d < 0: one packed fma + two v_med3 per
-    // neighbour and hidden-unit pair (value within an ulp of the two-relu form)
+    // a = 1 corrections relu(z0 + d) - relu(z0) = d clamp((s z0 + t) / d, 0, 1) with
+    // (s, t) = (1, d) for d >= 0 and (-1, 0) for d < 0: z0 is affine in x_j, so the
+    // clamp argument is x_j A + B and a neighbour costs ONE clamped packed fma (+ the
+    // accumulate); d multiplies the sum once.  |d| < 2^-100 counts as d = 0 (the
+    // correction is then below the sum's rounding).
     f2 sp = {0.f, 0.f};
     const f2 sg = {dd.x >= 0.f ? 1.f : -1.f, dd.y >= 0.f ? 1.f : -1.f};
     const f2 tg = {dd.x >= 0.f ? dd.x : 0.f, dd.y >= 0.f ? dd.y : 0.f};
+    const f2 rd = {fabsf(dd.x) >= 0x1p-100f ? 1.f / dd.x : 0.f,
+                   fabsf(dd.y) >= 0x1p-100f ? 1.f / dd.y : 0.f};
     {
-      const f2 bw = sg * w1, aa = __builtin_elementwise_fma(sg, u, tg);
+      const f2 ca = sg * w1 * rd, cb = __builtin_elementwise_fma(sg, u, tg) * rd;
       const int d = ((ABL & 4) || !live) ? 0 : offr[ic + 1] - offr[ic];
       for_each_nbr<EG_L, false>(lr + offr[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
-        const f2 zz = __builtin_elementwise_fma((f2){xj, xj}, bw, aa);
-        sp += (f2){__builtin_amdgcn_fmed3f(zz.x, 0.f, dd.x), __builtin_amdgcn_fmed3f(zz.y, 0.f, dd.y)};
+        sp += clamp_fma2(xj, ca, cb);
       });
     }
     {
-      const f2 bw = sg * w0, aa = __builtin_elementwise_fma(sg, c0 + v, tg);
+      const f2 ca = sg * w0 * rd, cb = __builtin_elementwise_fma(sg, c0 + v, tg) * rd;
       const int d = ((ABL & 8) || !live) ? 0 : offc[ic + 1] - offc[ic];
       for_each_nbr<EG_L, false>(lc + offc[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
-        const f2 zz = __builtin_elementwise_fma((f2){xj, xj}, bw, aa);
-        sp += (f2){__builtin_amdgcn_fmed3f(zz.x, 0.f, dd.x), __builtin_amdgcn_fmed3f(zz.y, 0.f, dd.y)};
+        sp += clamp_fma2(xj, ca, cb);
       });
     }
+    sp *= dd;
     if (live && kp < EG_L) {
       const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
       *reinterpret_cast<float2*>(Ps + i * HS + k0) = P;
@@ -830,9 +853,9 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       const f2 rj = *reinterpret_cast<const f2*>(rho + j * HS + k0);
       const f2 z0 = u + xj * w1;
       const f2 z1 = z0 + dd;
-      const f2 gs = ri + rj;
-      const f2 m1g = {z1.x > 0.f ? gs.x : 0.f, z1.y > 0.f ? gs.y : 0.f};
-      const f2 m0g = {z0.x > 0.f ? gs.x : 0.f, z0.y > 0.f ? gs.y : 0.f};
+      const f2 gs = ri + rj;                 // finite: step2(z) * gs == [z > 0] gs
+      const f2 m1g = step2(z1) * gs;
+      const f2 m0g = step2(z0) * gs;
       const f2 dm = m1g - m0g;
       sd += dm;
       sx = __builtin_elementwise_fma((f2){xj, xj}, dm, sx);
@@ -939,7 +962,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* EbG = EG + Ne * HS;
   float* hEG = EbG + Ne * HS;
   float* pb = part + (size_t)b * NPART;
-  float* gam = gamg + (size_t)b * NC16 * NC16;
+  constexpr bool GAML = gam_lds(SMAXC);
+  float* gamG = gamg + (size_t)b * NC16 * NC16;
   uint16_t* rq = rowq + (size_t)b * Ne * HS;
   const float Nc1 = (float)(Nc - 1);
   const float twoNe1 = 2.f * (float)(Ne - 1);
@@ -1145,6 +1169,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
   for (int q = 0; q < NBUF_H; ++q) Bf[q] = U + q * NC16 * HS;
   float* credg = U + NBUF_H * NC16 * HS + g * CRED;
+  float* gam = GAML ? U + NBUF_H * NC16 * HS + NG_MID * CRED : gamG;   // compile-time choice
   float* alpha = Bf[0];
   float* beta = Bf[1];
   if (msl < NSL) {

@@ -55,6 +55,8 @@ class Engine:
                                  self.beta_pow.data_ptr())
         self._out = _lib.Outputs(self.probs.data_ptr(), self.logits.data_ptr(),
                                  self.stats.data_ptr())
+        # a training sess.run fetches C_edge_output2 (the probabilities), not the logits
+        self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr())
 
     # ---- parameters ---------------------------------------------------------
     def set_params(self, flat):
@@ -82,10 +84,15 @@ class Engine:
             raise ValueError("batch prepared for path %d, engine runs path %d (use "
                              "Engine.upload)" % (dbatch.path, self.path))
 
-    def fwd_bwd(self, dbatch, outputs=True):
+    def _outputs(self, outputs, logits):
+        if not outputs:
+            return None
+        return self._out if logits else self._out_train
+
+    def fwd_bwd(self, dbatch, outputs=True, logits=True):
         self._check(dbatch)
         b = dbatch.struct()
-        out = self._out if outputs else None
+        out = self._outputs(outputs, logits)
         _lib.check(self.lib.hdg_fwd_bwd(ctypes.byref(self.shape), ctypes.byref(b),
                                         ctypes.c_void_p(self.params.data_ptr()),
                                         ctypes.c_void_p(self.grad.data_ptr()),
@@ -108,19 +115,20 @@ class Engine:
                                        and torch.distributed.is_initialized()
                                        and torch.distributed.get_world_size() > 1)
 
-    def train_step(self, dbatch, outputs=True):
+    def train_step(self, dbatch, outputs=True, logits=False):
         """sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer]) equivalent:
-        outputs land in self.probs / self.stats (pre-update), params updated in place.
+        outputs land in self.probs / self.stats (pre-update), params updated in place;
+        self.logits only with logits=True (the reference's training run does not fetch them).
         Single process: hdg_train_step (step kernel + fused reduce/Adam).  Data parallel:
         hdg_fwd_bwd -> all-reduce of the flat gradient -> hdg_adam_tf."""
         if self._distributed():
-            self.fwd_bwd(dbatch, outputs)
+            self.fwd_bwd(dbatch, outputs, logits)
             self.allreduce()
             self.adam()
             return
         self._check(dbatch)
         b = dbatch.struct()
-        out = self._out if outputs else None
+        out = self._outputs(outputs, logits)
         _lib.check(self.lib.hdg_train_step(ctypes.byref(self.shape), ctypes.byref(b),
                                            ctypes.byref(self._state), ctypes.c_float(self.lr),
                                            ctypes.byref(out) if out is not None else None,
@@ -129,18 +137,18 @@ class Engine:
                                            self._stream()))
 
     # ---- HIP graph of one training step ----------------------------------------
-    def capture(self, dbatch, outputs=True):
+    def capture(self, dbatch, outputs=True, logits=False):
         """Capture train_step(dbatch) (fwd_bwd [+ RCCL all-reduce] + Adam) into a HIP graph;
         replay() then runs one step with a single launch.  dbatch must stay alive."""
         saved = [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
-        self.train_step(dbatch, outputs)          # warm: attributes set, RCCL comm built
+        self.train_step(dbatch, outputs, logits)  # warm: attributes set, RCCL comm built
         for t, v in zip((self.params, self.m, self.v, self.beta_pow), saved):
             t.copy_(v)                            # the warm-up step leaves no trace
         torch.cuda.synchronize(self.device)
         self._graph_batch = dbatch
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.train_step(dbatch, outputs)
+            self.train_step(dbatch, outputs, logits)
         torch.cuda.synchronize(self.device)
         self._graph = g
         return g

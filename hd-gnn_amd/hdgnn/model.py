@@ -189,7 +189,7 @@ class graph2graph(object):
                                                                       float(host[1]),
                                                                       float(host[2]))
                 self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
-                self.C_edge_output2_logits = eng.logits
+                self.C_edge_output2_logits = None          # not fetched in training
                 correct += int(round(float(host[5])))
             torch.cuda.synchronize(eng.device)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0

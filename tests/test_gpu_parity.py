@@ -191,7 +191,7 @@ def test_full_size_properties():
     eng = _engine(B, ne, nc)
     flat = layout.init_flat(0)
     eng.set_params(flat)
-    eng.train_step(cb.to_device())
+    eng.train_step(cb.to_device(), logits=True)
     torch.cuda.synchronize()
     probs = eng.probs.cpu().numpy()
     logits = eng.logits.cpu().numpy().astype(np.float64)
