@@ -82,6 +82,74 @@ __device__ __forceinline__ float xrow_sum4(float v) {
 
 __device__ __forceinline__ float wave_sum(float v) { return xrow_sum4(row16_sum(v)); }
 
+// x <-> y exchange of DPP rows: swap32 trades x's lanes 32-63 for y's lanes 0-31, swap16
+// x's rows 1, 3 for y's rows 0, 2 (v_permlane{32,16}_swap, same hazard handling as above)
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+// Transposed cross-row reduction of N per-lane values: value n summed over the 4 DPP rows
+// (lane columns kept apart) with one swap + one add per PAIR of values at each of the two
+// levels, instead of two swaps + two adds per value.  Afterwards vector i (i < H2) holds
+// value i in row 0, i + H2 in row 1, i + H in row 2 and i + H + H2 in row 3, H = ceil(N/2),
+// H2 = ceil(H/2); store(n, row_value) is called by every lane for the valid n of its row.
+template <int N, class F>
+__device__ __forceinline__ void xrow_sums(const float (&v)[N], const int lane, F store) {
+  constexpr int H = (N + 1) / 2, H2 = (H + 1) / 2;
+  float a[H], b[H2];
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    float x = v[i], y = (i + H < N) ? v[i + H] : 0.f;
+    swap32(x, y);
+    a[i] = x + y;              // rows 0,1: value i; rows 2,3: value i + H
+  }
+#pragma unroll
+  for (int i = 0; i < H2; ++i) {
+    float x = a[i], y = (i + H2 < H) ? a[i + H2] : 0.f;
+    swap16(x, y);
+    b[i] = x + y;
+  }
+  const int r = lane >> 4;
+  const int off = ((r & 1) ? H2 : 0) + ((r & 2) ? H : 0);
+#pragma unroll
+  for (int i = 0; i < H2; ++i) {
+    const bool ok = ((r & 1) ? (i + H2 < H) : true) && (i + off < N);
+    if (ok) store(i + off, b[i]);
+  }
+}
+
+// Full 64-lane sums of N values: xrow_sums, then one 16-lane DPP reduction per vector;
+// store(n, total) runs on lane 0 of the row that holds n.
+template <int N, class F>
+__device__ __forceinline__ void wave_sums(const float (&v)[N], const int lane, F store) {
+  constexpr int H = (N + 1) / 2, H2 = (H + 1) / 2;
+  float a[H], b[H2];
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    float x = v[i], y = (i + H < N) ? v[i + H] : 0.f;
+    swap32(x, y);
+    a[i] = x + y;
+  }
+#pragma unroll
+  for (int i = 0; i < H2; ++i) {
+    float x = a[i], y = (i + H2 < H) ? a[i + H2] : 0.f;
+    swap16(x, y);
+    b[i] = row16_sum(x + y);
+  }
+  if ((lane & 15) == 0) {
+    const int r = lane >> 4;
+    const int off = ((r & 1) ? H2 : 0) + ((r & 2) ? H : 0);
+#pragma unroll
+    for (int i = 0; i < H2; ++i) {
+      const bool ok = ((r & 1) ? (i + H2 < H) : true) && (i + off < N);
+      if (ok) store(i + off, b[i]);
+    }
+  }
+}
+
 __device__ __forceinline__ float reluf(float v) { return fmaxf(v, 0.f); }
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
@@ -261,26 +329,20 @@ __device__ __forceinline__ void pair_tile(
   if constexpr (KT) yacc[KK - 1] = yacct;
   // close the column partials: 4 ti per wave by shuffles, then 4 waves via LDS
   float* credy = cred + 4 * NP16 * KK;
-#pragma unroll
-  for (int c = 0; c < SMAX; ++c)
-#pragma unroll
-    for (int k = 0; k < KK; ++k) cacc[c][k] = xrow_sum4(cacc[c][k]);
-  if constexpr (MODE != 0) {
-#pragma unroll
-    for (int k = 0; k < KK; ++k) yacc[k] = wave_sum(yacc[k]);
-  }
-  if (lane < 16) {           // one predicated block of stores
-    float* cw = cred + (wv * NP16 + tj) * KK;
+  {                          // column partials summed over the wave's 4 rows (transposed)
+    float cf[SMAX * KK];
 #pragma unroll
     for (int c = 0; c < SMAX; ++c)
 #pragma unroll
-      for (int k = 0; k < KK; ++k) cw[16 * c * KK + k] = cacc[c][k];
-    if constexpr (MODE != 0) {
-      if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < KK; ++k) credy[wv * KK + k] = yacc[k];
-      }
-    }
+      for (int k = 0; k < KK; ++k) cf[c * KK + k] = cacc[c][k];
+    float* cw = cred + (wv * NP16 + tj) * KK;
+    xrow_sums(cf, lane, [&](int n, float x) {
+      const int c = n / KK, k = n - c * KK;
+      cw[16 * c * KK + k] = x;
+    });
+  }
+  if constexpr (MODE != 0) {
+    wave_sums(yacc, lane, [&](int k, float x) { credy[wv * KK + k] = x; });
   }
   __syncthreads();
   for (int e = t; e < NP16 * KK; e += 256) {
@@ -1315,20 +1377,19 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       }
     }
   }
-  {
+  if constexpr (TRAIN) {   // red[wv][0] CE, [1] sum gamma, [2 + k] dU2 terms, [2 + HS] count
+    float v[3 + HS];
+    v[0] = ce_acc;
+    v[1] = gsum;
+#pragma unroll
+    for (int k = 0; k < HS; ++k) v[2 + k] = zacc[k];
+    v[2 + HS] = corr;
+    float* rw = red + wv * 32;
+    wave_sums(v, lane, [&](int n, float x) { rw[n] = x; });
+  } else {
     const float s0 = wave_sum(ce_acc);
     const float sc = wave_sum(corr);
     if (lane == 0) { red[wv * 32] = s0; red[wv * 32 + 2 + HS] = sc; }
-    if constexpr (TRAIN) {
-      const float s1 = wave_sum(gsum);
-      if (lane == 0) red[wv * 32 + 1] = s1;
-#pragma unroll
-      for (int k = 0; k < HS; ++k) zacc[k] = wave_sum(zacc[k]);
-      if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < HS; ++k) red[wv * 32 + 2 + k] = zacc[k];
-      }
-    }
   }
   __syncthreads();
   MID_STAMP();
