@@ -67,6 +67,26 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// row16_sum of N values as fused v_add_f32_dpp (one VALU op per value and step; the
+// compiler otherwise splits some into v_mov_dpp + v_add).  Steps run over all N values
+// in turn, so each DPP read is >= N-1 >= 2 instructions after the write it depends on;
+// one s_nop covers the producers before the first step.
+#define HDG_DPP_ADD(v, ctl) asm volatile("v_add_f32_dpp %0, %0, %0 " ctl : "+v"(v))
+template <int N>
+__device__ __forceinline__ void row16_sums(float (&v)[N]) {
+  static_assert(N >= 3, "row16_sums needs >= 3 independent values (DPP hazard spacing)");
+  asm volatile("s_nop 1" ::);
+#pragma unroll
+  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "row_mirror row_mask:0xf bank_mask:0xf");
+#pragma unroll
+  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "row_half_mirror row_mask:0xf bank_mask:0xf");
+#pragma unroll
+  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf");
+#pragma unroll
+  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf");
+}
+#undef HDG_DPP_ADD
+
 // Sum over the 4 DPP rows of a wave for every lane column: lane l gets
 // v[l] + v[l^16] + v[l^32] + v[l^48].  v_permlane{32,16}_swap in the VALU (no LDS);
 // inline asm because the ROCm 7.2 builtins mis-assign the two results, with the two
@@ -301,11 +321,7 @@ __device__ __forceinline__ void pair_tile(
       rs[2 * p + 1] = racc2[p].y;
     }
     if constexpr (KT) rs[KK - 1] = racct;
-#pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      asm volatile("" : "+v"(rs[k]));
-      if constexpr (!(ABL & 2)) rs[k] = row16_sum(rs[k]);
-    }
+    if constexpr (!(ABL & 2)) row16_sums(rs);
     if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
 #pragma unroll
       for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = rs[k];
