@@ -27,6 +27,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hdgnn.h"
@@ -208,6 +209,8 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 //   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e                 (pair weights)
 //   Rout[i] = sum_j e_ij   Cout[j] = sum_i e_ij   (diagonal INCLUDED for MODE 0/1:
 //   callers subtract it; MODE 2 masks it)
+// Rows swept: i = rmul * r + radd, r = 0, 1, ... while i < N (a block pair splits the rows
+// by parity: rmul = 2, radd = half); Cout then holds the partial column sums of those rows.
 // A, B, wr, wc, Rout, Cout: LDS [node][LD] (rows/cols >= N padded with -inf in A/B).
 // Rout may alias A and Cout may alias B (rows are consumed before they are written,
 // columns are written after the closing barrier).  cred: 4*16*SMAX*KK + 8*KK words.
@@ -222,13 +225,14 @@ __device__ __forceinline__ void pair_tile(
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
-    float* __restrict__ ysum, float* __restrict__ cred) {
+    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0) {
   typedef float p2 __attribute__((ext_vector_type(2)));
   constexpr int NP16 = 16 * SMAX;
   constexpr int NW = (SMAX + 1) / 2;
   constexpr int KP = KK / 2, KT = KK & 1;      // packed fp32 pairs (v_pk_*) + odd tail
   const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
-  const int S = (N + 15) >> 4;
+  const int nown = (N - radd + rmul - 1) / rmul;   // rows i = rmul r + radd < N
+  const int S = (nown + 15) >> 4;
   const p2 z2 = {0.f, 0.f};
 
   p2 cacc2[SMAX][KP > 0 ? KP : 1];
@@ -248,21 +252,31 @@ __device__ __forceinline__ void pair_tile(
   }
 
   for (int s = 0; s < S; ++s) {
-    const int i = ti + 16 * s;
-    const bool iv = i < N;
+    const int r = ti + 16 * s;
+    const int i = rmul * r + radd;
+    const bool iv = r < nown;
     p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
-    const float* Ai = A + i * LD + k0;
+    // rows past the sweep read row 0 and are selected to A = -inf, w = 0 (e = 0): the
+    // sweep may run past the padded buffer when the rows are split by parity
+    const int ib = iv ? i : 0;
+    const float* Ai = A + ib * LD + k0;
+    const float ninf = -INFINITY;
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      a2[p] = (p2){Ai[2 * p], Ai[2 * p + 1]};
-      rw2[p] = (MODE == 1) ? (p2){wr[i * LD + k0 + 2 * p], wr[i * LD + k0 + 2 * p + 1]} : z2;
+      const p2 av = {Ai[2 * p], Ai[2 * p + 1]};
+      a2[p] = iv ? av : (p2){ninf, ninf};
+      if constexpr (MODE == 1) {
+        const p2 wv2 = {wr[ib * LD + k0 + 2 * p], wr[ib * LD + k0 + 2 * p + 1]};
+        rw2[p] = iv ? wv2 : z2;
+      } else {
+        rw2[p] = z2;
+      }
       racc2[p] = z2;
     }
-    const float at = KT ? Ai[KK - 1] : 0.f;
-    const float rwt = (MODE == 1 && KT) ? wr[i * LD + k0 + KK - 1] : 0.f;
+    const float at = KT ? (iv ? Ai[KK - 1] : ninf) : 0.f;
+    const float rwt = (MODE == 1 && KT) ? (iv ? wr[ib * LD + k0 + KK - 1] : 0.f) : 0.f;
     float racct = 0.f;
     uint32_t wrow[NW];
-    const int ib = iv ? i : 0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {      // branch-free: clamped load, masked value
       const uint32_t w = bits[ib * W + (q < W ? q : 0)];
@@ -889,16 +903,16 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
                                            const int nd, const uint16_t* __restrict__ rq,
                                            const float* rho, const float* Tr, const float* Tx,
                                            const int TL, const int* offr, const uint8_t* lr,
-                                           const int Ne, float* red2) {
+                                           const int n0, const int n1, float* red2) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
   const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
   const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f};
   f2 S0 = {0.f, 0.f}, S1 = S0, S2 = S0, S3 = S0;
-  for (int base = EG_N * wv; base < Ne; base += EG_N * (NT_MID / 64)) {     // wave-uniform
+  for (int base = n0 + EG_N * wv; base < n1; base += EG_N * (NT_MID / 64)) {   // wave-uniform
     const int i = base + sub;
-    const bool live = sub < EG_N && i < Ne;
+    const bool live = sub < EG_N && i < n1;
     const int ic = live ? i : 0;
     const float xi = xs[ic];
     const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
@@ -964,7 +978,61 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
   }
 }
 
-template <int SMAXC, bool TRAIN, bool STAMPS = false>
+// ------------------------------------------------------------------------------
+// Block-pair exchange (split mode: the two blocks of a commit split the hunk rows).
+// pair_send + pair_recv_add: v[0..n) (LDS) += the partner block's v[0..n); both blocks
+// end with the same bits (fp32 addition commutes).  Values travel as (value, tag) 8-byte
+// pairs, two per 16-byte write-through store (global_store_dwordx4 sc0 sc1: system scope,
+// to memory) into the partner's inbox: no L2 writeback fence (the 8 XCD L2s are not
+// coherent; an agent-scope release writes back the whole dirty L2, 5-11 us,
+// tools/probe/xchg2.hip).  The receiver polls its own inbox with L2-bypassing loads
+// (sc0 sc1) until both tags match (1.6 us per 1480-value exchange measured, hidden behind
+// independent work between send and receive), then clears the words (tag 0) for the next
+// launch, so a slot's tag is constant.  The pair is co-resident by construction (host:
+// 2 B blocks <= CUs, one block per CU); a partner that never arrives ends the wait after
+// ~20 ms and poisons the CE slot with NaN (loud, no hang).  v must not change between
+// send and receive; n is even.
+// ------------------------------------------------------------------------------
+constexpr uint32_t XTAG = 0xC0DE0000u;          // + slot + 1; no NaN/Inf/huge fill pattern
+constexpr int XSLOTS = 3;                       // H partial, D_tau partial, dn partial
+constexpr unsigned long long XWAIT = 2000000ull;   // s_memrealtime ticks (100 MHz) = 20 ms
+typedef uint32_t xu4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void xstore(xu4* p, const xu4 w) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ xu4 xload(const xu4* p) {
+  xu4 w;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(w) : "v"(p) : "memory");
+  return w;
+}
+
+__device__ __forceinline__ void pair_send(const float* v, const int n, xu4* __restrict__ out,
+                                          const uint32_t tag, const int t) {
+  for (int e = t; 2 * e < n; e += NT_MID)
+    xstore(out + e, (xu4){__float_as_uint(v[2 * e]), tag, __float_as_uint(v[2 * e + 1]), tag});
+}
+
+__device__ __forceinline__ bool pair_recv_add(float* v, const int n, xu4* __restrict__ in,
+                                              const uint32_t tag, const int t) {
+  bool late = false;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int e = t; 2 * e < n; e += NT_MID) {
+    xu4 w = xload(in + e);
+    while (w.y != tag || w.w != tag) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT) { late = true; break; }
+      w = xload(in + e);
+    }
+    v[2 * e] += __uint_as_float(w.x);
+    v[2 * e + 1] += __uint_as_float(w.z);
+    xstore(in + e, (xu4){0u, 0u, 0u, 0u});
+  }
+  __syncthreads();
+  return late;
+}
+
+template <int SMAXC, bool TRAIN, bool STAMPS = false, bool SPLIT = false>
 __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float* __restrict__ x, const uint32_t* __restrict__ abits,
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ prep,
@@ -972,14 +1040,31 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     float* __restrict__ gamg, float* __restrict__ part, float* __restrict__ probs,
     float* __restrict__ logits, int Ne, int Nc, float ce_scale,
     unsigned long long* __restrict__ stamps, float* __restrict__ aux,
-    const float* __restrict__ bpow) {
+    const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch) {
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const StepLayout L = step_layout(Ne, Nc, SMAXC);
   const PrepLayout PL = prep_layout(Ne, Nc);
-  const int b = blockIdx.x;
+  // split mode: commit b runs on blocks 2b + h, h = 0, 1; block h owns the hunk rows
+  // p = 2r + h and the entity nodes of its half for E2
+  int b, h;
+  if constexpr (SPLIT) {
+    b = blockIdx.x >> 1;
+    h = blockIdx.x & 1;
+  } else {
+    b = blockIdx.x;
+    h = 0;
+  }
+  if (b >= B) return;                                // (uniform; the grid is exact)
+  const int rmul = SPLIT ? 2 : 1, radd = h;          // own hunk rows p = rmul r + radd
+  const int prow = SPLIT ? 2 * b + h : b;            // this block's partial-gradient row
+  const bool redund = SPLIT && h == 1;               // redundant phases: h = 0 writes grads
+  bool xlate = false;
+  constexpr int XS = 16 * SMAXC * HS / 2;            // 16-byte words per inbox slot
+  xu4* xin = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + h) * XSLOTS * XS : nullptr;
+  xu4* xout = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + 1 - h) * XSLOTS * XS : nullptr;
   // Thread ids are re-derived from an opaque copy of threadIdx.x at every phase
   // boundary (PHASE()), so the compiler cannot keep addresses derived from them live
   // across phases: this kernel runs at the 128-VGPR ceiling of 1024-thread blocks.
@@ -993,7 +1078,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #define MID_STAMP()                                                                     \
   do {                                                                                  \
     if constexpr (STAMPS) {                                                             \
-      if (threadIdx.x == 0) stamps[blockIdx.x * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
+      if (threadIdx.x == 0) stamps[prow * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
       ++nstamp;                                                                         \
     }                                                                                   \
     asm volatile("" : "+v"(t));                                                         \
@@ -1039,7 +1124,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* EG = Esave + (size_t)b * 3 * Ne * HS;     // P | E_bar | h
   float* EbG = EG + Ne * HS;
   float* hEG = EbG + Ne * HS;
-  float* pb = part + (size_t)b * NPART;
+  float* pb = part + (size_t)prow * NPART;
   constexpr bool GAML = gam_lds(SMAXC);
   float* gamG = gamg + (size_t)b * NC16 * NC16;
   uint16_t* rq = rowq + (size_t)b * Ne * HS;
@@ -1064,7 +1149,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     Ws[i] = w;
     l2 = fmaf(w, w, l2);
   }
-  if (aux && b == 0) {                     // pre-update loss_para / loss_map / Adam factor
+  if (aux && b == 0 && h == 0) {           // pre-update loss_para / loss_map / Adam factor
     l2 = wave_sum(l2);
     if (lane == 0) red[wv * 32] = l2;
   }
@@ -1087,7 +1172,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   if (t == 0) { kzero[0] = 0.f; kzero[1] = 1.f; }
   __syncthreads();
-  if (aux && b == 0 && t == 0) {           // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
+  if (aux && b == 0 && h == 0 && t == 0) {   // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
     float s2 = 0.f;
     for (int w = 0; w < NT_MID / 64; ++w) s2 += red[w * 32];
     const float n1 = sqrtf(Ws[TH1] * Ws[TH1] + Ws[TH1 + 1] * Ws[TH1 + 1]);
@@ -1276,13 +1361,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* G = Bf[2];
   float* Hh = Bf[3];
   pair_tile<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
-                                  nullptr, 0, G, Hh, nullptr, credg);
+                                  nullptr, 0, G, Hh, nullptr, credg, rmul, radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
+    if (SPLIT && ((e / HS) & 1) != h) continue;       // the diagonal of the own rows
     const float dg = reluf(alpha[e] + beta[e]);
     G[e] -= dg;
     Hh[e] -= dg;
   }
   __syncthreads();
+  if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, XTAG + 1, t);   // received in M6
   MID_STAMP();
 
   // ---- M6: classifier first layer on eff = S_p + T_q, S = G V2 + (Nc-1) c2:
@@ -1290,27 +1377,37 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* sig = Bf[4];
   float* tau = Bf[5];
   float* tauE = TAUE ? Bf[6] : nullptr;     // tau + eps: the y = 1 column operand of pass A
-  for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {
-    const int which = tile & 1, row0 = ((tile >> 2)) * 16, col0 = ((tile >> 1) & 1) * 16;
-    const float* src = which ? Hh : G;
-    const int pr = row0 + (lane & 15), mc = col0 + (lane & 15);
-    const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
-                                mc < HS ? Mm + mc : kzero, mc < HS ? HS : 0, HS, lane);
-    const int m = col0 + (lane & 15);
-    if (m < HS) {
-      const float off = which ? t0v[m] : s0v[m], ek = eps[m];
-      float* dst = which ? tau : sig;
+  // sigma tiles first, tau tiles after the H exchange (split mode: the sigma tiles
+  // overlap the exchange latency)
+  auto m6_tiles = [&](const int which) {
+    for (int tile = wv; tile < 2 * SMAXC; tile += NT_MID / 64) {     // wave-uniform
+      const int row0 = (tile >> 1) * 16, col0 = (tile & 1) * 16;
+      const float* src = which ? Hh : G;
+      const int pr = row0 + (lane & 15), mc = col0 + (lane & 15);
+      const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
+                                  mc < HS ? Mm + mc : kzero, mc < HS ? HS : 0, HS, lane);
+      const int m = col0 + (lane & 15);
+      if (m < HS) {
+        const float off = which ? t0v[m] : s0v[m], ek = eps[m];
+        float* dst = which ? tau : sig;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = row0 + 4 * (lane >> 4) + q;
-        const float v = p < Nc ? c[q] + off : -INFINITY;
-        dst[p * HS + m] = v;
-        if constexpr (TAUE) {
-          if (which) tauE[p * HS + m] = v + ek;
+        for (int q = 0; q < 4; ++q) {
+          const int p = row0 + 4 * (lane >> 4) + q;
+          const float v = p < Nc ? c[q] + off : -INFINITY;
+          dst[p * HS + m] = v;
+          if constexpr (TAUE) {
+            if (which) tauE[p * HS + m] = v + ek;
+          }
         }
       }
     }
+  };
+  m6_tiles(0);
+  if constexpr (SPLIT) {
+    if constexpr (STAMPS) MID_STAMP();
+    xlate |= pair_recv_add(Hh, Nc * HS, xin, XTAG + 1, t);
   }
+  m6_tiles(1);
   __syncthreads();
   MID_STAMP();
 
@@ -1327,9 +1424,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     // U2 rows (w0_k, w1_k) read as broadcast LDS float4 pairs: keeps 40 VGPRs free
     const float4* u2 = reinterpret_cast<const float4*>(lds + L.u2);
     const float b0 = Ws[H2_B2], b1 = Ws[H2_B2 + 1];
-    for (int e = t; e < Pc; e += NT_MID) {
-      int p, qq;
-      divmod_bf(e, Nc1i, invNc1, p, qq);
+    const int Pown = ((Nc - radd + rmul - 1) / rmul) * Nc1i;    // pairs of the own rows
+    for (int el = t; el < Pown; el += NT_MID) {
+      int r, qq;
+      divmod_bf(el, Nc1i, invNc1, r, qq);
+      const int p = rmul * r + radd;
+      const int e = SPLIT ? p * Nc1i + qq : el;
       const int q = qq + (qq >= p ? 1 : 0);
       const float yf = (float)((yb[__mul24(p, WC) + (q >> 5)] >> (q & 31)) & 1u);
       const float4* sp = reinterpret_cast<const float4*>(sig + p * HS);
@@ -1426,43 +1526,52 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Dsig = sig;
   float* Dtau = tau;
   pair_tile<KK_MID, SMAXC, 2, HS>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr,
-                                  gam, NC16, Dsig, Dtau, ysumv, credg);
+                                  gam, NC16, Dsig, Dtau, ysumv, credg, rmul, radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const int k = e % HS;
     Dsig[e] *= cvec[k];
     Dtau[e] *= cvec[k];
   }
   __syncthreads();
+  if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, XTAG + 2, t);   // received in M9
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
   //   one MFMA GEMM [G^T; 1; 0 | H^T; 0; 1] (22 x 2Nc) . [Dsig; Dtau] (2Nc x 20): rows
-  //   20, 21 are sum_p Dsig, sum_p Dtau.  4 tiles x 4 K-quarters, partials in the pair-
-  //   tile scratch (dead after pass B), then one fixed-order sum.
+  //   20, 21 are sum_p Dsig, sum_p Dtau.  4 tiles x 4 K-quarters (two per half: waves 0-7
+  //   take the G / Dsig half, waves 8-15 the H / Dtau half, after the D_tau exchange in
+  //   split mode), partials in the pair-tile scratch (dead after pass B), then one
+  //   fixed-order sum.  Split mode sums over the block's own rows p only.
   {
     float* xpart = U + NBUF_H * NC16 * HS;            // [4 kq][4 tiles][256]
-    const int Nc4 = (Nc + 3) & ~3, K2 = 2 * Nc4;
-    const int kq = wv >> 2, tl = wv & 3;
+    const int Nc4 = (Nc + 3) & ~3;
+    const int kq = wv >> 2, tl = wv & 3, half = kq >> 1;
     const int row0 = (tl >> 1) * 16, col0 = (tl & 1) * 16;
-    const int kl = ((K2 / 4 + 3) & ~3) * kq;
-    const int kh = (kl + ((K2 / 4 + 3) & ~3) < K2) ? kl + ((K2 / 4 + 3) & ~3) : K2;
-    const f4v c = mfma_tile16(
-        [&](int r, int k) {
-          const int kk = kl + k, l = row0 + r;
-          const bool hi = kk >= Nc4;
-          const int p = hi ? kk - Nc4 : kk;
-          if (kk >= kh || p >= Nc) return 0.f;
-          if (l < HS) return (hi ? Hh : G)[p * HS + l];
-          return (l == HS + (hi ? 1 : 0)) ? 1.f : 0.f;
-        },
-        [&](int k, int j) {
-          const int kk = kl + k, m = col0 + j;
-          const bool hi = kk >= Nc4;
-          const int p = hi ? kk - Nc4 : kk;
-          return (kk < kh && p < Nc && m < HS) ? (hi ? Dtau : Dsig)[p * HS + m] : 0.f;
-        }, kh > kl ? kh - kl : 0, lane);
+    const int mq = ((Nc4 / 2) + 3) & ~3;
+    const int kl = (kq & 1) * mq;
+    const int kh = (kl + mq < Nc4) ? kl + mq : Nc4;
+    auto xtile = [&]() {
+      const f4v c = mfma_tile16(
+          [&](int r, int k) {
+            const int p = kl + k, l = row0 + r;
+            if (p >= Nc || (SPLIT && (p & 1) != h)) return 0.f;     // own rows
+            if (l < HS) return (half ? Hh : G)[p * HS + l];
+            return (l == HS + half) ? 1.f : 0.f;
+          },
+          [&](int k, int j) {
+            const int p = kl + k, m = col0 + j;
+            return (p < Nc && m < HS && (!SPLIT || (p & 1) == h)) ? (half ? Dtau : Dsig)[p * HS + m]
+                                                                  : 0.f;
+          }, kh > kl ? kh - kl : 0, lane);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      xpart[(kq * 4 + tl) * 256 + (4 * (lane >> 4) + q) * 16 + (lane & 15)] = c[q];
+      for (int q = 0; q < 4; ++q)
+        xpart[(kq * 4 + tl) * 256 + (4 * (lane >> 4) + q) * 16 + (lane & 15)] = c[q];
+    };
+    if (half == 0) xtile();
+    if constexpr (SPLIT) {
+      if constexpr (STAMPS) MID_STAMP();
+      xlate |= pair_recv_add(Dtau, Nc * HS, xin + XS, XTAG + 2, t);
+    }
+    if (half == 1) xtile();
     __syncthreads();
     {
       const int tl2 = t >> 8, e = t & 255;
@@ -1533,14 +1642,31 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Dal = Bf[4];   // Dsig/Dtau dead after dG/dH
   float* Dbe = Bf[5];
   pair_tile<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
-                                  Dal, Dbe, ysumv, credg);
+                                  Dal, Dbe, ysumv, credg, rmul, radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
+    if (SPLIT && ((e / HS) & 1) != h) {             // partner's rows: no D_alpha here
+      Dal[e] = 0.f;
+      continue;
+    }
     const float dz = (alpha[e] + beta[e] > 0.f) ? (dG[e] + dH[e]) : 0.f;
     Dal[e] -= dz;
     Dbe[e] -= dz;
   }
   __syncthreads();
   MID_STAMP();
+  for (int e = t; e < NC16 * 2; e += NT_MID) {      // dn_c[m], m in {0,1} (x' components)
+    const int c = e >> 1, m = e & 1;
+    float acc = 0.f;
+    if (c < Nc) {
+#pragma unroll
+      for (int k = 0; k < HS; ++k)
+        acc = fmaf(Ws[H1_W1 + m * HS + k], Dal[c * HS + k],
+                   fmaf(Ws[H1_W1 + (4 + m) * HS + k], Dbe[c * HS + k], acc));
+    }
+    dnb[e] = acc;
+  }
+  __syncthreads();
+  if constexpr (SPLIT) pair_send(dnb, 2 * Nc, xout + 2 * XS, XTAG + 3, t);   // dV1 overlaps
   if (wv < 4) {         // dV1 rows 0..7 and dc1: [n^T; 1] . Dalpha, n^T . Dbeta  (MFMA)
     const int side = wv >> 1, col0 = (wv & 1) * 16;
     const float* D = side ? Dbe : Dal;
@@ -1561,18 +1687,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       }
     }
   }
-  for (int e = t; e < NC16 * 2; e += NT_MID) {      // dn_c[m], m in {0,1} (x' components)
-    const int c = e >> 1, m = e & 1;
-    float acc = 0.f;
-    if (c < Nc) {
-#pragma unroll
-      for (int k = 0; k < HS; ++k)
-        acc = fmaf(Ws[H1_W1 + m * HS + k], Dal[c * HS + k],
-                   fmaf(Ws[H1_W1 + (4 + m) * HS + k], Dbe[c * HS + k], acc));
-    }
-    dnb[e] = acc;
+  if constexpr (SPLIT) {
+    if constexpr (STAMPS) MID_STAMP();
+    xlate |= pair_recv_add(dnb, 2 * Nc, xin + 2 * XS, XTAG + 3, t);
+  } else {
+    __syncthreads();
   }
-  __syncthreads();
   MID_STAMP();
 
   // ---- M11: cross-graph backward: dx'_I = sum_c dn_c[0] ks[c][I] + dn_c[1] kt[c][I] ----
@@ -1684,8 +1804,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int l = row0 + 4 * (lane >> 4) + q;
-        if (l <= HS) pb[E3_W1 + l * HS + k] = c[q];
-        else if (l == HS + 1) pb[E3_B1 + k] = c[q];
+        if (l <= HS) pb[E3_W1 + l * HS + k] = redund ? 0.f : c[q];
+        else if (l == HS + 1) pb[E3_B1 + k] = redund ? 0.f : c[q];
       }
     }
   } else if (wv < 8) {
@@ -1698,14 +1818,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int l = row0 + 4 * (lane >> 4) + q;
-        if (l < HS) pb[E1_W5 + l * HS + k] = c[q];
-        else if (l == HS) pb[E1_B5 + k] = twoNe1 * c[q];
+        if (l < HS) pb[E1_W5 + l * HS + k] = redund ? 0.f : c[q];
+        else if (l == HS) pb[E1_B5 + k] = redund ? 0.f : twoNe1 * c[q];
       }
     }
   } else if (wv == 8 && lane <= HS) {
     float acc = 0.f;
     for (int rb = 0; rb < ntm_e; ++rb) acc += dw2p[rb * 21 + lane];
-    pb[lane < HS ? E3_W2 + lane : E3_B2] = acc;
+    pb[lane < HS ? E3_W2 + lane : E3_B2] = redund ? 0.f : acc;
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 3) pb[NP + 2 + t] = 0.f;                  // trailer / pad
@@ -1761,7 +1881,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, lrow2, Ne, red2);
+  const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
+  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, lrow2, nlo, nhi, red2);
   __syncthreads();
   if (t < 4 * HS) {
     const int w = t / HS, k = t - w * HS;
@@ -1778,6 +1899,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     pb[E1_W1 + 3 * HS + t] = s3;
     pb[E1_B1 + t] = s2;
   }
+  if (SPLIT && xlate) pb[NP] = __builtin_nanf("");    // a pair exchange timed out: loud
   MID_STAMP();
 #undef MID_STAMP
 }
@@ -1940,7 +2062,7 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
 
 struct Work {   // workspace carve (floats)
-  size_t Esave, rowq, gam, part, aux, total;
+  size_t Esave, rowq, gam, part, aux, xch, total;
 };
 
 Work work_layout(const hdg_shape* s) {
@@ -1952,8 +2074,11 @@ Work work_layout(const hdg_shape* s) {
   w.Esave = take(3 * B * Ne * HS);
   w.rowq = take((B * Ne * HS + 1) / 2);     // u16
   w.gam = take(B * NC16 * NC16);
-  w.part = take(B * (size_t)NPART);
+  w.part = take(2 * B * (size_t)NPART);    // one partial row per block (2 per commit split)
   w.aux = take(8);
+  // block-pair inboxes (split mode): [B][2 halves][XSLOTS][NC16*HS] u64 (value, tag) words;
+  // zero at allocation, left zero by every completed launch
+  w.xch = take(2 * B * 2 * (size_t)XSLOTS * NC16 * HS);
   w.total = o;
   return w;
 }
@@ -2066,7 +2191,26 @@ int check_batch(const hdg_batch* bt) {
   const int var = resolve(s);                    \
   if (var < 0) return HDG_EINVAL
 
-template <int SMAXC, bool TRAIN, bool STAMPS>
+// Split mode (two blocks per commit, hunk rows split by parity, three block-pair
+// exchanges) needs every block resident at once: one 1024-thread block per CU, so
+// 2 B <= CUs of the device.  HDG_FUSED_SPLIT=0 forces one block per commit, =1 asks for
+// the split whenever it is safe; default: split when safe.
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return n;
+}
+
+bool use_split(const hdg_shape* s) {
+  const char* e = getenv("HDG_FUSED_SPLIT");
+  if (e && e[0] == '0') return false;
+  return 2 * s->batch <= cu_count();
+}
+
+int part_rows(const hdg_shape* s, bool split) { return split ? 2 * s->batch : s->batch; }
+
+template <int SMAXC, bool TRAIN, bool STAMPS, bool SPLIT>
 hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                        const Work& w, float* probs, float* logits, float ce_scale,
                        unsigned long long* stamps, const float* bpow, hipStream_t st) {
@@ -2074,27 +2218,36 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
   const size_t lds = (size_t)L.total * 4;
   static bool attr_set = false;   // the attribute is per function; 160 KiB covers every shape
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_commit_step<SMAXC, TRAIN, STAMPS>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_commit_step<SMAXC, TRAIN, STAMPS, SPLIT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS>), dim3(s->batch), dim3(NT_MID), lds, st,
-                     bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params, ws + w.Esave,
-                     (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, probs, logits, s->ne,
-                     s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow);
+  const int grid = SPLIT ? 2 * s->batch : s->batch;
+  hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS, SPLIT>), dim3(grid), dim3(NT_MID), lds,
+                     st, bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params,
+                     ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, probs, logits,
+                     s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow, s->batch,
+                     (unsigned long long*)(ws + w.xch));
   return hipGetLastError();
 }
 
 template <bool TRAIN, bool STAMPS = false>
 hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                          const Work& w, float* probs, float* logits, float ce_scale,
-                         unsigned long long* stamps, hipStream_t st, const float* bpow = nullptr) {
+                         unsigned long long* stamps, hipStream_t st, bool split,
+                         const float* bpow = nullptr) {
+#define HDG_STEP(SM)                                                                              \
+  return split ? launch_step<SM, TRAIN, STAMPS, true>(s, bt, params, ws, w, probs, logits,       \
+                                                      ce_scale, stamps, bpow, st)                 \
+               : launch_step<SM, TRAIN, STAMPS, false>(s, bt, params, ws, w, probs, logits,      \
+                                                       ce_scale, stamps, bpow, st)
   switch (smax_c(s->nc)) {
-    case 5: return launch_step<5, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
-    case 8: return launch_step<8, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
-    default: return launch_step<10, TRAIN, STAMPS>(s, bt, params, ws, w, probs, logits, ce_scale, stamps, bpow, st);
+    case 5: HDG_STEP(5);
+    case 8: HDG_STEP(8);
+    default: HDG_STEP(10);
   }
+#undef HDG_STEP
 }
 
 float pair_count(const hdg_shape* s) {
@@ -2161,12 +2314,14 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
   }
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
+  const bool split = use_split(s);
   HIP_TRY(mark(0));
   HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, 10.f / pair_count(s), nullptr, st));
+                              out ? out->logits : nullptr, 10.f / pair_count(s), nullptr, st,
+                              split));
   HIP_TRY(mark(1));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st,
-                     ws + w.part, s->batch, 0, GRAD_LEN, grad);
+                     ws + w.part, part_rows(s, split), 0, GRAD_LEN, grad);
   HIP_TRY(hipGetLastError());
   HIP_TRY(mark(2));
   return 0;
@@ -2185,7 +2340,8 @@ int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* 
   if (!stamps || !workspace || !params) return fail(HDG_EINVAL, "NULL stamps/workspace/params");
   const Work w = work_layout(s);
   const hipError_t e = dispatch_step<true, true>(s, bt, params, (float*)workspace, w, nullptr,
-                                                 nullptr, 1.f, stamps, (hipStream_t)stream);
+                                                 nullptr, 1.f, stamps, (hipStream_t)stream,
+                                                 use_split(s));
   HIP_TRY(e);
   return 0;
 }
@@ -2221,11 +2377,12 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
   const float pairs = pair_count(s);
+  const bool split = use_split(s);
   HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, 10.f / pairs, nullptr, st,
+                              out ? out->logits : nullptr, 10.f / pairs, nullptr, st, split,
                               state->beta_pow));
   hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st, ws + w.part,
-                     s->batch, state->params, state->adam_m, state->adam_v, state->beta_pow,
+                     part_rows(s, split), state->params, state->adam_m, state->adam_v, state->beta_pow,
                      ws + w.aux, lr, 1.f / pairs, out ? out->stats : nullptr, grad);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -2241,11 +2398,12 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
     return hdg::wide_run(s, bt, params, nullptr, out, ce_sum, workspace, false, st);
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
+  const bool split = use_split(s);
   HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                               out ? out->logits : nullptr, 0.f, nullptr, st));
+                               out ? out->logits : nullptr, 0.f, nullptr, st, split));
   if (ce_sum) {
-    hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part, s->batch, m2::NP,
-                       m2::NP + 1, ce_sum);
+    hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part,
+                       part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);
     HIP_TRY(hipGetLastError());
   }
   return 0;

@@ -40,7 +40,7 @@ class Engine:
             raise RuntimeError(self.lib.hdg_last_error().decode())
         dev = self.device
         f32 = torch.float32
-        self.workspace = torch.empty(wsb // 4, dtype=f32, device=dev)
+        self.workspace = torch.zeros(wsb // 4, dtype=f32, device=dev)   # block-pair inboxes start at 0
         self.params = torch.zeros(self.np, dtype=f32, device=dev)
         self.m = torch.zeros(self.np, dtype=f32, device=dev)
         self.v = torch.zeros(self.np, dtype=f32, device=dev)

@@ -22,6 +22,14 @@ pytestmark = pytest.mark.gpu
 KEYS = [k for k, _, _ in __import__("oracle.layout", fromlist=["keyed_specs"]).keyed_specs(2)]
 
 
+@pytest.fixture(params=["1", "0"], ids=["split", "one_block"])
+def split_mode(request, monkeypatch):
+    """HDG_FUSED_SPLIT: "1" two blocks per commit (hunk rows split by parity, block-pair
+    exchanges; the default whenever 2 B <= CUs), "0" one block per commit."""
+    monkeypatch.setenv("HDG_FUSED_SPLIT", request.param)
+    return request.param
+
+
 def _engine(B, ne, nc):
     from hdgnn.engine import Engine
     return Engine(ne, nc, B)
@@ -87,7 +95,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("B,ne,nc,seed", CASES)
-def test_forward_matches_oracle(B, ne, nc, seed):
+def test_forward_matches_oracle(B, ne, nc, seed, split_mode):
     cb = synth_commits(B, ne, nc, seed)
     flat = layout.init_flat(seed)
     eng = _engine(B, ne, nc)
@@ -101,7 +109,7 @@ def test_forward_matches_oracle(B, ne, nc, seed):
 
 
 @pytest.mark.parametrize("B,ne,nc,seed", CASES)
-def test_gradients_match_oracle(B, ne, nc, seed):
+def test_gradients_match_oracle(B, ne, nc, seed, split_mode):
     cb = synth_commits(B, ne, nc, seed)
     flat = layout.init_flat(seed + 10)
     eng = _engine(B, ne, nc)
@@ -157,7 +165,7 @@ EDGE = {
 
 
 @pytest.mark.parametrize("case", sorted(EDGE))
-def test_edge_cases(case):
+def test_edge_cases(case, split_mode):
     B, ne, nc, seed = 2, 21, 9, 7
     cb = EDGE[case](synth_commits(B, ne, nc, seed))
     flat = layout.init_flat(seed)

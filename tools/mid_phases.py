@@ -18,14 +18,15 @@ eng = Engine(ne, nc, B)
 eng.set_params(layout.init_flat(0))
 for _ in range(3):
     eng.train_step(db)
-st = torch.zeros(B * 32, dtype=torch.int64, device="cuda")
+st = torch.zeros(2 * B * 32, dtype=torch.int64, device="cuda")   # one row per block (split: 2 per commit)
 for _ in range(3):
     _lib.check(eng.lib.hdg_debug_step_stamps(ctypes.byref(eng.shape), ctypes.byref(db.struct()),
                                             ctypes.c_void_p(eng.params.data_ptr()),
                                             ctypes.c_void_p(eng.workspace.data_ptr()),
                                             ctypes.c_void_p(st.data_ptr()), eng._stream()))
 torch.cuda.synchronize()
-s = st.view(B, 32).cpu().numpy().astype(np.int64)
+s = st.view(2 * B, 32).cpu().numpy().astype(np.int64)
+s = s[s[:, 0] > 0]
 n = int((s[0] > 0).sum())
 d = np.diff(s[:, :n], axis=1) * 10e-3   # us
 med = np.median(d, axis=0)

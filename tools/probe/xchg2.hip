@@ -37,6 +37,65 @@ __global__ __launch_bounds__(1024) void k_pair(float* xbuf, unsigned* flags, flo
   __shared__ int bad;
   if (t == 0) { bad = 0; st[0] = __builtin_amdgcn_s_memrealtime(); }
   __syncthreads();
+  if (mode == 3) {
+    // mode 3: mode 2 with two (value, tag) pairs per 16-byte write-through store / load
+    // (global_store_dwordx4 / global_load_dwordx4 sc0 sc1): half the round trips
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    u4* xb = reinterpret_cast<u4*>(xbuf);
+    const int nv = (words + 1) / 2;
+    for (int e = 1; e <= NEX; ++e) {
+      u4* mine = xb + (((size_t)c * 2 + h) * 2 + (e & 1)) * nv;
+      const u4* theirs = xb + (((size_t)c * 2 + 1 - h) * 2 + (e & 1)) * nv;
+      for (int i = t; i < nv; i += 1024) {
+        const float v0 = (float)(e * 100000 + h * 10000 + 2 * i) + lds[2 * i];
+        const float v1 = (float)(e * 100000 + h * 10000 + 2 * i + 1) + lds[2 * i + 1];
+        const u4 w = {__float_as_uint(v0), (unsigned)e, __float_as_uint(v1), (unsigned)e};
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(mine + i), "v"(w) : "memory");
+      }
+      int lb = 0;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (int i = t; i < nv; i += 1024) {
+        u4 w;
+        do {
+          asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(w) : "v"(theirs + i) : "memory");
+        } while ((w.y != (unsigned)e || w.w != (unsigned)e) &&
+                 __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull);
+        const float want0 = (float)(e * 100000 + (1 - h) * 10000 + 2 * i) + lds[2 * i];
+        const float want1 = (float)(e * 100000 + (1 - h) * 10000 + 2 * i + 1) + lds[2 * i + 1];
+        lb += w.y != (unsigned)e || w.w != (unsigned)e || __uint_as_float(w.x) != want0 ||
+              __uint_as_float(w.z) != want1;
+      }
+      if (lb) atomicAdd(&bad, lb);
+      __syncthreads();
+      if (t == 0) st[e] = __builtin_amdgcn_s_memrealtime();
+    }
+  } else if (mode == 2) {
+    unsigned long long* xb = reinterpret_cast<unsigned long long*>(xbuf);
+    for (int e = 1; e <= NEX; ++e) {
+      // double-buffered by parity (the partner may still poll round e-1's buffer)
+      unsigned long long* mine = xb + (((size_t)c * 2 + h) * 2 + (e & 1)) * words;
+      const unsigned long long* theirs = xb + (((size_t)c * 2 + 1 - h) * 2 + (e & 1)) * words;
+      for (int i = t; i < words; i += 1024) {
+        const float v = (float)(e * 100000 + h * 10000 + i) + lds[i];
+        const unsigned long long w = ((unsigned long long)(unsigned)e << 32) | __float_as_uint(v);
+        __hip_atomic_store(mine + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      int lb = 0;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (int i = t; i < words; i += 1024) {
+        unsigned long long w;
+        do {
+          w = __hip_atomic_load(theirs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } while ((unsigned)(w >> 32) != (unsigned)e &&
+                 __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull);
+        const float want = (float)(e * 100000 + (1 - h) * 10000 + i) + lds[i];
+        lb += (unsigned)(w >> 32) != (unsigned)e || __uint_as_float((unsigned)w) != want;
+      }
+      if (lb) atomicAdd(&bad, lb);
+      __syncthreads();
+      if (t == 0) st[e] = __builtin_amdgcn_s_memrealtime();
+    }
+  } else
   for (int e = 1; e <= NEX; ++e) {
     // double-buffered by exchange parity: the partner may still read exchange e-1
     float* mine = xbuf + (((size_t)c * 2 + h) * 2 + (e & 1)) * words;
@@ -89,7 +148,8 @@ int main() {
   unsigned* flags;
   unsigned long long* stamps;
   int* errs;
-  hipMalloc(&xbuf, (size_t)B * 4 * WMAX * 4);
+  hipMalloc(&xbuf, (size_t)B * 4 * WMAX * 8);
+  hipMemset(xbuf, 0, (size_t)B * 4 * WMAX * 8);
   hipMalloc(&dirty, (size_t)G * 64 * 1024 * 4);
   hipMalloc(&flags, (size_t)B * 2 * 4);
   hipMalloc(&stamps, (size_t)G * (NEX + 1) * 8);
@@ -97,8 +157,8 @@ int main() {
   hipFuncSetAttribute((const void*)k_pair, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024);
   unsigned long long* hs = (unsigned long long*)malloc((size_t)G * (NEX + 1) * 8);
   int* he = (int*)malloc(G * 4);
-  const int wl[3] = {256, 1024, 4096};
-  for (int mode = 0; mode < 2; ++mode)
+  const int wl[3] = {256, 1480, 4096};
+  for (int mode = 2; mode < 4; ++mode)
     for (int xcd = 0; xcd < 2; ++xcd)
       for (int wi = 0; wi < 3; ++wi) {
         const int words = wl[wi];
