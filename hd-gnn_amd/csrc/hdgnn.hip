@@ -524,6 +524,7 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
     atl[e] = bits;
   }
   __syncthreads();
+  __shared__ int xof[2][260];
   if (t < Ne) {
     int dr = 0, dc = 0;
     for (int w = 0; w < WE; ++w) {
@@ -532,8 +533,24 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
     }
     offl[0][t] = dr;
     offl[1][t] = dc;
+    xof[0][t] = (dr + 3) & ~3;
+    xof[1][t] = (dc + 3) & ~3;
   }
   __syncthreads();
+  if (t == 0) {            // serial scans of the padded x-list lengths, rows then columns
+    int acc = 0;
+    for (int s2 = 0; s2 < 2; ++s2) {
+      int* dst = (int*)(pb + (s2 ? L.xoffc : L.xoffr));
+      for (int i = 0; i < Ne; ++i) {
+        const int d = xof[s2][i];
+        xof[s2][i] = acc;
+        dst[i] = acc;
+        acc += d;
+      }
+      xof[s2][Ne] = acc;
+      dst[Ne] = acc;
+    }
+  }
   if (t < 2) {                                       // serial exclusive scans, once per batch
     int acc = 0;
     for (int i = 0; i < Ne; ++i) {
@@ -554,13 +571,28 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
   }
   if (t < Ne) {
     uint8_t* lb = reinterpret_cast<uint8_t*>(pb + L.lists);
+    float* xlp = reinterpret_cast<float*>(pb + L.xl);
     int nr = offl[0][t], nc2 = cbase + offl[1][t];
+    int xr = xof[0][t], xc = xof[1][t];
     for (int w = 0; w < WE; ++w) {
       uint32_t m = al[t * WE + w];
-      while (m) { lb[nr++] = (uint8_t)(32 * w + __builtin_ctz(m)); m &= m - 1u; }
+      while (m) {
+        const int j = 32 * w + __builtin_ctz(m);
+        lb[nr++] = (uint8_t)j;
+        xlp[xr++] = xl[j];
+        m &= m - 1u;
+      }
       m = atl[t * WE + w];
-      while (m) { lb[nc2++] = (uint8_t)(32 * w + __builtin_ctz(m)); m &= m - 1u; }
+      while (m) {
+        const int j = 32 * w + __builtin_ctz(m);
+        lb[nc2++] = (uint8_t)j;
+        xlp[xc++] = xl[j];
+        m &= m - 1u;
+      }
     }
+    const float qnan = __builtin_nanf("");      // clamp_fma2(NaN) = 0: pads add nothing
+    for (; xr < xof[0][t + 1]; ++xr) xlp[xr] = qnan;
+    for (; xc < xof[1][t + 1]; ++xc) xlp[xc] = qnan;
   }
   __syncthreads();
   if (t == 0) {   // serial over <= 256 sorted values, once per batch
@@ -820,7 +852,7 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
                                            const float* xs, const float* xu, const int* cum,
                                            const double* pxd, const int nd,
                                            const int* offr, const int* offc,
-                                           const uint8_t* lr, const uint8_t* lc,
+                                           const float* xlr, const float* xlc,
                                            const int Ne, float* Ps,
                                            float* __restrict__ EG, uint16_t* __restrict__ rq) {
 #pragma clang fp contract(off)
@@ -871,19 +903,30 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
     const f2 tg = {dd.x >= 0.f ? dd.x : 0.f, dd.y >= 0.f ? dd.y : 0.f};
     const f2 rd = {fabsf(dd.x) >= 0x1p-100f ? 1.f / dd.x : 0.f,
                    fabsf(dd.y) >= 0x1p-100f ? 1.f / dd.y : 0.f};
+    // neighbour x values come from the prepared NaN-padded x-lists (offr / offc here are
+    // their 4-aligned float offsets), four per 16-byte read, identical across the 10
+    // lanes of a node group (LDS broadcast): no id lookup, no cross-lane traffic
     {
       const f2 ca = sg * w1 * rd, cb = __builtin_elementwise_fma(sg, u, tg) * rd;
-      const int d = ((ABL & 4) || !live) ? 0 : offr[ic + 1] - offr[ic];
-      for_each_nbr<EG_L, false>(lr + offr[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
-        sp += clamp_fma2(xj, ca, cb);
-      });
+      const int o1 = ((ABL & 4) || !live) ? 0 : offr[ic + 1];
+      for (int o = ((ABL & 4) || !live) ? 0 : offr[ic]; o < o1; o += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xlr + o);
+        sp += clamp_fma2(xv.x, ca, cb);
+        sp += clamp_fma2(xv.y, ca, cb);
+        sp += clamp_fma2(xv.z, ca, cb);
+        sp += clamp_fma2(xv.w, ca, cb);
+      }
     }
     {
       const f2 ca = sg * w0 * rd, cb = __builtin_elementwise_fma(sg, c0 + v, tg) * rd;
-      const int d = ((ABL & 8) || !live) ? 0 : offc[ic + 1] - offc[ic];
-      for_each_nbr<EG_L, false>(lc + offc[ic], d, sub * EG_L, kp, xs, [&](int, float xj) {
-        sp += clamp_fma2(xj, ca, cb);
-      });
+      const int o1 = ((ABL & 8) || !live) ? 0 : offc[ic + 1];
+      for (int o = ((ABL & 8) || !live) ? 0 : offc[ic]; o < o1; o += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xlc + o);
+        sp += clamp_fma2(xv.x, ca, cb);
+        sp += clamp_fma2(xv.y, ca, cb);
+        sp += clamp_fma2(xv.z, ca, cb);
+        sp += clamp_fma2(xv.w, ca, cb);
+      }
     }
     sp *= dd;
     if (live && kp < EG_L) {
@@ -1137,12 +1180,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* hE = U + 2 * NE4 * HS;
   // neighbour lists (u8 ids, rows | columns): staged behind P when they fit, else read
   // from the prepared buffer in HBM through the same (generic) pointer
-  const int nnz_r = (int)pp[PL.meta + 1], nnz_c = (int)pp[PL.meta + 2];
-  const int cbase = (int)pp[PL.meta + 3];
-  const int lwords = (cbase + nnz_c + 3) >> 2;
-  const bool lfit = lwords <= L.Uwords - NE4 * HS;
-  const uint8_t* lrow = lfit ? reinterpret_cast<const uint8_t*>(U + NE4 * HS)
-                             : reinterpret_cast<const uint8_t*>(pp + PL.lists);
+  const int nnz_r = (int)pp[PL.meta + 1];
+  // neighbour x-lists (rows | columns, NaN-padded, k_prep_sort): staged behind P when they
+  // fit, else read from the prepared buffer in HBM through the same (generic) pointer
+  const int xwords = (int)pp[PL.xoffc + Ne];
+  const bool lfit = xwords <= L.Uwords - NE4 * HS;
+  const float* xlist = lfit ? U + NE4 * HS : reinterpret_cast<const float*>(pp + PL.xl);
   float l2 = 0.f;
   for (int i = t; i < NP; i += NT_MID) {
     const float w = Wg[i];
@@ -1163,12 +1206,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     cum[q] = reinterpret_cast<const int*>(pp + PL.cum)[q];
     pxd[q] = reinterpret_cast<const double*>(pp + PL.pxd)[q];
   }
-  for (int i = t; i <= Ne; i += NT_MID) {
-    offr[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
-    offc[i] = reinterpret_cast<const int*>(pp + PL.offc)[i];
+  for (int i = t; i <= Ne; i += NT_MID) {   // x-list offsets (E1); the id offsets for E2
+    offr[i] = reinterpret_cast<const int*>(pp + PL.xoffr)[i];   // are restaged before E2
+    offc[i] = reinterpret_cast<const int*>(pp + PL.xoffc)[i];
   }
   if (lfit)
-    for (int w = t; w < lwords; w += NT_MID) U[NE4 * HS + w] = __builtin_bit_cast(float, pp[PL.lists + w]);
+    for (int w = 4 * t; w < xwords; w += 4 * NT_MID)
+      *reinterpret_cast<float4*>(U + NE4 * HS + w) =
+          *reinterpret_cast<const float4*>(pp + PL.xl + w);
   for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   if (t == 0) { kzero[0] = 0.f; kzero[1] = 1.f; }
   __syncthreads();
@@ -1197,7 +1242,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   i of a and of a^T); the diagonal is removed once.  Lane map: a wave takes 3 nodes,
   //   lane = (node sub, hidden unit k), so the 20 lanes of a node walk its bits together.
   //   The row-set boundaries are kept for the backward.
-  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, lrow, lrow + cbase, Ne, Ps, EG, rq);
+  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlist, xlist, Ne, Ps, EG, rq);
   __syncthreads();
   MID_STAMP();
 
@@ -1850,6 +1895,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
                               : reinterpret_cast<const uint8_t*>(pp + PL.lists);
   if (rfit)
     for (int w = t; w < ((nnz_r + 3) >> 2); w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
+  for (int i = t; i <= Ne; i += NT_MID) offr[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];   // id CSR
   for (int task = wv; task < 2 * HS; task += NT_MID / 64) {        // wave-uniform
     const int k = task >> 1, which = task & 1;
     const bool suf = Ws[E1_W1 + HS + k] >= 0.f;

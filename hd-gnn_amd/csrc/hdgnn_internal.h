@@ -26,13 +26,16 @@ constexpr int HS = 20;   // h_size = De_e = De_er (model_2.py:163, 192, 247, 306
 //   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
 //   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
 //   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
+//   xoffr, xoffc offsets (in floats, multiples of 4) of each node's neighbour x-list in xl
+//   xl           f32 x_j of the a = 1 neighbours j of each node, row lists then column
+//                lists, each padded with NaN to a multiple of 4 (16-byte vector reads)
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // The general path has its own per-commit layout (wide.hip, GenPrep): ks / kt / ncst as
 // here, transposed class bits, and the sorted-x tables without the byte neighbour lists.
 // ------------------------------------------------------------------------------
 struct PrepLayout {
-  int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, words;
+  int xsrt, perm, xu, cum, pxd, meta, offr, offc, ks, kt, ncst, lists, xoffr, xoffc, xl, words;
 };
 
 __host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
@@ -52,6 +55,10 @@ __host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
   L.kt = o;   o += kw;
   L.ncst = o; o += (2 * Nc + 3) & ~3;
   L.lists = o; o += (2 * Ne * (Ne - 1) + 4 + 3) / 4;   // u8 neighbour ids: rows | columns
+  L.xoffr = o; o += NE4 + 4;
+  L.xoffc = o; o += NE4 + 4;
+  o = (o + 3) & ~3;                   // 16-byte aligned
+  L.xl = o;   o += 2 * Ne * (Ne - 1) + 6 * Ne + 8;   // f32 neighbour x-lists, NaN-padded
   L.words = (o + 63) & ~63;
   return L;
 }

@@ -12,10 +12,11 @@ __global__ __launch_bounds__(1024) void mb_e1(int Ne, int iters, float* out, flo
   __shared__ float xs[256], xu[256], Ps[256 * HS];
   __shared__ int cum[260], offr[260], offc[260];
   __shared__ double pxd[260];
-  __shared__ uint8_t lr[256 * 16], lc[256 * 16];
+  __shared__ __attribute__((aligned(16))) float lr[256 * 16], lc[256 * 16];   // x-lists
   const int t = threadIdx.x, b = blockIdx.x;
   for (int i = t; i < 2128; i += 1024) Ws[i] = 0.01f * (float)((i * 2654435761u) % 200) - 1.f;
   for (int i = t; i < Ne; i += 1024) xs[i] = (float)((i * 7 + b) % 10);
+  __syncthreads();
   if (t < 10) { xu[t] = (float)t; }
   if (t <= 10) { cum[t] = t * Ne / 10; pxd[t] = 0.0; }
   if (t == 0) {              // ~5 % density: degree 8..12 per row and column
@@ -23,8 +24,10 @@ __global__ __launch_bounds__(1024) void mb_e1(int Ne, int iters, float* out, flo
     for (int i = 0; i < Ne; ++i) {
       offr[i] = ar; offc[i] = ac;
       const int dr = 8 + (i * 3 + b) % 5, dc = 8 + (i * 7 + b) % 5;
-      for (int n = 0; n < dr; ++n) lr[ar++] = (uint8_t)((i + 1 + 17 * n) % Ne);
-      for (int n = 0; n < dc; ++n) lc[ac++] = (uint8_t)((i + 3 + 13 * n) % Ne);
+      for (int n = 0; n < dr; ++n) lr[ar++] = xs[(i + 1 + 17 * n) % Ne];
+      for (int n = 0; n < dc; ++n) lc[ac++] = xs[(i + 3 + 13 * n) % Ne];
+      while (ar & 3) lr[ar++] = __builtin_nanf("");
+      while (ac & 3) lc[ac++] = __builtin_nanf("");
     }
     offr[Ne] = ar; offc[Ne] = ac;
   }

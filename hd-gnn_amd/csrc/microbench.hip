@@ -7,7 +7,7 @@
 namespace {
 
 template <int MODE, int ABL = 0>
-__global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
+__global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out, int rmul = 1) {
   constexpr int SMAXC = 5, NC16 = 80;
   __shared__ __attribute__((aligned(16))) float A[NC16 * HS], B[NC16 * HS], R[NC16 * HS],
       C[NC16 * HS], wr[NC16 * HS], wc[NC16 * HS], dl[HS], ys[HS];
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(1024) void mb_tile(int N, int iters, float* out) {
   const int g = t >> 8, tg = t & 255;
   for (int it = 0; it < iters; ++it)
     pair_tile<5, SMAXC, MODE, HS, ABL>(N, tg, A, B, g * 5, dl, bits, 3, wr, wc, gam, NC16, R, C, ys,
-                                  cred + g * tile_cred_words<SMAXC, 5>());
+                                  cred + g * tile_cred_words<SMAXC, 5>(), rmul, 0);
   if (t == 0) out[blockIdx.x] = R[7] + C[11] + ys[3];
 }
 
@@ -67,6 +67,14 @@ int main() {
   printf("  MODE0 neither %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<0, 3>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE1 no y    %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<1, 1>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
   printf("  MODE2 no y    %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<2, 1>), dim3(nb), dim3(1024), 0, 0, 74, it, out); }, B, IT));
+  printf("half rows (split mode, rmul = 2):\n");
+  printf("  MODE0 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<0>, dim3(nb), dim3(1024), 0, 0, 74, it, out, 2); }, B, IT));
+  printf("  MODE1 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<1>, dim3(nb), dim3(1024), 0, 0, 74, it, out, 2); }, B, IT));
+  printf("  MODE2 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<2>, dim3(nb), dim3(1024), 0, 0, 74, it, out, 2); }, B, IT));
+  printf("  MODE0 neither %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL((mb_tile<0, 3>), dim3(nb), dim3(1024), 0, 0, 74, it, out, 2); }, B, IT));
+  printf("  N=16 MODE0 (one row block, fixed cost) %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<0>, dim3(nb), dim3(1024), 0, 0, 16, it, out, 1); }, B, IT));
+  printf("  N=16 MODE1 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<1>, dim3(nb), dim3(1024), 0, 0, 16, it, out, 1); }, B, IT));
+  printf("  N=16 MODE2 %8.2f us\n", time_kernel([&](int nb, int it) { hipLaunchKernelGGL(mb_tile<2>, dim3(nb), dim3(1024), 0, 0, 16, it, out, 1); }, B, IT));
   CK(hipDeviceSynchronize());
   return 0;
 }

@@ -14,3 +14,4 @@ for f in ("bench_split", "bench_one"):
             d = json.loads(l); print(f, d["value"], d["ms_per_step"], d["kernels_ms"])
 PY
 grep -v amdgpu gpurun_out/phases_split.log
+timeout -k 10 60 hd-gnn_amd/csrc/mb_entity > gpurun_out/mbe.log 2>&1 && cat gpurun_out/mbe.log
