@@ -474,7 +474,7 @@ __device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n 
 //   xu[NE4]      the nd distinct x values      cum[NE4+4] cum[q] = #nodes with x < xu[q]
 //   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
 //   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
-//   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
+//   lists        u8 ids of the row neighbours, padded like the row x-lists (xoffr)
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // ------------------------------------------------------------------------------
@@ -572,26 +572,23 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
   if (t < Ne) {
     uint8_t* lb = reinterpret_cast<uint8_t*>(pb + L.lists);
     float* xlp = reinterpret_cast<float*>(pb + L.xl);
-    int nr = offl[0][t], nc2 = cbase + offl[1][t];
     int xr = xof[0][t], xc = xof[1][t];
     for (int w = 0; w < WE; ++w) {
       uint32_t m = al[t * WE + w];
       while (m) {
         const int j = 32 * w + __builtin_ctz(m);
-        lb[nr++] = (uint8_t)j;
+        lb[xr] = (uint8_t)j;
         xlp[xr++] = xl[j];
         m &= m - 1u;
       }
       m = atl[t * WE + w];
       while (m) {
-        const int j = 32 * w + __builtin_ctz(m);
-        lb[nc2++] = (uint8_t)j;
-        xlp[xc++] = xl[j];
+        xlp[xc++] = xl[32 * w + __builtin_ctz(m)];
         m &= m - 1u;
       }
     }
     const float qnan = __builtin_nanf("");      // clamp_fma2(NaN) = 0: pads add nothing
-    for (; xr < xof[0][t + 1]; ++xr) xlp[xr] = qnan;
+    for (; xr < xof[0][t + 1]; ++xr) { xlp[xr] = qnan; lb[xr] = 0; }
     for (; xc < xof[1][t + 1]; ++xc) xlp[xc] = qnan;
   }
   __syncthreads();
@@ -945,7 +942,8 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
                                            const float* xs, const int* cum, const double* pxd,
                                            const int nd, const uint16_t* __restrict__ rq,
                                            const float* rho, const float* Tr, const float* Tx,
-                                           const int TL, const int* offr, const uint8_t* lr,
+                                           const int TL, const int* xoff, const int* coff,
+                                           const uint8_t* idl, const float* xlr,
                                            const int n0, const int n1, float* red2) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
@@ -983,8 +981,9 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       s2[h] = rs;
     }
     f2 sd = {0.f, 0.f}, sx = sd;                     // sum dm, sum x_j dm
-    const int d = live ? offr[ic + 1] - offr[ic] : 0;
-    for_each_nbr<EG_L, true>(lr + offr[ic], d, sub * EG_L, kp, xs, [&](int j, float xj) {
+    // row neighbours from the padded (id, x) lists: 4 ids in one u32 and 4 x values in one
+    // 16-byte read per step, identical across the node group's lanes (LDS broadcast)
+    auto nbr = [&](const int j, const float xj) {
       const f2 rj = *reinterpret_cast<const f2*>(rho + j * HS + k0);
       const f2 z0 = u + xj * w1;
       const f2 z1 = z0 + dd;
@@ -995,7 +994,25 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       sd += dm;
       sx = __builtin_elementwise_fma((f2){xj, xj}, dm, sx);
       s3 += m1g;
-    });
+    };
+    const int o0 = live ? xoff[ic] : 0;
+    const int d = live ? coff[ic + 1] - coff[ic] : 0;
+    int q = 0;
+    for (; q + 4 <= d; q += 4) {
+      const float4 xv = *reinterpret_cast<const float4*>(xlr + o0 + q);
+      const uint32_t jw = *reinterpret_cast<const uint32_t*>(idl + o0 + q);
+      nbr(jw & 0xffu, xv.x);
+      nbr((jw >> 8) & 0xffu, xv.y);
+      nbr((jw >> 16) & 0xffu, xv.z);
+      nbr(jw >> 24, xv.w);
+    }
+    if (q < d) {                             // 1-3 left (group-uniform); pads are skipped
+      const float4 xv = *reinterpret_cast<const float4*>(xlr + o0 + q);
+      const uint32_t jw = *reinterpret_cast<const uint32_t*>(idl + o0 + q);
+      nbr(jw & 0xffu, xv.x);
+      if (q + 1 < d) nbr((jw >> 8) & 0xffu, xv.y);
+      if (q + 2 < d) nbr((jw >> 16) & 0xffu, xv.z);
+    }
     s0 = __builtin_elementwise_fma((f2){xi, xi}, sd, s0);
     s1 += sx;
     s2 += sd;
@@ -1180,7 +1197,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* hE = U + 2 * NE4 * HS;
   // neighbour lists (u8 ids, rows | columns): staged behind P when they fit, else read
   // from the prepared buffer in HBM through the same (generic) pointer
-  const int nnz_r = (int)pp[PL.meta + 1];
   // neighbour x-lists (rows | columns, NaN-padded, k_prep_sort): staged behind P when they
   // fit, else read from the prepared buffer in HBM through the same (generic) pointer
   const int xwords = (int)pp[PL.xoffc + Ne];
@@ -1889,13 +1905,20 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Tr = U + NE4 * HS;                // [HS][TL]   (E_bar, dq, dE slots are dead)
   float* Tx = Tr + HS * TL;                // [HS][TL]
   float* red2 = Tx + HS * TL;              // [16 waves][4][HS]  (ends below rho_off)
-  // row neighbour lists again, staged into the P slot (dead after dW5) when they fit
-  const bool rfit = ((nnz_r + 3) >> 2) <= NE4 * HS;
-  const uint8_t* lrow2 = rfit ? reinterpret_cast<const uint8_t*>(Ps)
-                              : reinterpret_cast<const uint8_t*>(pp + PL.lists);
-  if (rfit)
-    for (int w = t; w < ((nnz_r + 3) >> 2); w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
-  for (int i = t; i <= Ne; i += NT_MID) offr[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];   // id CSR
+  // row neighbour (id, x) lists (padded, offsets xoffr still in offr), staged into the P
+  // slot (dead after dW5) when they fit; offc <- the compact row CSR (degrees)
+  const int rl = (int)pp[PL.xoffc];                 // padded row-list length (multiple of 4)
+  const bool rfit = rl / 4 + rl <= NE4 * HS;
+  const uint8_t* idl2 = rfit ? reinterpret_cast<const uint8_t*>(Ps)
+                             : reinterpret_cast<const uint8_t*>(pp + PL.lists);
+  const float* xl2 = rfit ? Ps + ((rl / 4 + 3) & ~3) : reinterpret_cast<const float*>(pp + PL.xl);
+  if (rfit) {
+    for (int w = t; w < rl / 4; w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
+    for (int w = 4 * t; w < rl; w += 4 * NT_MID)
+      *reinterpret_cast<float4*>(Ps + ((rl / 4 + 3) & ~3) + w) =
+          *reinterpret_cast<const float4*>(pp + PL.xl + w);
+  }
+  for (int i = t; i <= Ne; i += NT_MID) offc[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
   for (int task = wv; task < 2 * HS; task += NT_MID / 64) {        // wave-uniform
     const int k = task >> 1, which = task & 1;
     const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
@@ -1928,7 +1951,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   __syncthreads();
   MID_STAMP();
   const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
-  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, lrow2, nlo, nhi, red2);
+  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc, idl2, xl2, nlo, nhi,
+             red2);
   __syncthreads();
   if (t < 4 * HS) {
     const int w = t / HS, k = t - w * HS;

@@ -25,8 +25,9 @@ constexpr int HS = 20;   // h_size = De_e = De_er (model_2.py:163, 192, 247, 306
 //   xu[NE4]      the nd distinct x values      cum[NE4+4] cum[q] = #nodes with x < xu[q]
 //   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
 //   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
-//   lists        u8 neighbour ids, row lists then column lists (byte offset meta[3])
-//   xoffr, xoffc offsets (in floats, multiples of 4) of each node's neighbour x-list in xl
+//   lists        u8 ids of the a = 1 row neighbours, laid out like the row x-lists
+//                (node i at byte xoffr[i], zero-padded to a multiple of 4)
+//   xoffr, xoffc offsets (in elements, multiples of 4) of each node's neighbour list in xl
 //   xl           f32 x_j of the a = 1 neighbours j of each node, row lists then column
 //                lists, each padded with NaN to a multiple of 4 (16-byte vector reads)
 //   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
@@ -54,7 +55,7 @@ __host__ __device__ inline PrepLayout prep_layout(int Ne, int Nc) {
   L.ks = o;   o += kw;
   L.kt = o;   o += kw;
   L.ncst = o; o += (2 * Nc + 3) & ~3;
-  L.lists = o; o += (2 * Ne * (Ne - 1) + 4 + 3) / 4;   // u8 neighbour ids: rows | columns
+  L.lists = o; o += (Ne * (Ne - 1) + 3 * Ne + 4 + 3) / 4;   // u8 row neighbour ids, padded
   L.xoffr = o; o += NE4 + 4;
   L.xoffc = o; o += NE4 + 4;
   o = (o + 3) & ~3;                   // 16-byte aligned
