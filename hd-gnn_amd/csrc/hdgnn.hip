@@ -445,6 +445,17 @@ __device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) 
 
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
 
+// write-through stores / L2-bypassing loads of rows a partner block reads (parked rows)
+__device__ __forceinline__ void st_wt(float* p, const float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float2 ld_wt2(const float* p) {   // system-scope atomic: sc0 sc1
+  const unsigned long long w = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_float2(__uint_as_float((uint32_t)w), __uint_as_float((uint32_t)(w >> 32)));
+}
+
+
 
 // inclusive scan over the 64 lanes of a wave with DPP only (GFX9 row_shr + row_bcast):
 // no LDS round trips.  Lanes shifted in from outside a row read 0 (bound_ctrl).
@@ -850,16 +861,17 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
                                            const double* pxd, const int nd,
                                            const int* offr, const int* offc,
                                            const float* xlr, const float* xlc,
-                                           const int Ne, float* Ps,
-                                           float* __restrict__ EG, uint16_t* __restrict__ rq) {
+                                           const int n0, const int n1, float* Ps,
+                                           float* __restrict__ EG, uint16_t* __restrict__ rq,
+                                           const bool wt = false) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
   const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
   const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f}, ca[2] = {ea.w0 >= 0.f, eb.w0 >= 0.f};
-  for (int base = EG_N * wv; base < Ne; base += EG_N * (NT_MID / 64)) {     // wave-uniform
+  for (int base = n0 + EG_N * wv; base < n1; base += EG_N * (NT_MID / 64)) {   // wave-uniform
     const int i = base + sub;
-    const bool live = sub < EG_N && i < Ne;
+    const bool live = sub < EG_N && i < n1;
     const int ic = live ? i : 0;
     const float xi = xs[ic];
     const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
@@ -929,7 +941,12 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
     if (live && kp < EG_L) {
       const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
       *reinterpret_cast<float2*>(Ps + i * HS + k0) = P;
-      *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
+      if (wt) {                          // parked for the partner block (split mode)
+        st_wt(EG + i * HS + k0, P.x);
+        st_wt(EG + i * HS + k0 + 1, P.y);
+      } else {
+        *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
+      }
       rq[i * HS + k0] = (uint16_t)br[0];
       rq[i * HS + k0 + 1] = (uint16_t)br[1];
     }
@@ -1054,7 +1071,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
 // send and receive; n is even.
 // ------------------------------------------------------------------------------
 constexpr uint32_t XTAG = 0xC0DE0000u;          // + slot + 1; no NaN/Inf/huge fill pattern
-constexpr int XSLOTS = 3;                       // H partial, D_tau partial, dn partial
+constexpr int XSLOTS = 4;                       // H, D_tau, dn partials; n partial + o rows
 constexpr unsigned long long XWAIT = 2000000ull;   // s_memrealtime ticks (100 MHz) = 20 ms
 typedef uint32_t xu4 __attribute__((ext_vector_type(4)));
 
@@ -1068,8 +1085,11 @@ __device__ __forceinline__ xu4 xload(const xu4* p) {
   return w;
 }
 
+// The send first waits for this thread's earlier stores (vmcnt counts stores on gfx9):
+// rows parked write-through before a send are in memory once the partner sees the tags.
 __device__ __forceinline__ void pair_send(const float* v, const int n, xu4* __restrict__ out,
                                           const uint32_t tag, const int t) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int e = t; 2 * e < n; e += NT_MID)
     xstore(out + e, (xu4){__float_as_uint(v[2 * e]), tag, __float_as_uint(v[2 * e + 1]), tag});
 }
@@ -1258,7 +1278,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   i of a and of a^T); the diagonal is removed once.  Lane map: a wave takes 3 nodes,
   //   lane = (node sub, hidden unit k), so the 20 lanes of a node walk its bits together.
   //   The row-set boundaries are kept for the backward.
-  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlist, xlist, Ne, Ps, EG, rq);
+  // split mode: each block of the pair takes its half of the nodes through E1 -> M3 (and
+  // E2); P, E_bar and h rows are parked write-through for the partner's redundant phases
+  const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
+  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlist, xlist, nlo, nhi, Ps, EG, rq,
+             SPLIT);
   __syncthreads();
   MID_STAMP();
 
@@ -1267,10 +1291,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   h = relu([x, E_bar] W1' + b1')     (mlp2_entity_B1, model_2.py:190-205)
   //   o = h w2' + b2',  x' = relu(o)
   const int ntm_e = (Ne + 15) >> 4;
-  for (int rb = wv; rb < ntm_e; rb += NT_MID / 64) {          // wave-uniform
+  for (int rb = (nlo >> 4) + wv; rb <= ((nhi - 1) >> 4); rb += NT_MID / 64) {   // wave-uniform
     const int row0 = rb * 16;
     const int ir = row0 + (lane & 15);                         // this lane's A row
-    const bool rv = ir < Ne;
+    const bool rv = ir >= nlo && ir < nhi;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int col0 = cb * 16;
@@ -1283,9 +1307,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) {
+          if (i >= nlo && i < nhi) {
             Eb[i * HS + m] = c[q] + bias;
-            EbG[i * HS + m] = c[q] + bias;
+            if (SPLIT) st_wt(EbG + i * HS + m, c[q] + bias);
+            else EbG[i * HS + m] = c[q] + bias;
           }
         }
       }
@@ -1302,15 +1327,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) {
+          if (i >= nlo && i < nhi) {
             const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
             hE[i * HS + m] = v;
-            hEG[i * HS + m] = v;
+            if (SPLIT) st_wt(hEG + i * HS + m, v);
+            else hEG[i * HS + m] = v;
           }
         }
       }
     }
-    if (lane < 16 && row0 + lane < Ne) {
+    if (lane < 16 && row0 + lane >= nlo && row0 + lane < nhi) {
       const int i = row0 + lane;
       float o = Ws[E3_B2];
 #pragma unroll
@@ -1328,38 +1354,49 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
     const float* ncst = reinterpret_cast<const float*>(pp + PL.ncst);
-    // 4 tasks (c, m) per trip, each lane's <= 4 elements per task unrolled: all 16 global
-    // loads of a trip are in flight before the first reduction
+    // 4 tasks (c, m) per trip, each lane's <= QN elements per task unrolled: all global
+    // loads of a trip are in flight before the first reduction.  Split mode: the block's
+    // own nodes only; the partial n and the own o rows go through one pair exchange.
+    constexpr int QN = SPLIT ? 2 : 4;                 // Ne <= 256: a half is <= 128 nodes
+    float* xsc = Ps;                                  // [2 Nc n partials | NE4 o rows]
     for (int t0 = 4 * wv; t0 < 2 * Nc; t0 += 4 * (NT_MID / 64)) {   // wave-uniform
-      float kv[4][4], xv[4];
+      float kv[4][QN], xv[QN];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int I = lane + 64 * q;
-        xv[q] = I < Ne ? xps[I] : 0.f;
+      for (int q = 0; q < QN; ++q) {
+        const int I = nlo + lane + 64 * q;
+        xv[q] = I < nhi ? xps[I] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int task = t0 + u < 2 * Nc ? t0 + u : 2 * Nc - 1;
         const uint16_t* kr = ((task & 1) ? kt : ks) + (size_t)(task >> 1) * Ne;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int I = lane + 64 * q;
-          kv[u][q] = (float)kr[I < Ne ? I : Ne - 1];
+        for (int q = 0; q < QN; ++q) {
+          const int I = nlo + lane + 64 * q;
+          kv[u][q] = (float)kr[I < nhi ? I : nlo];
         }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float a = 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a = fmaf(kv[u][q], xv[q], a);
+        for (int q = 0; q < QN; ++q) a = fmaf(kv[u][q], xv[q], a);
         const float v = wave_sum(a);
         const int task = t0 + u;
-        if (lane == 0 && task < 2 * Nc) nb[4 * (task >> 1) + (task & 1)] = v;
+        if (lane == 0 && task < 2 * Nc) {
+          if (SPLIT) xsc[task] = v;
+          else nb[4 * (task >> 1) + (task & 1)] = v;
+        }
       }
     }
     for (int c = t; c < Nc; c += NT_MID) {
       nb[4 * c + 2] = ncst[2 * c];
       nb[4 * c + 3] = ncst[2 * c + 1];
+    }
+    if constexpr (SPLIT) {
+      for (int i = t; i < NE4; i += NT_MID) xsc[2 * Nc + i] = (i >= nlo && i < nhi) ? os[i] : 0.f;
+      __syncthreads();
+      pair_send(xsc, 2 * Nc + NE4, xout + 3 * XS, XTAG + 4, t);   // constants overlap
     }
   }
   // per-block constants: delta, eps, c, M = V2 U1e, sigma/tau offsets
@@ -1381,6 +1418,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
     for (int m = 0; m < HS; ++m) acc = fmaf(Ws[H1_W2 + l * HS + m], Ws[H2_W1 + (2 + m) * HS + k], acc);
     Mm[e] = acc;
+  }
+  if constexpr (SPLIT) {
+    float* xsc = Ps;
+    xlate |= pair_recv_add(xsc, 2 * Nc + NE4, xin + 3 * XS, XTAG + 4, t);
+    for (int e = t; e < 2 * Nc; e += NT_MID) nb[4 * (e >> 1) + (e & 1)] = xsc[e];
+    for (int i = t; i < Ne; i += NT_MID) os[i] = xsc[2 * Nc + i];
   }
   __syncthreads();
   MID_STAMP();
@@ -1727,7 +1770,17 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     dnb[e] = acc;
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(dnb, 2 * Nc, xout + 2 * XS, XTAG + 3, t);   // dV1 overlaps
+  if constexpr (SPLIT) {
+    pair_send(dnb, 2 * Nc, xout + 2 * XS, XTAG + 3, t);   // dV1 overlaps
+    // waves 4-15 warm this XCD's L2 with the count matrices (M11 reads every column; M3
+    // fetched only the own half) while waves 0-3 run dV1
+    if (wv >= 4) {
+      const int nw = PL.ncst - PL.ks;                     // ks | kt words
+      uint32_t acc = 0;
+      for (int w = (t - 256) * 16; w < nw; w += (NT_MID - 256) * 16) acc ^= pp[PL.ks + w];
+      asm volatile("" ::"v"(acc));
+    }
+  }
   if (wv < 4) {         // dV1 rows 0..7 and dc1: [n^T; 1] . Dalpha, n^T . Dbeta  (MFMA)
     const int side = wv >> 1, col0 = (wv & 1) * 16;
     const float* D = side ? Dbe : Dal;
@@ -1796,7 +1849,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     float4* d0 = reinterpret_cast<float4*>(Ps);
     float4* d1 = reinterpret_cast<float4*>(Eb);
     float4* d2 = reinterpret_cast<float4*>(hB);
-    for (int e = t; e < Ne * HS / 4; e += NT_MID) { d0[e] = s0[e]; d1[e] = s1[e]; d2[e] = s2[e]; }
+    if constexpr (SPLIT) {        // half the rows were parked write-through by the partner
+      float2* e0 = reinterpret_cast<float2*>(Ps);
+      float2* e1 = reinterpret_cast<float2*>(Eb);
+      float2* e2 = reinterpret_cast<float2*>(hB);
+      for (int e = t; e < Ne * HS / 2; e += NT_MID) {
+        e0[e] = ld_wt2(EG + 2 * e);
+        e1[e] = ld_wt2(EbG + 2 * e);
+        e2[e] = ld_wt2(hEG + 2 * e);
+      }
+    } else {
+      for (int e = t; e < Ne * HS / 4; e += NT_MID) { d0[e] = s0[e]; d1[e] = s1[e]; d2[e] = s2[e]; }
+    }
   }
   __syncthreads();
   MID_STAMP();
@@ -1950,7 +2014,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
   entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc, idl2, xl2, nlo, nhi,
              red2);
   __syncthreads();

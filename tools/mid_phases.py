@@ -33,3 +33,6 @@ med = np.median(d, axis=0)
 for i, v in enumerate(med):
     print("phase %2d->%2d  %8.2f us" % (i, i + 1, v))
 print("total (median block) %.1f us; block span max %.1f us" % (np.median(d.sum(1)), d.sum(1).max()))
+t0 = s[:, 0] - s[:, 0].min()
+print("block start skew: median %.2f us, max %.2f us; first start -> last end %.1f us" % (
+    np.median(t0) * 10e-3, t0.max() * 10e-3, (s[:, n - 1].max() - s[:, 0].min()) * 10e-3))
