@@ -915,28 +915,33 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
     // neighbour x values come from the prepared NaN-padded x-lists (offr / offc here are
     // their 4-aligned float offsets), four per 16-byte read, identical across the 10
     // lanes of a node group (LDS broadcast): no id lookup, no cross-lane traffic
-    {
-      const f2 ca = sg * w1 * rd, cb = __builtin_elementwise_fma(sg, u, tg) * rd;
-      const int o1 = ((ABL & 4) || !live) ? 0 : offr[ic + 1];
-      for (int o = ((ABL & 4) || !live) ? 0 : offr[ic]; o < o1; o += 4) {
-        const float4 xv = *reinterpret_cast<const float4*>(xlr + o);
-        sp += clamp_fma2(xv.x, ca, cb);
-        sp += clamp_fma2(xv.y, ca, cb);
-        sp += clamp_fma2(xv.z, ca, cb);
-        sp += clamp_fma2(xv.w, ca, cb);
+    // (eight per trip: two 16-byte reads in flight; xlr / xlc point into LDS when staged,
+    // so the reads are ds_read_b128, not flat)
+    auto xsum = [&](const float* xl, int o, const int o1, const f2 ca, const f2 cb) {
+      for (; o + 8 <= o1; o += 8) {
+        const float4 xa = *reinterpret_cast<const float4*>(xl + o);
+        const float4 xb = *reinterpret_cast<const float4*>(xl + o + 4);
+        sp += clamp_fma2(xa.x, ca, cb);
+        sp += clamp_fma2(xa.y, ca, cb);
+        sp += clamp_fma2(xa.z, ca, cb);
+        sp += clamp_fma2(xa.w, ca, cb);
+        sp += clamp_fma2(xb.x, ca, cb);
+        sp += clamp_fma2(xb.y, ca, cb);
+        sp += clamp_fma2(xb.z, ca, cb);
+        sp += clamp_fma2(xb.w, ca, cb);
       }
-    }
-    {
-      const f2 ca = sg * w0 * rd, cb = __builtin_elementwise_fma(sg, c0 + v, tg) * rd;
-      const int o1 = ((ABL & 8) || !live) ? 0 : offc[ic + 1];
-      for (int o = ((ABL & 8) || !live) ? 0 : offc[ic]; o < o1; o += 4) {
-        const float4 xv = *reinterpret_cast<const float4*>(xlc + o);
-        sp += clamp_fma2(xv.x, ca, cb);
-        sp += clamp_fma2(xv.y, ca, cb);
-        sp += clamp_fma2(xv.z, ca, cb);
-        sp += clamp_fma2(xv.w, ca, cb);
+      if (o < o1) {
+        const float4 xa = *reinterpret_cast<const float4*>(xl + o);
+        sp += clamp_fma2(xa.x, ca, cb);
+        sp += clamp_fma2(xa.y, ca, cb);
+        sp += clamp_fma2(xa.z, ca, cb);
+        sp += clamp_fma2(xa.w, ca, cb);
       }
-    }
+    };
+    xsum(xlr, ((ABL & 4) || !live) ? 0 : offr[ic], ((ABL & 4) || !live) ? 0 : offr[ic + 1],
+         sg * w1 * rd, __builtin_elementwise_fma(sg, u, tg) * rd);
+    xsum(xlc, ((ABL & 8) || !live) ? 0 : offc[ic], ((ABL & 8) || !live) ? 0 : offc[ic + 1],
+         sg * w0 * rd, __builtin_elementwise_fma(sg, c0 + v, tg) * rd);
     sp *= dd;
     if (live && kp < EG_L) {
       const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
@@ -1221,7 +1226,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // fit, else read from the prepared buffer in HBM through the same (generic) pointer
   const int xwords = (int)pp[PL.xoffc + Ne];
   const bool lfit = xwords <= L.Uwords - NE4 * HS;
-  const float* xlist = lfit ? U + NE4 * HS : reinterpret_cast<const float*>(pp + PL.xl);
+  const float* xlistg = reinterpret_cast<const float*>(pp + PL.xl);
   float l2 = 0.f;
   for (int i = t; i < NP; i += NT_MID) {
     const float w = Wg[i];
@@ -1281,8 +1286,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // split mode: each block of the pair takes its half of the nodes through E1 -> M3 (and
   // E2); P, E_bar and h rows are parked write-through for the partner's redundant phases
   const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
-  entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlist, xlist, nlo, nhi, Ps, EG, rq,
-             SPLIT);
+  if (lfit)        // two inlined copies: the staged lists are read as LDS, not flat
+    entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, U + NE4 * HS, U + NE4 * HS, nlo,
+               nhi, Ps, EG, rq, SPLIT);
+  else
+    entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG,
+               rq, SPLIT);
   __syncthreads();
   MID_STAMP();
 
@@ -1973,13 +1982,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // slot (dead after dW5) when they fit; offc <- the compact row CSR (degrees)
   const int rl = (int)pp[PL.xoffc];                 // padded row-list length (multiple of 4)
   const bool rfit = rl / 4 + rl <= NE4 * HS;
-  const uint8_t* idl2 = rfit ? reinterpret_cast<const uint8_t*>(Ps)
-                             : reinterpret_cast<const uint8_t*>(pp + PL.lists);
-  const float* xl2 = rfit ? Ps + ((rl / 4 + 3) & ~3) : reinterpret_cast<const float*>(pp + PL.xl);
+  const int xl2o = (rl / 4 + 3) & ~3;              // staged x values after the ids
   if (rfit) {
     for (int w = t; w < rl / 4; w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
     for (int w = 4 * t; w < rl; w += 4 * NT_MID)
-      *reinterpret_cast<float4*>(Ps + ((rl / 4 + 3) & ~3) + w) =
+      *reinterpret_cast<float4*>(Ps + xl2o + w) =
           *reinterpret_cast<const float4*>(pp + PL.xl + w);
   }
   for (int i = t; i <= Ne; i += NT_MID) offc[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
@@ -2014,8 +2021,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc, idl2, xl2, nlo, nhi,
-             red2);
+  if (rfit)
+    entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc,
+               reinterpret_cast<const uint8_t*>(Ps), Ps + xl2o, nlo, nhi, red2);
+  else
+    entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc,
+               reinterpret_cast<const uint8_t*>(pp + PL.lists),
+               reinterpret_cast<const float*>(pp + PL.xl), nlo, nhi, red2);
   __syncthreads();
   if (t < 4 * HS) {
     const int w = t / HS, k = t - w * HS;
