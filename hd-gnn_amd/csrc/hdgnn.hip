@@ -856,7 +856,7 @@ constexpr int EG_L = HS / 2, EG_N = 6;
 // ABL: ablation bits for the microbenchmark (1 = skip search, 2 = skip dense sums,
 // 4 = skip row bits, 8 = skip column bits); 0 in the engine.
 template <int ABL = 0>
-__device__ __forceinline__ void entity_fwd(const int lane, const int wv, const float* Ws,
+__device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
                                            const float* xs, const float* xu, const int* cum,
                                            const double* pxd, const int nd,
                                            const int* offr, const int* offc,
@@ -865,13 +865,16 @@ __device__ __forceinline__ void entity_fwd(const int lane, const int wv, const f
                                            float* __restrict__ EG, uint16_t* __restrict__ rq,
                                            const bool wt = false) {
 #pragma clang fp contract(off)
-  const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
+  // block-wide lane map (no cross-lane traffic left in E1): thread t takes node group
+  // sub = t / 10 (102 nodes per pass), hidden units (2 kp, 2 kp + 1), kp = t % 10
+  const int sub = t / EG_L, kp = t - sub * EG_L, k0 = 2 * kp;
   const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
   const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f}, ca[2] = {ea.w0 >= 0.f, eb.w0 >= 0.f};
-  for (int base = n0 + EG_N * wv; base < n1; base += EG_N * (NT_MID / 64)) {   // wave-uniform
+  constexpr int NG = NT_MID / EG_L;                // 102 node groups per pass
+  for (int base = n0; base < n1; base += NG) {       // block-uniform
     const int i = base + sub;
-    const bool live = sub < EG_N && i < n1;
+    const bool live = sub < NG && i < n1;
     const int ic = live ? i : 0;
     const float xi = xs[ic];
     const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
@@ -1287,11 +1290,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // E2); P, E_bar and h rows are parked write-through for the partner's redundant phases
   const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
   if (lfit)        // two inlined copies: the staged lists are read as LDS, not flat
-    entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, U + NE4 * HS, U + NE4 * HS, nlo,
-               nhi, Ps, EG, rq, SPLIT);
+    entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, U + NE4 * HS, U + NE4 * HS, nlo, nhi, Ps,
+               EG, rq, SPLIT);
   else
-    entity_fwd(lane, wv, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG,
-               rq, SPLIT);
+    entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG, rq,
+               SPLIT);
   __syncthreads();
   MID_STAMP();
 

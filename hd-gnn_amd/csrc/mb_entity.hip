@@ -33,7 +33,7 @@ __global__ __launch_bounds__(1024) void mb_e1(int Ne, int iters, float* out, flo
   }
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
-    entity_fwd<ABL>(t & 63, t >> 6, Ws, xs, xu, cum, pxd, 10, offr, offc, lr, lc, Ne, Ps,
+    entity_fwd<ABL>(t, Ws, xs, xu, cum, pxd, 10, offr, offc, lr, lc, 0, Ne, Ps,
                     EG + (size_t)b * Ne * HS, rq + (size_t)b * Ne * HS);
     __syncthreads();
   }
