@@ -2053,33 +2053,38 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 }
 
 // ------------------------------------------------------------------------------
-// deterministic reduction of per-commit partial rows: a 1024-thread block takes 64
-// parameters x 16 commit phases (commit b -> phase b % 16, fixed order), then a fixed
-// 16-way combine.  Bitwise reproducible.
+// deterministic reduction of the partial rows (one per block of k_commit_step): a
+// 1024-thread block takes RED_P = 16 parameters x 64 row phases (row r -> phase r % 64,
+// fixed order); a thread's <= 4 rows per trip are loaded before they are added (one
+// memory round trip up to 256 rows), the 4 phases of a wave close with two permlane
+// swaps, the 16 waves in a fixed-order LDS sum.  Bitwise reproducible.
 // ------------------------------------------------------------------------------
-constexpr int RED_PH = 16;
+constexpr int RED_P = 16, RED_PH = NT_MID / RED_P;   // 16 parameters x 64 phases
 
-__device__ __forceinline__ float reduce_commits(const float* __restrict__ part, int B, int p,
-                                                bool valid, float (*sh)[64]) {
-  const int pl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+__device__ __forceinline__ float reduce_commits(const float* __restrict__ part, int R, int p,
+                                                bool valid, float (*sh)[RED_P]) {
+  const int pl = threadIdx.x & (RED_P - 1), ph = threadIdx.x / RED_P;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float acc = 0.f;
   if (valid) {
-    int b = ph;
-    for (; b + 3 * RED_PH < B; b += 4 * RED_PH) {
-      const float v0 = part[(size_t)b * NPART + p];
-      const float v1 = part[(size_t)(b + RED_PH) * NPART + p];
-      const float v2 = part[(size_t)(b + 2 * RED_PH) * NPART + p];
-      const float v3 = part[(size_t)(b + 3 * RED_PH) * NPART + p];
-      acc += v0; acc += v1; acc += v2; acc += v3;
+    for (int b0 = ph; b0 < R; b0 += 4 * RED_PH) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = b0 + u * RED_PH;
+        v[u] = b < R ? part[(size_t)b * NPART + p] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += v[u];
     }
-    for (; b < B; b += RED_PH) acc += part[(size_t)b * NPART + p];
   }
-  sh[ph][pl] = acc;
+  acc = xrow_sum4(acc);                 // the wave's 4 phases (lanes pl, pl+16, +32, +48)
+  if (lane < RED_P) sh[wv][pl] = acc;
   __syncthreads();
   float g = 0.f;
-  if (ph == 0) {
+  if (threadIdx.x < RED_P) {
 #pragma unroll
-    for (int q = 0; q < RED_PH; ++q) g += sh[q][pl];
+    for (int q = 0; q < NT_MID / 64; ++q) g += sh[q][pl];
   }
   return g;
 }
@@ -2087,10 +2092,10 @@ __device__ __forceinline__ float reduce_commits(const float* __restrict__ part, 
 __global__ __launch_bounds__(1024) void k_grad_reduce(const float* __restrict__ part, int B,
                                                       int p_begin, int p_end,
                                                       float* __restrict__ out) {
-  __shared__ float sh[RED_PH][64];
-  const int p = p_begin + blockIdx.x * 64 + (threadIdx.x & 63);
+  __shared__ float sh[NT_MID / 64][RED_P];
+  const int p = p_begin + blockIdx.x * RED_P + (threadIdx.x & (RED_P - 1));
   const float g = reduce_commits(part, B, p, p < p_end, sh);
-  if ((threadIdx.x >> 6) == 0 && p < p_end) out[p - p_begin] = g;
+  if (threadIdx.x < RED_P && p < p_end) out[p - p_begin] = g;
 }
 
 // Single-process training step tail: the reduction above fused with TF1 Adam for the
@@ -2106,14 +2111,14 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
                                                       float inv_pairs, float* __restrict__ stats,
                                                       float* __restrict__ grad) {
   using namespace m2;
-  __shared__ float sh[RED_PH][64];
-  const int p = blockIdx.x * 64 + (threadIdx.x & 63);
-  const bool upd = (threadIdx.x >> 6) == 0 && p < NP;
+  __shared__ float sh[NT_MID / 64][RED_P];
+  const int p = blockIdx.x * RED_P + (threadIdx.x & (RED_P - 1));
+  const bool upd = threadIdx.x < RED_P && p < NP;
   // the update's operands are fetched before the reduction so both latencies overlap
   const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
   const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
   const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh);
-  if ((threadIdx.x >> 6) != 0) return;
+  if (threadIdx.x >= RED_P) return;
   if (p < GRAD_LEN) grad[p] = g;
   if (p == NP) {
     const float ce = g * inv_pairs;
@@ -2468,7 +2473,7 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
                               out ? out->logits : nullptr, 10.f / pair_count(s), nullptr, st,
                               split));
   HIP_TRY(mark(1));
-  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st,
+  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
                      ws + w.part, part_rows(s, split), 0, GRAD_LEN, grad);
   HIP_TRY(hipGetLastError());
   HIP_TRY(mark(2));
@@ -2529,7 +2534,7 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
   HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, out ? out->probs : nullptr,
                               out ? out->logits : nullptr, 10.f / pairs, nullptr, st, split,
                               state->beta_pow));
-  hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + 63) / 64), dim3(1024), 0, st, ws + w.part,
+  hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st, ws + w.part,
                      part_rows(s, split), state->params, state->adam_m, state->adam_v, state->beta_pow,
                      ws + w.aux, lr, 1.f / pairs, out ? out->stats : nullptr, grad);
   HIP_TRY(hipGetLastError());

@@ -1,7 +1,7 @@
 # GPU box: fused-path parity (split + one-block), then bench both modes and phase stamps.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/split_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/split_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/split_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --no-cpu > gpurun_out/bench_split.log 2>&1 || exit $?
 HDG_FUSED_SPLIT=0 timeout -k 10 300 python bench.py --no-cpu > gpurun_out/bench_one.log 2>&1 || exit $?
