@@ -202,13 +202,26 @@ def main():
         if (tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne
                 and tj.get("nc") == nc and fused):
             traffic = tj.get("bytes_per_launch")
+    executed = None              # executed-instruction view (SQ counters, tools/valu_issue.py)
+    vj = os.path.join(ROOT, "profiles", "r01", "valu_issue.json")
+    if fused and (ne, nc, B) == (200, 74, 100) and os.path.exists(vj):
+        with open(vj) as f:
+            ev = json.load(f)
+        executed = {"valu_wave_insts_per_launch": ev.get("sq_insts_valu_per_launch"),
+                    "issue_frac_chip": round(ev.get("issue_frac_chip", 0.0), 4),
+                    "issue_frac_busy_cus": round(ev.get("issue_frac_busy_cus", 0.0), 4),
+                    "source": "profiles/r01/valu_issue.json (rocprofv3 SQ_INSTS_VALU over the "
+                              "kernel's rocprof duration; 4 cycles per wave64 VALU op per SIMD)"}
     roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic, "kernel": dom,
                 "flops_per_launch": flops_launch, "avg_launch_ms": round(kern_ms[dom], 5),
                 "algorithmic_bytes_per_launch": hbm_bytes_per_commit(ne, nc) * B,
                 "note": "SURVEY 8(d) dense-graph FLOPs (3 F_fwd per commit) over the measured "
-                        "%s time; the engine executes fewer ops (DESIGN.md 3)" % dom}
+                        "%s time: work-equivalent, can exceed 1 because the sorted-x / "
+                        "per-node algebra (DESIGN.md 3) does not execute most of them; "
+                        "'executed' is the hardware view (VALU issue-slot utilisation)" % dom,
+                "executed": executed}
     cpu = None
     if world == 1 and not args.no_cpu and v == 2:
         threads = min(16, os.cpu_count() or 1)

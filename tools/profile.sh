@@ -13,4 +13,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch -o run -- 
     python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $OUT/bench_fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write -o run -- \
     python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $OUT/bench_write.log 2>&1 || exit $?
-# summarise locally afterwards: python tools/prof_summary.py gpurun_out/prof_$TAG $TAG
+bash $R/tools/pmc_sq.sh || exit $?
+# summarise locally afterwards: python tools/prof_summary.py gpurun_out/prof_$TAG $TAG; python tools/valu_issue.py gpurun_out/pmc_sq gpurun_out/prof_$TAG $TAG 200
