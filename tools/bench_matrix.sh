@@ -10,6 +10,8 @@ run() {   # run <tag> <bench args...>
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 }
 run m2_fused_glide
+run_env() { local v=$1; shift; HDG_FUSED_SPLIT=$v run "$@"; }
+run_env 0 m2_fused_glide_oneblock
 run m2_general_glide --path 2
 run m1_glide --variant 1
 run m3_glide --variant 3
