@@ -98,6 +98,13 @@ int         hdg_param_count(int32_t variant);
  * argmax prediction equals the label, the numerator of EvaluationFuncs.top_ACC with
  * np.argmax's tie rule, exact); all-reduce the whole buffer.                       */
 int         hdg_grad_len(int32_t variant);
+/* Scratch the library carves per call (parked node rows, partial gradient rows, the
+ * block-pair inboxes of the fused path's split mode).  Allocate it zeroed once and keep
+ * it per shape: the inboxes are (value, tag) words that every completed call leaves
+ * zero, and a stale word equal to a live tag (0xC0DE0001..4 in its high half) would be
+ * taken as the partner's data.  Any other content is overwritten before it is read.
+ * Split mode (two blocks per commit) runs whenever 2 * batch <= the device's CU count;
+ * the environment variable HDG_FUSED_SPLIT=0 forces one block per commit.            */
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
 /* bytes of batch->prep for this shape (0 on a shape error) */
 size_t      hdg_prep_bytes(const hdg_shape* shape);
@@ -118,7 +125,8 @@ int hdg_fwd_bwd_events(const hdg_shape* shape, const hdg_batch* batch, const flo
                        void* const* events);
 
 /* Diagnostic: run k_commit_step alone with s_memrealtime (100 MHz) stamps at every
- * phase barrier, stamps[B][32] (device).  Overwrites the workspace.                 */
+ * phase barrier, stamps[2B][32] (device; row = the block's partial-gradient row, 2b + h
+ * in split mode).  Overwrites the workspace.                                        */
 int hdg_debug_step_stamps(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                          void* workspace, unsigned long long* stamps, void* stream);
 
