@@ -231,6 +231,12 @@ __device__ __forceinline__ void pair_tile(
   constexpr int NW = (SMAX + 1) / 2;
   constexpr int KP = KK / 2, KT = KK & 1;      // packed fp32 pairs (v_pk_*) + odd tail
   const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
+  // hidden units of the chunk [k0, k0 + KK): the packed pairs start at the even unit kpb
+  // (k0 or k0 + 1), so every pair is one 8-byte-aligned LDS read at an immediate offset
+  // from a per-thread base; the unit left over is the tail ktl
+  const int kpb = k0 + (k0 & 1);
+  const int ktl = (k0 & 1) ? k0 : k0 + KK - 1;
+  auto kof = [&](const int k) { return k < 2 * KP ? kpb + k : ktl; };   // local -> unit
   const int nown = (N - radd + rmul - 1) / rmul;   // rows i = rmul r + radd < N
   const int S = (nown + 15) >> 4;
   const p2 z2 = {0.f, 0.f};
@@ -244,11 +250,11 @@ __device__ __forceinline__ void pair_tile(
     cacct[c] = 0.f;
   }
   p2 yacc2[KP > 0 ? KP : 1], dk2[KP > 0 ? KP : 1];
-  float yacct = 0.f, dkt = KT ? dl[k0 + KK - 1] : 0.f;
+  float yacct = 0.f, dkt = KT ? dl[ktl] : 0.f;
 #pragma unroll
   for (int p = 0; p < KP; ++p) {
     yacc2[p] = z2;
-    dk2[p] = (p2){dl[k0 + 2 * p], dl[k0 + 2 * p + 1]};
+    dk2[p] = *reinterpret_cast<const p2*>(dl + kpb + 2 * p);
   }
 
   for (int s = 0; s < S; ++s) {
@@ -259,22 +265,22 @@ __device__ __forceinline__ void pair_tile(
     // rows past the sweep read row 0 and are selected to A = -inf, w = 0 (e = 0): the
     // sweep may run past the padded buffer when the rows are split by parity
     const int ib = iv ? i : 0;
-    const float* Ai = A + ib * LD + k0;
+    const float* Ai = A + ib * LD;
     const float ninf = -INFINITY;
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      const p2 av = {Ai[2 * p], Ai[2 * p + 1]};
+      const p2 av = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p);
       a2[p] = iv ? av : (p2){ninf, ninf};
       if constexpr (MODE == 1) {
-        const p2 wv2 = {wr[ib * LD + k0 + 2 * p], wr[ib * LD + k0 + 2 * p + 1]};
+        const p2 wv2 = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p);
         rw2[p] = iv ? wv2 : z2;
       } else {
         rw2[p] = z2;
       }
       racc2[p] = z2;
     }
-    const float at = KT ? (iv ? Ai[KK - 1] : ninf) : 0.f;
-    const float rwt = (MODE == 1 && KT) ? (iv ? wr[ib * LD + k0 + KK - 1] : 0.f) : 0.f;
+    const float at = KT ? (iv ? Ai[ktl] : ninf) : 0.f;
+    const float rwt = (MODE == 1 && KT) ? (iv ? wr[ib * LD + ktl] : 0.f) : 0.f;
     float racct = 0.f;
     uint32_t wrow[NW];
 #pragma unroll
@@ -293,10 +299,10 @@ __device__ __forceinline__ void pair_tile(
         const float gl = gam[ic * gld + jc];
         g = (iv && j < N && j != i) ? gl : 0.f;
       }
-      const float* Bj = Bv + j * LD + k0;
+      const float* Bj = Bv + j * LD;
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
-        const p2 bb = {Bj[2 * p], Bj[2 * p + 1]};
+        const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
         p2 e;
         if constexpr (MODE == 0) {
@@ -304,7 +310,7 @@ __device__ __forceinline__ void pair_tile(
         } else {
           p2 w;
           if constexpr (MODE == 1) {
-            w = rw2[p] + (p2){wc[j * LD + k0 + 2 * p], wc[j * LD + k0 + 2 * p + 1]};
+            w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
           } else {
             w = (p2){g, g};
           }
@@ -315,12 +321,12 @@ __device__ __forceinline__ void pair_tile(
         cacc2[c][p] += e;
       }
       if constexpr (KT) {
-        const float z = at + fmaf(af, dkt, Bj[KK - 1]);
+        const float z = at + fmaf(af, dkt, Bj[ktl]);
         float e;
         if constexpr (MODE == 0) {
           e = reluf(z);
         } else {
-          const float w = (MODE == 1) ? (rwt + wc[j * LD + k0 + KK - 1]) : g;
+          const float w = (MODE == 1) ? (rwt + wc[j * LD + ktl]) : g;
           e = (z > 0.f) ? w : 0.f;
           yacct = fmaf(af, e, yacct);
         }
@@ -338,7 +344,7 @@ __device__ __forceinline__ void pair_tile(
     if constexpr (!(ABL & 2)) row16_sums(rs);
     if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
 #pragma unroll
-      for (int k = 0; k < KK; ++k) Rout[i * LD + k0 + k] = rs[k];
+      for (int k = 0; k < KK; ++k) Rout[i * LD + kof(k)] = rs[k];
     }
   }
   float cacc[SMAX][KK], yacc[KK];
@@ -378,10 +384,10 @@ __device__ __forceinline__ void pair_tile(
   for (int e = t; e < NP16 * KK; e += 256) {
     const int j = e / KK, k = e - j * KK;
     const float v = cred[e] + cred[e + NP16 * KK] + cred[e + 2 * NP16 * KK] + cred[e + 3 * NP16 * KK];
-    if (j < N) Cout[j * LD + k0 + k] = v;
+    if (j < N) Cout[j * LD + kof(k)] = v;
   }
   if constexpr (MODE != 0) {
-    if (t < KK) ysum[k0 + t] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
+    if (t < KK) ysum[kof(t)] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
   }
   __syncthreads();
 }
