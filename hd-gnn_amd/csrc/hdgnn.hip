@@ -451,15 +451,6 @@ __device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) 
 
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
 
-// write-through stores / L2-bypassing loads of rows a partner block reads (parked rows)
-__device__ __forceinline__ void st_wt(float* p, const float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float2 ld_wt2(const float* p) {   // system-scope atomic: sc0 sc1
-  const unsigned long long w = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return make_float2(__uint_as_float((uint32_t)w), __uint_as_float((uint32_t)(w >> 32)));
-}
 
 
 
@@ -868,8 +859,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
                                            const int* offr, const int* offc,
                                            const float* xlr, const float* xlc,
                                            const int n0, const int n1, float* Ps,
-                                           float* __restrict__ EG, uint16_t* __restrict__ rq,
-                                           const bool wt = false) {
+                                           float* __restrict__ EG, uint16_t* __restrict__ rq) {
 #pragma clang fp contract(off)
   // block-wide lane map (no cross-lane traffic left in E1): thread t takes node group
   // sub = t / 10 (102 nodes per pass), hidden units (2 kp, 2 kp + 1), kp = t % 10
@@ -955,12 +945,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
     if (live && kp < EG_L) {
       const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
       *reinterpret_cast<float2*>(Ps + i * HS + k0) = P;
-      if (wt) {                          // parked for the partner block (split mode)
-        st_wt(EG + i * HS + k0, P.x);
-        st_wt(EG + i * HS + k0 + 1, P.y);
-      } else {
-        *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
-      }
+      *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
       rq[i * HS + k0] = (uint16_t)br[0];
       rq[i * HS + k0 + 1] = (uint16_t)br[1];
     }
@@ -1086,6 +1071,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
 // ------------------------------------------------------------------------------
 constexpr uint32_t XTAG = 0xC0DE0000u;          // + slot + 1; no NaN/Inf/huge fill pattern
 constexpr int XSLOTS = 4;                       // H, D_tau, dn partials; n partial + o rows
+constexpr int XRHO = 256 * HS / 2;              // + the rho rows of a node half (Ne <= 256)
 constexpr unsigned long long XWAIT = 2000000ull;   // s_memrealtime ticks (100 MHz) = 20 ms
 typedef uint32_t xu4 __attribute__((ext_vector_type(4)));
 
@@ -1108,6 +1094,7 @@ __device__ __forceinline__ void pair_send(const float* v, const int n, xu4* __re
     xstore(out + e, (xu4){__float_as_uint(v[2 * e]), tag, __float_as_uint(v[2 * e + 1]), tag});
 }
 
+template <bool ADD = true>
 __device__ __forceinline__ bool pair_recv_add(float* v, const int n, xu4* __restrict__ in,
                                               const uint32_t tag, const int t) {
   bool late = false;
@@ -1118,8 +1105,13 @@ __device__ __forceinline__ bool pair_recv_add(float* v, const int n, xu4* __rest
       if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT) { late = true; break; }
       w = xload(in + e);
     }
-    v[2 * e] += __uint_as_float(w.x);
-    v[2 * e + 1] += __uint_as_float(w.z);
+    if (ADD) {
+      v[2 * e] += __uint_as_float(w.x);
+      v[2 * e + 1] += __uint_as_float(w.z);
+    } else {                                 // the partner's own rows: taken as they are
+      v[2 * e] = __uint_as_float(w.x);
+      v[2 * e + 1] = __uint_as_float(w.z);
+    }
     xstore(in + e, (xu4){0u, 0u, 0u, 0u});
   }
   __syncthreads();
@@ -1154,11 +1146,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if (b >= B) return;                                // (uniform; the grid is exact)
   const int rmul = SPLIT ? 2 : 1, radd = h;          // own hunk rows p = rmul r + radd
   const int prow = SPLIT ? 2 * b + h : b;            // this block's partial-gradient row
-  const bool redund = SPLIT && h == 1;               // redundant phases: h = 0 writes grads
   bool xlate = false;
   constexpr int XS = 16 * SMAXC * HS / 2;            // 16-byte words per inbox slot
-  xu4* xin = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + h) * XSLOTS * XS : nullptr;
-  xu4* xout = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + 1 - h) * XSLOTS * XS : nullptr;
+  constexpr int XB = XSLOTS * XS + XRHO;             // per block inbox
+  xu4* xin = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + h) * XB : nullptr;
+  xu4* xout = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + 1 - h) * XB : nullptr;
   // Thread ids are re-derived from an opaque copy of threadIdx.x at every phase
   // boundary (PHASE()), so the compiler cannot keep addresses derived from them live
   // across phases: this kernel runs at the 128-VGPR ceiling of 1024-thread blocks.
@@ -1292,15 +1284,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   i of a and of a^T); the diagonal is removed once.  Lane map: a wave takes 3 nodes,
   //   lane = (node sub, hidden unit k), so the 20 lanes of a node walk its bits together.
   //   The row-set boundaries are kept for the backward.
-  // split mode: each block of the pair takes its half of the nodes through E1 -> M3 (and
-  // E2); P, E_bar and h rows are parked write-through for the partner's redundant phases
+  // split mode: each block of the pair takes its half of the nodes through E1 -> M3 and
+  // M11 -> E2; the P, E_bar and h rows it parks in the workspace are read back by itself
   const int nlo = SPLIT && h ? (Ne + 1) / 2 : 0, nhi = SPLIT && !h ? (Ne + 1) / 2 : Ne;
   if (lfit)        // two inlined copies: the staged lists are read as LDS, not flat
     entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, U + NE4 * HS, U + NE4 * HS, nlo, nhi, Ps,
-               EG, rq, SPLIT);
+               EG, rq);
   else
-    entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG, rq,
-               SPLIT);
+    entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG, rq);
   __syncthreads();
   MID_STAMP();
 
@@ -1308,7 +1299,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //   E_bar = P W5 + 2(Ne-1) b5          (agg_entity_B1, model_2.py:181-188)
   //   h = relu([x, E_bar] W1' + b1')     (mlp2_entity_B1, model_2.py:190-205)
   //   o = h w2' + b2',  x' = relu(o)
-  const int ntm_e = (Ne + 15) >> 4;
   for (int rb = (nlo >> 4) + wv; rb <= ((nhi - 1) >> 4); rb += NT_MID / 64) {   // wave-uniform
     const int row0 = rb * 16;
     const int ir = row0 + (lane & 15);                         // this lane's A row
@@ -1327,8 +1317,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           const int i = row0 + 4 * (lane >> 4) + q;
           if (i >= nlo && i < nhi) {
             Eb[i * HS + m] = c[q] + bias;
-            if (SPLIT) st_wt(EbG + i * HS + m, c[q] + bias);
-            else EbG[i * HS + m] = c[q] + bias;
+            EbG[i * HS + m] = c[q] + bias;
           }
         }
       }
@@ -1348,8 +1337,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           if (i >= nlo && i < nhi) {
             const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
             hE[i * HS + m] = v;
-            if (SPLIT) st_wt(hEG + i * HS + m, v);
-            else hEG[i * HS + m] = v;
+            hEG[i * HS + m] = v;
           }
         }
       }
@@ -1833,15 +1821,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   {
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
-    const int cq = (Nc + NG_MID - 1) / NG_MID;
-    const int cb0 = g * cq, cb1 = (cb0 + cq < Nc) ? cb0 + cq : Nc;
-    for (int I = tg; I < Ne; I += 256) {
+    // split mode: the own node half only, 8 hunk ranges x 128 nodes
+    constexpr int NGX = SPLIT ? 8 : NG_MID, TX = NT_MID / NGX;
+    const int gx = t / TX, tx = t - gx * TX;
+    const int cq = (Nc + NGX - 1) / NGX;
+    const int cb0 = gx * cq, cb1 = (cb0 + cq < Nc) ? cb0 + cq : Nc;
+    for (int I = nlo + tx; I < nhi; I += TX) {
       float a0 = 0.f, a1 = 0.f;
       for (int c = cb0; c < cb1; ++c) {
         a0 = fmaf(dnb[2 * c], (float)ks[(size_t)c * Ne + I], a0);
         a1 = fmaf(dnb[2 * c + 1], (float)kt[(size_t)c * Ne + I], a1);
       }
-      dxpart[g * NE4 + I] = a0 + a1;
+      dxpart[gx * NE4 + I] = a0 + a1;
     }
   }
   __syncthreads();
@@ -1856,8 +1847,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* hB = U + rho_off;                          // h, overwritten by rho row block by row block
   float* rho = hB;
   float* dw2p = Xm;                                 // [row block][21] partial dw2', db2'
-  for (int i = t; i < Ne; i += NT_MID) {
-    const float d = (dxpart[i] + dxpart[NE4 + i]) + (dxpart[2 * NE4 + i] + dxpart[3 * NE4 + i]);
+  for (int i = nlo + t; i < nhi; i += NT_MID) {
+    float d = (dxpart[i] + dxpart[NE4 + i]) + (dxpart[2 * NE4 + i] + dxpart[3 * NE4 + i]);
+    if constexpr (SPLIT)
+      d += (dxpart[4 * NE4 + i] + dxpart[5 * NE4 + i]) + (dxpart[6 * NE4 + i] + dxpart[7 * NE4 + i]);
     dxp[i] = (os[i] > 0.f) ? d : 0.f;               // d o_i (x' = relu(o))
   }
   {
@@ -1867,39 +1860,33 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     float4* d0 = reinterpret_cast<float4*>(Ps);
     float4* d1 = reinterpret_cast<float4*>(Eb);
     float4* d2 = reinterpret_cast<float4*>(hB);
-    if constexpr (SPLIT) {        // half the rows were parked write-through by the partner
-      float2* e0 = reinterpret_cast<float2*>(Ps);
-      float2* e1 = reinterpret_cast<float2*>(Eb);
-      float2* e2 = reinterpret_cast<float2*>(hB);
-      for (int e = t; e < Ne * HS / 2; e += NT_MID) {
-        e0[e] = ld_wt2(EG + 2 * e);
-        e1[e] = ld_wt2(EbG + 2 * e);
-        e2[e] = ld_wt2(hEG + 2 * e);
-      }
-    } else {
-      for (int e = t; e < Ne * HS / 4; e += NT_MID) { d0[e] = s0[e]; d1[e] = s1[e]; d2[e] = s2[e]; }
+    // the own node half's rows (this block parked them: same L2, plain loads)
+    for (int e = nlo * HS / 4 + t; e < nhi * HS / 4; e += NT_MID) {
+      d0[e] = s0[e];
+      d1[e] = s1[e];
+      d2[e] = s2[e];
     }
   }
   __syncthreads();
   MID_STAMP();
   // row-local chain per 16-row block: dq = [h > 0] w2' do;  dE = dq W1'[1:]^T;
   // rho = dE W5^T (into h's rows, consumed first); partial dw2' / db2' of the block
-  for (int rb = wv; rb < ntm_e; rb += NT_MID / 64) {          // wave-uniform
+  for (int rb = (nlo >> 4) + wv; rb <= ((nhi - 1) >> 4); rb += NT_MID / 64) {   // wave-uniform
     const int row0 = rb * 16;
     for (int e = lane; e < 16 * HS; e += 64) {
       const int i = row0 + e / HS, k = e - (e / HS) * HS;
-      if (i < Ne) dq[i * HS + k] = (hB[i * HS + k] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
+      if (i >= nlo && i < nhi) dq[i * HS + k] = (hB[i * HS + k] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
     }
     if (lane <= HS) {
       float acc = 0.f;
       for (int r = 0; r < 16; ++r) {
         const int i = row0 + r;
-        if (i < Ne) acc = fmaf(lane < HS ? hB[i * HS + lane] : 1.f, dxp[i], acc);
+        if (i >= nlo && i < nhi) acc = fmaf(lane < HS ? hB[i * HS + lane] : 1.f, dxp[i], acc);
       }
       dw2p[rb * 21 + lane] = acc;
     }
     const int ir = row0 + (lane & 15);
-    const bool rv = ir < Ne;
+    const bool rv = ir >= nlo && ir < nhi;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int col0 = cb * 16;
@@ -1912,7 +1899,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) dE[i * HS + m] = c[q];
+          if (i >= nlo && i < nhi) dE[i * HS + m] = c[q];
         }
       }
     }
@@ -1927,52 +1914,61 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = row0 + 4 * (lane >> 4) + q;
-          if (i < Ne) rho[i * HS + m] = c[q];
+          if (i >= nlo && i < nhi) rho[i * HS + m] = c[q];
         }
       }
     }
   }
   __syncthreads();
+  if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, XTAG + 5, t);
   MID_STAMP();
   // ---- M13: reductions over rows: dW1' = [x, E_bar, 1]^T dq (waves 0-3),
-  //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8)
+  //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8);
+  //      split mode: over the own node half (partial gradients), the rho exchange overlaps
   if (wv < 4) {
     const int row0 = (wv >> 1) * 16, col0 = (wv & 1) * 16;
     const int lr = row0 + (lane & 15), kc = col0 + (lane & 15);
     const float* pa = lr == 0 ? xs : (lr <= HS ? Eb + lr - 1 : (lr == HS + 1 ? kone : kzero));
     const int sa = lr == 0 ? 1 : (lr <= HS ? HS : 0);
-    const f4v c = mfma_tile16_p(pa, sa, kc < HS ? dq + kc : kzero, kc < HS ? HS : 0, Ne, lane);
+    const f4v c = mfma_tile16_p(pa + nlo * sa, sa, kc < HS ? dq + kc + nlo * HS : kzero,
+                                kc < HS ? HS : 0, nhi - nlo, lane);
     const int k = col0 + (lane & 15);
     if (k < HS) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int l = row0 + 4 * (lane >> 4) + q;
-        if (l <= HS) pb[E3_W1 + l * HS + k] = redund ? 0.f : c[q];
-        else if (l == HS + 1) pb[E3_B1 + k] = redund ? 0.f : c[q];
+        if (l <= HS) pb[E3_W1 + l * HS + k] = c[q];
+        else if (l == HS + 1) pb[E3_B1 + k] = c[q];
       }
     }
   } else if (wv < 8) {
     const int row0 = ((wv - 4) >> 1) * 16, col0 = ((wv - 4) & 1) * 16;
     const int lr = row0 + (lane & 15), kc = col0 + (lane & 15);
-    const f4v c = mfma_tile16_p(lr < HS ? Ps + lr : (lr == HS ? kone : kzero), lr < HS ? HS : 0,
-                                kc < HS ? dE + kc : kzero, kc < HS ? HS : 0, Ne, lane);
+    const f4v c = mfma_tile16_p(lr < HS ? Ps + lr + nlo * HS : (lr == HS ? kone : kzero),
+                                lr < HS ? HS : 0, kc < HS ? dE + kc + nlo * HS : kzero,
+                                kc < HS ? HS : 0, nhi - nlo, lane);
     const int k = col0 + (lane & 15);
     if (k < HS) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int l = row0 + 4 * (lane >> 4) + q;
-        if (l < HS) pb[E1_W5 + l * HS + k] = redund ? 0.f : c[q];
-        else if (l == HS) pb[E1_B5 + k] = redund ? 0.f : twoNe1 * c[q];
+        if (l < HS) pb[E1_W5 + l * HS + k] = c[q];
+        else if (l == HS) pb[E1_B5 + k] = twoNe1 * c[q];
       }
     }
   } else if (wv == 8 && lane <= HS) {
     float acc = 0.f;
-    for (int rb = 0; rb < ntm_e; ++rb) acc += dw2p[rb * 21 + lane];
-    pb[lane < HS ? E3_W2 + lane : E3_B2] = redund ? 0.f : acc;
+    for (int rb = nlo >> 4; rb <= ((nhi - 1) >> 4); ++rb) acc += dw2p[rb * 21 + lane];
+    pb[lane < HS ? E3_W2 + lane : E3_B2] = acc;
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
   if (t < 3) pb[NP + 2 + t] = 0.f;                  // trailer / pad
-  __syncthreads();
+  if constexpr (SPLIT) {                             // the partner half's rho rows
+    const int plo = h ? 0 : (Ne + 1) / 2, phi = h ? (Ne + 1) / 2 : Ne;
+    xlate |= pair_recv_add<false>(rho + plo * HS, (phi - plo) * HS, xin + XSLOTS * XS, XTAG + 5, t);
+  } else {
+    __syncthreads();
+  }
   MID_STAMP();
 
   // ---- E2: mlp_entity_B1 first-layer backward -----------------------------------------
@@ -2237,7 +2233,7 @@ Work work_layout(const hdg_shape* s) {
   w.aux = take(8);
   // block-pair inboxes (split mode): [B][2 halves][XSLOTS][NC16*HS] u64 (value, tag) words;
   // zero at allocation, left zero by every completed launch
-  w.xch = take(2 * B * 2 * (size_t)XSLOTS * NC16 * HS);
+  w.xch = take(2 * B * 4 * ((size_t)XSLOTS * NC16 * HS / 2 + XRHO));
   w.total = o;
   return w;
 }
