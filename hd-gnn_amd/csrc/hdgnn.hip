@@ -1995,34 +1995,45 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           *reinterpret_cast<const float4*>(pp + PL.xl + w);
   }
   for (int i = t; i <= Ne; i += NT_MID) offc[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
-  for (int task = wv; task < 2 * HS; task += NT_MID / 64) {        // wave-uniform
-    const int k = task >> 1, which = task & 1;
-    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
-    float* T = (which ? Tx : Tr) + k * TL;
-    float run[4];
-    float r = 0.f;
+  for (int k = wv; k < HS; k += NT_MID / 64) {        // wave-uniform; both tables of unit k
+    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;      // from one gather of rho
+    float* T0 = Tr + k * TL;
+    float* T1 = Tx + k * TL;
+    float run0[4], run1[4];
+    float r0 = 0.f, r1 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int s = 4 * lane + q;                 // scan position
-      float val = 0.f;
+      float v0 = 0.f, v1 = 0.f;
       if (s < Ne) {
         const int m = suf ? Ne - 1 - s : s;
-        val = rho[perm[m] * HS + k];
-        if (which) val *= xsrt[m];
+        v0 = rho[perm[m] * HS + k];
+        v1 = v0 * xsrt[m];
       }
-      r += val;
-      run[q] = r;
+      r0 += v0;
+      r1 += v1;
+      run0[q] = r0;
+      run1[q] = r1;
     }
-    const float off = wave_incl_scan_dpp(r) - r;
+    const float off0 = wave_incl_scan_dpp(r0) - r0;
+    const float off1 = wave_incl_scan_dpp(r1) - r1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int s = 4 * lane + q;
       if (s < Ne) {
-        if (suf) T[Ne - 1 - s] = off + run[q];   // sum over sorted slots [m, Ne)
-        else T[s + 1] = off + run[q];            // sum over sorted slots [0, m)
+        if (suf) {                                  // sums over sorted slots [m, Ne)
+          T0[Ne - 1 - s] = off0 + run0[q];
+          T1[Ne - 1 - s] = off1 + run1[q];
+        } else {                                    // sums over sorted slots [0, m)
+          T0[s + 1] = off0 + run0[q];
+          T1[s + 1] = off1 + run1[q];
+        }
       }
     }
-    if (lane == 0) T[suf ? Ne : 0] = 0.f;
+    if (lane == 0) {
+      T0[suf ? Ne : 0] = 0.f;
+      T1[suf ? Ne : 0] = 0.f;
+    }
   }
   __syncthreads();
   MID_STAMP();
