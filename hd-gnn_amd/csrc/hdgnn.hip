@@ -824,6 +824,51 @@ __device__ __forceinline__ f4v mfma_tile16_p(const float* pa, const int sa, cons
   return c0 + c1;
 }
 
+// Two 16x16 tiles sharing the A rows (the two 16-column halves of a 20-wide output):
+// one A read per k step feeds both MFMAs, the two accumulation chains interleave.
+__device__ __forceinline__ void mfma_tile16x2_p(const float* pa, const int sa, const float* pb0,
+                                                const int sb0, const float* pb1, const int sb1,
+                                                const int K, const int lane, f4v& o0, f4v& o1) {
+  const int q = lane >> 4;
+  const float* a = pa + q * sa;
+  const float* b0 = pb0 + q * sb0;
+  const float* b1 = pb1 + q * sb1;
+  f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  int k = 0;
+  for (; k + 16 <= K; k += 16) {
+    float av[4], bv0[4], bv1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      av[u] = a[4 * u * sa];
+      bv0[u] = b0[4 * u * sb0];
+      bv1[u] = b1[4 * u * sb1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv0[u], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv1[u], c1, 0, 0, 0);
+    }
+    a += 16 * sa;
+    b0 += 16 * sb0;
+    b1 += 16 * sb1;
+  }
+  for (; k + 4 <= K; k += 4) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b1[0], c1, 0, 0, 0);
+    a += 4 * sa;
+    b0 += 4 * sb0;
+    b1 += 4 * sb1;
+  }
+  if (k < K) {                       // K % 4 tail, as in mfma_tile16_p
+    const bool ok = k + q < K;
+    const float av = ok ? a[0] : 0.f;
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ok ? b0[0] : 0.f, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ok ? b1[0] : 0.f, c1, 0, 0, 0);
+  }
+  o0 = c0;
+  o1 = c1;
+}
+
 // first layer of mlp_entity_B1 for hidden unit kk (model_2.py:165-170):
 //   W1^T [x_i, x_j, [a=0], [a=1]] + b1 = u_i + v_j + a_ij d,
 //   u = fma(x, W1[0], W1[2] + b1), v = x * W1[1], d = W1[3] - W1[2]
@@ -1303,41 +1348,49 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const int row0 = rb * 16;
     const int ir = row0 + (lane & 15);                         // this lane's A row
     const bool rv = ir >= nlo && ir < nhi;
+    {                                  // both 16-column halves, shared A reads
+      f4v cc[2];
+      const int m0 = lane & 15, m1 = 16 + (lane & 15);
+      mfma_tile16x2_p(rv ? Ps + ir * HS : kzero, rv ? 1 : 0, Ws + E1_W5 + m0, HS,
+                      m1 < HS ? Ws + E1_W5 + m1 : kzero, m1 < HS ? HS : 0, HS, lane, cc[0], cc[1]);
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int col0 = cb * 16;
-      const int mc = col0 + (lane & 15);                       // this lane's B column
-      const f4v c = mfma_tile16_p(rv ? Ps + ir * HS : kzero, rv ? 1 : 0,
-                                  mc < HS ? Ws + E1_W5 + mc : kzero, mc < HS ? HS : 0, HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
-        const float bias = twoNe1 * Ws[E1_B5 + m];
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col0 = cb * 16;
+        const f4v c = cc[cb];
+        const int m = col0 + (lane & 15);
+        if (m < HS) {
+          const float bias = twoNe1 * Ws[E1_B5 + m];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i >= nlo && i < nhi) {
-            Eb[i * HS + m] = c[q] + bias;
-            EbG[i * HS + m] = c[q] + bias;
+          for (int q = 0; q < 4; ++q) {
+            const int i = row0 + 4 * (lane >> 4) + q;
+            if (i >= nlo && i < nhi) {
+              Eb[i * HS + m] = c[q] + bias;
+              EbG[i * HS + m] = c[q] + bias;
+            }
           }
         }
       }
     }
+    {                                  // both 16-column halves, shared A reads
+      f4v cc[2];
+      const int m0 = lane & 15, m1 = 16 + (lane & 15);
+      mfma_tile16x2_p(rv ? Eb + ir * HS : kzero, rv ? 1 : 0, Ws + E3_W1 + HS + m0, HS,
+                      m1 < HS ? Ws + E3_W1 + HS + m1 : kzero, m1 < HS ? HS : 0, HS, lane, cc[0], cc[1]);
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {   // same wave: its E_bar rows are complete (LDS in order)
-      const int col0 = cb * 16;        // [x, E_bar] W1' = E_bar W1'[1:] (MFMA) + x W1'[0]
-      const int mc = col0 + (lane & 15);
-      const f4v c = mfma_tile16_p(rv ? Eb + ir * HS : kzero, rv ? 1 : 0,
-                                  mc < HS ? Ws + E3_W1 + HS + mc : kzero, mc < HS ? HS : 0, HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
-        const float bias = Ws[E3_B1 + m], w0 = Ws[E3_W1 + m];
+      for (int cb = 0; cb < 2; ++cb) {   // same wave: its E_bar rows are complete (LDS in order)
+        const int col0 = cb * 16;        // [x, E_bar] W1' = E_bar W1'[1:] (MFMA) + x W1'[0]
+        const f4v c = cc[cb];
+        const int m = col0 + (lane & 15);
+        if (m < HS) {
+          const float bias = Ws[E3_B1 + m], w0 = Ws[E3_W1 + m];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i >= nlo && i < nhi) {
-            const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
-            hE[i * HS + m] = v;
-            hEG[i * HS + m] = v;
+          for (int q = 0; q < 4; ++q) {
+            const int i = row0 + 4 * (lane >> 4) + q;
+            if (i >= nlo && i < nhi) {
+              const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
+              hE[i * HS + m] = v;
+              hEG[i * HS + m] = v;
+            }
           }
         }
       }
@@ -1887,34 +1940,41 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
     const int ir = row0 + (lane & 15);
     const bool rv = ir >= nlo && ir < nhi;
+    {                                  // both 16-column halves, shared A reads
+      f4v cc[2];
+      const int m0 = lane & 15, m1 = 16 + (lane & 15);
+      mfma_tile16x2_p(rv ? dq + ir * HS : kzero, rv ? 1 : 0, Ws + E3_W1 + (1 + m0) * HS, 1,
+                      m1 < HS ? Ws + E3_W1 + (1 + m1) * HS : kzero, m1 < HS ? 1 : 0, HS, lane, cc[0], cc[1]);
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int col0 = cb * 16;
-      const int mc = col0 + (lane & 15);
-      const f4v c = mfma_tile16_p(rv ? dq + ir * HS : kzero, rv ? 1 : 0,
-                                  mc < HS ? Ws + E3_W1 + (1 + mc) * HS : kzero, mc < HS ? 1 : 0,
-                                  HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col0 = cb * 16;
+        const f4v c = cc[cb];
+        const int m = col0 + (lane & 15);
+        if (m < HS) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i >= nlo && i < nhi) dE[i * HS + m] = c[q];
+          for (int q = 0; q < 4; ++q) {
+            const int i = row0 + 4 * (lane >> 4) + q;
+            if (i >= nlo && i < nhi) dE[i * HS + m] = c[q];
+          }
         }
       }
     }
+    {                                  // both 16-column halves, shared A reads
+      f4v cc[2];
+      const int m0 = lane & 15, m1 = 16 + (lane & 15);
+      mfma_tile16x2_p(rv ? dE + ir * HS : kzero, rv ? 1 : 0, Ws + E1_W5 + m0 * HS, 1,
+                      m1 < HS ? Ws + E1_W5 + m1 * HS : kzero, m1 < HS ? 1 : 0, HS, lane, cc[0], cc[1]);
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int col0 = cb * 16;
-      const int mc = col0 + (lane & 15);
-      const f4v c = mfma_tile16_p(rv ? dE + ir * HS : kzero, rv ? 1 : 0,
-                                  mc < HS ? Ws + E1_W5 + mc * HS : kzero, mc < HS ? 1 : 0, HS, lane);
-      const int m = col0 + (lane & 15);
-      if (m < HS) {
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col0 = cb * 16;
+        const f4v c = cc[cb];
+        const int m = col0 + (lane & 15);
+        if (m < HS) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = row0 + 4 * (lane >> 4) + q;
-          if (i >= nlo && i < nhi) rho[i * HS + m] = c[q];
+          for (int q = 0; q < 4; ++q) {
+            const int i = row0 + 4 * (lane >> 4) + q;
+            if (i >= nlo && i < nhi) rho[i * HS + m] = c[q];
+          }
         }
       }
     }
