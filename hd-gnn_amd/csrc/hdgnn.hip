@@ -1930,13 +1930,27 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const int i = row0 + e / HS, k = e - (e / HS) * HS;
       if (i >= nlo && i < nhi) dq[i * HS + k] = (hB[i * HS + k] > 0.f) ? Ws[E3_W2 + k] * dxp[i] : 0.f;
     }
-    if (lane <= HS) {
-      float acc = 0.f;
-      for (int r = 0; r < 16; ++r) {
-        const int i = row0 + r;
-        if (i >= nlo && i < nhi) acc = fmaf(lane < HS ? hB[i * HS + lane] : 1.f, dxp[i], acc);
+    {   // dw2' / db2' partials of the block: lane = (row r = lane / 4, units k = kq + 4 j)
+      const int r = lane >> 2, kq = lane & 3, i = row0 + r;
+      const bool ok = i >= nlo && i < nhi;
+      const float d = ok ? dxp[i] : 0.f;
+      float v[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int k = kq + 4 * j;
+        v[j] = (ok && k < HS) ? hB[i * HS + k] * d : (k == HS ? d : 0.f);
       }
-      dw2p[rb * 21 + lane] = acc;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {                 // sum over the 16 rows (lane bits 2..5)
+        v[j] += __shfl_xor(v[j], 4);
+        v[j] += __shfl_xor(v[j], 8);
+        v[j] = xrow_sum4(v[j]);
+      }
+      if (r == 0) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (kq + 4 * j <= HS) dw2p[rb * 21 + kq + 4 * j] = v[j];
+      }
     }
     const int ir = row0 + (lane & 15);
     const bool rv = ir >= nlo && ir < nhi;
