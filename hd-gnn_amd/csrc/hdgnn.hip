@@ -1265,7 +1265,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M0: stage weights, commit inputs, sorted-x tables and entity class bits --------
   float* Ps = U;
   float* Eb = U + NE4 * HS;
-  float* hE = U + 2 * NE4 * HS;
   // neighbour lists (u8 ids, rows | columns): staged behind P when they fit, else read
   // from the prepared buffer in HBM through the same (generic) pointer
   // neighbour x-lists (rows | columns, NaN-padded, k_prep_sort): staged behind P when they
@@ -1376,32 +1375,33 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const int m0 = lane & 15, m1 = 16 + (lane & 15);
       mfma_tile16x2_p(rv ? Eb + ir * HS : kzero, rv ? 1 : 0, Ws + E3_W1 + HS + m0, HS,
                       m1 < HS ? Ws + E3_W1 + HS + m1 : kzero, m1 < HS ? HS : 0, HS, lane, cc[0], cc[1]);
+      // h = relu(...) in the tile registers; o = h w2' + b2' as a 16-lane row sum of the
+      // lanes' h w2' products (no LDS round trip for h)
+      float ow[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {   // same wave: its E_bar rows are complete (LDS in order)
         const int col0 = cb * 16;        // [x, E_bar] W1' = E_bar W1'[1:] (MFMA) + x W1'[0]
         const f4v c = cc[cb];
         const int m = col0 + (lane & 15);
         if (m < HS) {
-          const float bias = Ws[E3_B1 + m], w0 = Ws[E3_W1 + m];
+          const float bias = Ws[E3_B1 + m], w0 = Ws[E3_W1 + m], w2 = Ws[E3_W2 + m];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int i = row0 + 4 * (lane >> 4) + q;
-            if (i >= nlo && i < nhi) {
-              const float v = reluf(fmaf(xs[i], w0, c[q]) + bias);
-              hE[i * HS + m] = v;
-              hEG[i * HS + m] = v;
-            }
+            const bool own = i >= nlo && i < nhi;
+            const float v = reluf(fmaf(xs[own ? i : nlo], w0, c[q]) + bias);
+            if (own) hEG[i * HS + m] = v;
+            ow[q] = fmaf(v, w2, ow[q]);
           }
         }
       }
-    }
-    if (lane < 16 && row0 + lane >= nlo && row0 + lane < nhi) {
-      const int i = row0 + lane;
-      float o = Ws[E3_B2];
-#pragma unroll
-      for (int k = 0; k < HS; ++k) o = fmaf(hE[i * HS + k], Ws[E3_W2 + k], o);
-      os[i] = o;
-      xps[i] = reluf(o);
+      row16_sums(ow);
+      const int q = lane & 15, i = row0 + 4 * (lane >> 4) + q;
+      if (q < 4 && i >= nlo && i < nhi) {
+        const float o = (q == 0 ? ow[0] : q == 1 ? ow[1] : q == 2 ? ow[2] : ow[3]) + Ws[E3_B2];
+        os[i] = o;
+        xps[i] = reluf(o);
+      }
     }
   }
   __syncthreads();
