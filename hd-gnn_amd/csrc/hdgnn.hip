@@ -1418,15 +1418,19 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     // own nodes only; the partial n and the own o rows go through one pair exchange.
     constexpr int QN = SPLIT ? 2 : 4;                 // Ne <= 256: a half is <= 128 nodes
     float* xsc = Ps;                                  // [2 Nc n partials | NE4 o rows]
-    for (int t0 = 4 * wv; t0 < 2 * Nc; t0 += 4 * (NT_MID / 64)) {   // wave-uniform
-      float kv[4][QN], xv[QN];
+    // a wave takes MT consecutive tasks (c, m) per trip: all MT * QN count loads are in
+    // flight before the products, and the MT wave sums close together (wave_sums)
+    constexpr int MT = 10;
+    float xv[QN];
 #pragma unroll
-      for (int q = 0; q < QN; ++q) {
-        const int I = nlo + lane + 64 * q;
-        xv[q] = I < nhi ? xps[I] : 0.f;
-      }
+    for (int q = 0; q < QN; ++q) {
+      const int I = nlo + lane + 64 * q;
+      xv[q] = I < nhi ? xps[I] : 0.f;
+    }
+    for (int t0 = MT * wv; t0 < 2 * Nc; t0 += MT * (NT_MID / 64)) {   // wave-uniform
+      float kv[MT][QN];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < MT; ++u) {
         const int task = t0 + u < 2 * Nc ? t0 + u : 2 * Nc - 1;
         const uint16_t* kr = ((task & 1) ? kt : ks) + (size_t)(task >> 1) * Ne;
 #pragma unroll
@@ -1435,18 +1439,20 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           kv[u][q] = (float)kr[I < nhi ? I : nlo];
         }
       }
+      float a[MT];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float a = 0.f;
+      for (int u = 0; u < MT; ++u) {
+        a[u] = 0.f;
 #pragma unroll
-        for (int q = 0; q < QN; ++q) a = fmaf(kv[u][q], xv[q], a);
-        const float v = wave_sum(a);
+        for (int q = 0; q < QN; ++q) a[u] = fmaf(kv[u][q], xv[q], a[u]);
+      }
+      wave_sums(a, lane, [&](int u, float v) {
         const int task = t0 + u;
-        if (lane == 0 && task < 2 * Nc) {
+        if (task < 2 * Nc) {
           if (SPLIT) xsc[task] = v;
           else nb[4 * (task >> 1) + (task & 1)] = v;
         }
-      }
+      });
     }
     for (int c = t; c < Nc; c += NT_MID) {
       nb[4 * c + 2] = ncst[2 * c];
