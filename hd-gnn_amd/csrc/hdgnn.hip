@@ -1594,9 +1594,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float4* u2 = reinterpret_cast<const float4*>(lds + L.u2);
     const float b0 = Ws[H2_B2], b1 = Ws[H2_B2 + 1];
     const int Pown = ((Nc - radd + rmul - 1) / rmul) * Nc1i;    // pairs of the own rows
+    // (row r, column slot qq) of pair el advance by a fixed step with one carry per trip
+    int r, qq;
+    divmod_bf(t, Nc1i, invNc1, r, qq);
+    const int dr = NT_MID / Nc1i, dqq = NT_MID - dr * Nc1i;
     for (int el = t; el < Pown; el += NT_MID) {
-      int r, qq;
-      divmod_bf(el, Nc1i, invNc1, r, qq);
       const int p = rmul * r + radd;
       const int e = SPLIT ? p * Nc1i + qq : el;
       const int q = qq + (qq >= p ? 1 : 0);
@@ -1607,7 +1609,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const float4* ep4 = reinterpret_cast<const float4*>(eps);
       const float ey = TAUE ? 0.f : yf;       // without tau+eps: add y*eps here
       typedef float p2 __attribute__((ext_vector_type(2)));
-      p2 zz = {b0, b1};                       // (z0, z1) += kappa_k (U2[k][0], U2[k][1])
+      p2 zz = {b0, b1}, zy = {0.f, 0.f};      // (z0, z1) += kappa_k (U2[k][0], U2[k][1]):
+                                              // two chains (even / odd hidden-unit pairs)
       float kap[HS];
 #pragma unroll
       for (int v = 0; v < HS / 4; ++v) {
@@ -1631,10 +1634,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           const float4 w = u2[2 * v + h];           // w0_k, w1_k, w0_k+1, w1_k+1
           zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h], kap[4 * v + 2 * h]},
                                          (p2){w.x, w.y}, zz);
-          zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h + 1], kap[4 * v + 2 * h + 1]},
-                                         (p2){w.z, w.w}, zz);
+          zy = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h + 1], kap[4 * v + 2 * h + 1]},
+                                         (p2){w.z, w.w}, zy);
         }
       }
+      zz += zy;
       const float z0 = zz.x, z1 = zz.y;
       const float mx = fmaxf(z0, z1);
       const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
@@ -1654,11 +1658,17 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 #pragma unroll
         for (int k = 0; k < HS; k += 2) {       // packed: two hidden units per v_pk_fma
           typedef float p2 __attribute__((ext_vector_type(2)));
-          const p2 r = __builtin_elementwise_fma((p2){kap[k], kap[k + 1]}, (p2){gmm, gmm},
-                                                 (p2){zacc[k], zacc[k + 1]});
-          zacc[k] = r.x;
-          zacc[k + 1] = r.y;
+          const p2 za = __builtin_elementwise_fma((p2){kap[k], kap[k + 1]}, (p2){gmm, gmm},
+                                                  (p2){zacc[k], zacc[k + 1]});
+          zacc[k] = za.x;
+          zacc[k + 1] = za.y;
         }
+      }
+      qq += dqq;                              // next pair of this thread
+      r += dr;
+      if (qq >= Nc1i) {
+        qq -= Nc1i;
+        ++r;
       }
     }
   }
