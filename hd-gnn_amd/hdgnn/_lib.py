@@ -51,7 +51,8 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    # HDG_LIB_PATH: an alternative build of the same library (diagnostic ablation builds)
+    path = path or os.environ.get("HDG_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError("libhdgnn.so is not built (%s); run __graft_entry__.build() or "
                            "python hd-gnn_amd/hdgnn/build.py" % path)
