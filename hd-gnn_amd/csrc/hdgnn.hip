@@ -206,7 +206,9 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 //   z_ij  = A[i] + B[j] + y_ij * dl          (y_ij = bit j of row i)
 //   MODE 0  e = relu(z)                                       (forward sums)
 //   MODE 1  e = [z > 0] * (wr[i] + wc[j])  , ysum += y*e      (backward, node weights)
-//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e                 (pair weights)
+//   MODE 2  e = [z > 0] * gam[i][j]        , ysum += y*e                 (pair weights;
+//           GFULL: gam (in LDS) finite on every swept row for j < 16 SMAX, 0 on the diagonal
+//           and for j >= N, read unmasked; else clamped reads, diagonal / padding masked)
 //   Rout[i] = sum_j e_ij   Cout[j] = sum_i e_ij   (diagonal INCLUDED for MODE 0/1:
 //   callers subtract it; MODE 2 masks it)
 // Rows swept: i = rmul * r + radd, r = 0, 1, ... while i < N (a block pair splits the rows
@@ -219,7 +221,7 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 template <int SMAX, int KK>
 constexpr int tile_cred_words() { return 4 * 16 * SMAX * KK + 8 * KK; }
 
-template <int KK, int SMAX, int MODE, int LD, int ABL = 0>
+template <int KK, int SMAX, int MODE, int LD, int ABL = 0, bool GFULL = false>
 __device__ __forceinline__ void pair_tile(
     const int N, const int t, const float* A, const float* Bv, const int k0,
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
@@ -294,7 +296,9 @@ __device__ __forceinline__ void pair_tile(
       const float af = (ABL & 1) ? 0.f : (float)((wrow[c >> 1] >> (tj + 16 * (c & 1))) & 1u);
       const p2 af2 = {af, af};
       float g = 0.f;
-      if constexpr (MODE == 2) {   // branch-free: clamped load, selected (not multiplied:
+      if constexpr (MODE == 2 && GFULL) {   // rows past the sweep read the first swept row
+        g = gam[(iv ? i : radd) * gld + j];  // (A = -inf zeroes their terms)
+      } else if constexpr (MODE == 2) {      // clamped load, selected (not multiplied:
         const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;   // garbage * 0 can be NaN)
         const float gl = gam[ic * gld + jc];
         g = (iv && j < N && j != i) ? gl : 0.f;
@@ -1598,6 +1602,14 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     int r, qq;
     divmod_bf(t, Nc1i, invNc1, r, qq);
     const int dr = NT_MID / Nc1i, dqq = NT_MID - dr * Nc1i;
+    const int npad = NC16 - Nc;
+    if (TRAIN && GAML && npad > 0) {   // gamma's padding columns [Nc, NC16) of the own rows:
+                                       // pass B reads LDS gamma rows unmasked
+      for (int e = t; e < ((Nc - radd + rmul - 1) / rmul) * npad; e += NT_MID) {
+        const int r2 = e / npad;
+        gam[(rmul * r2 + radd) * NC16 + Nc + (e - r2 * npad)] = 0.f;
+      }
+    }
     for (int el = t; el < Pown; el += NT_MID) {
       const int p = rmul * r + radd;
       const int e = SPLIT ? p * Nc1i + qq : el;
@@ -1704,8 +1716,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
-  pair_tile<KK_MID, SMAXC, 2, HS>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr,
-                                  gam, NC16, Dsig, Dtau, ysumv, credg, rmul, radd);
+  pair_tile<KK_MID, SMAXC, 2, HS, 0, GAML>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
+                                           nullptr, gam, NC16, Dsig, Dtau, ysumv, credg, rmul,
+                                           radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const int k = e % HS;
     Dsig[e] *= cvec[k];
