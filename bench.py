@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="training steps captured per HIP graph (a divisor of --steps)")
     ap.add_argument("--variant", type=int, default=2, choices=(1, 2, 3, 4),
                     help="model_<variant>.py (the BASELINE metric is model_2)")
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
@@ -144,18 +146,23 @@ def main():
         if launched:
             torch.distributed.barrier()
 
+    # S training steps per HIP graph launch (S = the largest divisor of --steps up to
+    # --graph-steps), so the timed region is exactly --steps steps
+    gsteps = 1
+    if not args.no_graph:
+        gsteps = max(d for d in range(1, max(1, args.graph_steps) + 1) if args.steps % d == 0)
     if args.no_graph:
         step = lambda: eng.train_step(db)
     else:
-        eng.capture(db)                          # one HIP graph per training step
+        eng.capture(db, steps=gsteps)            # one HIP graph per gsteps training steps
         step = eng.replay
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup // gsteps)):
         step()
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps // gsteps):
         step()
     torch.cuda.synchronize(dev)
     barrier()
@@ -235,7 +242,8 @@ def main():
                            v, {1: "HD-GNN/ES", 2: "HD-GNN/S", 3: "HD-GNN/E", 4: "HD-GNN"}[v],
                            "glide step=2" if (ne, nc) == (200, 74) else "Ne=%d Nc=%d" % (ne, nc)),
                        "engine_path": "fused" if fused else "general",
-                       "launch": "eager" if args.no_graph else "hipGraph replay per step",
+                       "launch": "eager" if args.no_graph else
+                                 "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -137,9 +137,10 @@ class Engine:
                                            self._stream()))
 
     # ---- HIP graph of one training step ----------------------------------------
-    def capture(self, dbatch, outputs=True, logits=False):
-        """Capture train_step(dbatch) (fwd_bwd [+ RCCL all-reduce] + Adam) into a HIP graph;
-        replay() then runs one step with a single launch.  dbatch must stay alive."""
+    def capture(self, dbatch, outputs=True, logits=False, steps=1):
+        """Capture `steps` consecutive train_step(dbatch) calls (fwd_bwd [+ RCCL all-reduce]
+        + Adam each) into one HIP graph; replay() then runs that many training steps with a
+        single launch (no per-step graph launch gap).  dbatch must stay alive."""
         saved = [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
         self.train_step(dbatch, outputs, logits)  # warm: attributes set, RCCL comm built
         for t, v in zip((self.params, self.m, self.v, self.beta_pow), saved):
@@ -148,9 +149,11 @@ class Engine:
         self._graph_batch = dbatch
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.train_step(dbatch, outputs, logits)
+            for _ in range(steps):
+                self.train_step(dbatch, outputs, logits)
         torch.cuda.synchronize(self.device)
         self._graph = g
+        self.graph_steps = steps
         return g
 
     def replay(self):

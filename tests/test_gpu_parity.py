@@ -239,3 +239,24 @@ def test_graph_replay_equals_eager():
     torch.cuda.synchronize()
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.stats, e2.stats)
     assert torch.equal(e1.probs, e2.probs)
+
+
+def test_multi_step_graph_equals_eager():
+    """bench.py captures several training steps per HIP graph: one replay of a 3-step
+    graph == 3 eager steps, bitwise (params, Adam state, last step's outputs)."""
+    B, ne, nc = 6, 50, 30
+    cb = synth_commits(B, ne, nc, 5)
+    flat = layout.init_flat(4)
+    e1, e2 = _engine(B, ne, nc), _engine(B, ne, nc)
+    e1.set_params(flat)
+    e2.set_params(flat)
+    db = cb.to_device()
+    e2.capture(db, steps=3)
+    for _ in range(2):
+        for _ in range(3):
+            e1.train_step(db)
+        e2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.m, e2.m)
+    assert torch.equal(e1.v, e2.v) and torch.equal(e1.beta_pow, e2.beta_pow)
+    assert torch.equal(e1.stats, e2.stats) and torch.equal(e1.probs, e2.probs)
