@@ -1112,13 +1112,18 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
 // coherent; an agent-scope release writes back the whole dirty L2, 5-11 us,
 // tools/probe/xchg2.hip).  The receiver polls its own inbox with L2-bypassing loads
 // (sc0 sc1) until both tags match (1.6 us per 1480-value exchange measured, hidden behind
-// independent work between send and receive), then clears the words (tag 0) for the next
-// launch, so a slot's tag is constant.  The pair is co-resident by construction (host:
+// independent work between send and receive); tags change every launch (xtag).  The pair is co-resident by construction (host:
 // 2 B blocks <= CUs, one block per CU); a partner that never arrives ends the wait after
 // ~20 ms and poisons the CE slot with NaN (loud, no hang).  v must not change between
 // send and receive; n is even.
 // ------------------------------------------------------------------------------
-constexpr uint32_t XTAG = 0xC0DE0000u;          // + slot + 1; no NaN/Inf/huge fill pattern
+// tag of exchange slot s (1..5) in the pair's launch epoch e (a per-commit counter the
+// pair reads at its start and block 0 advances after the last exchange): stale words
+// of earlier launches carry other tags, so the inboxes are never cleared; the xor keeps
+// a tag different from the word's own fill pattern in a garbage workspace
+__device__ __forceinline__ uint32_t xtag(const uint32_t epoch, const int slot) {
+  return (epoch * 8u + (uint32_t)slot) ^ 0xC0DE5A5Au;
+}
 constexpr int XSLOTS = 4;                       // H, D_tau, dn partials; n partial + o rows
 constexpr int XRHO = 256 * HS / 2;              // + the rho rows of a node half (Ne <= 256)
 constexpr unsigned long long XWAIT = 2000000ull;   // s_memrealtime ticks (100 MHz) = 20 ms
@@ -1161,7 +1166,6 @@ __device__ __forceinline__ bool pair_recv_add(float* v, const int n, xu4* __rest
       v[2 * e] = __uint_as_float(w.x);
       v[2 * e + 1] = __uint_as_float(w.z);
     }
-    xstore(in + e, (xu4){0u, 0u, 0u, 0u});
   }
   __syncthreads();
   return late;
@@ -1200,6 +1204,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   constexpr int XB = XSLOTS * XS + XRHO;             // per block inbox
   xu4* xin = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + h) * XB : nullptr;
   xu4* xout = SPLIT ? reinterpret_cast<xu4*>(xch) + (size_t)(2 * b + 1 - h) * XB : nullptr;
+  // per-commit launch epoch of the pair's exchange tags (after the 2B inboxes)
+  uint32_t* xctr = SPLIT ? reinterpret_cast<uint32_t*>(reinterpret_cast<xu4*>(xch) +
+                                                      (size_t)2 * B * XB) + b
+                         : nullptr;
+  const uint32_t epoch = SPLIT ? *xctr : 0u;
   // Thread ids are re-derived from an opaque copy of threadIdx.x at every phase
   // boundary (PHASE()), so the compiler cannot keep addresses derived from them live
   // across phases: this kernel runs at the 128-VGPR ceiling of 1024-thread blocks.
@@ -1465,7 +1474,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     if constexpr (SPLIT) {
       for (int i = t; i < NE4; i += NT_MID) xsc[2 * Nc + i] = (i >= nlo && i < nhi) ? os[i] : 0.f;
       __syncthreads();
-      pair_send(xsc, 2 * Nc + NE4, xout + 3 * XS, XTAG + 4, t);   // constants overlap
+      pair_send(xsc, 2 * Nc + NE4, xout + 3 * XS, xtag(epoch, 4), t);   // constants overlap
     }
   }
   // per-block constants: delta, eps, c, M = V2 U1e, sigma/tau offsets
@@ -1490,7 +1499,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   if constexpr (SPLIT) {
     float* xsc = Ps;
-    xlate |= pair_recv_add(xsc, 2 * Nc + NE4, xin + 3 * XS, XTAG + 4, t);
+    xlate |= pair_recv_add(xsc, 2 * Nc + NE4, xin + 3 * XS, xtag(epoch, 4), t);
     for (int e = t; e < 2 * Nc; e += NT_MID) nb[4 * (e >> 1) + (e & 1)] = xsc[e];
     for (int i = t; i < Ne; i += NT_MID) os[i] = xsc[2 * Nc + i];
   }
@@ -1542,7 +1551,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     Hh[e] -= dg;
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, XTAG + 1, t);   // received in M6
+  if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, xtag(epoch, 1), t);   // received in M6
   MID_STAMP();
 
   // ---- M6: classifier first layer on eff = S_p + T_q, S = G V2 + (Nc-1) c2:
@@ -1578,7 +1587,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   m6_tiles(0);
   if constexpr (SPLIT) {
     if constexpr (STAMPS) MID_STAMP();
-    xlate |= pair_recv_add(Hh, Nc * HS, xin, XTAG + 1, t);
+    xlate |= pair_recv_add(Hh, Nc * HS, xin, xtag(epoch, 1), t);
   }
   m6_tiles(1);
   __syncthreads();
@@ -1710,7 +1719,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       if (t >= 2 && t < 2 + HS) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
     }
   }
-  if constexpr (!TRAIN) return;   // uniform exit: forward-only launch
+  if constexpr (!TRAIN) {         // uniform exit: forward-only launch (the H exchange was
+    if (SPLIT && h == 0 && t == 0) *xctr = epoch + 1u;   // the pair's last: next epoch)
+    return;
+  }
 
   // ---- M8: classifier backward: dkappa_pq = c (.) [kappa_pq > 0] gamma_pq,
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
@@ -1725,7 +1737,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     Dtau[e] *= cvec[k];
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, XTAG + 2, t);   // received in M9
+  if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, xtag(epoch, 2), t);   // received in M9
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
   //   one MFMA GEMM [G^T; 1; 0 | H^T; 0; 1] (22 x 2Nc) . [Dsig; Dtau] (2Nc x 20): rows
@@ -1761,7 +1773,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     if (half == 0) xtile();
     if constexpr (SPLIT) {
       if constexpr (STAMPS) MID_STAMP();
-      xlate |= pair_recv_add(Dtau, Nc * HS, xin + XS, XTAG + 2, t);
+      xlate |= pair_recv_add(Dtau, Nc * HS, xin + XS, xtag(epoch, 2), t);
     }
     if (half == 1) xtile();
     __syncthreads();
@@ -1859,7 +1871,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   if constexpr (SPLIT) {
-    pair_send(dnb, 2 * Nc, xout + 2 * XS, XTAG + 3, t);   // dV1 overlaps
+    pair_send(dnb, 2 * Nc, xout + 2 * XS, xtag(epoch, 3), t);   // dV1 overlaps
     // waves 4-15 warm this XCD's L2 with the count matrices (M11 reads every column; M3
     // fetched only the own half) while waves 0-3 run dV1
     if (wv >= 4) {
@@ -1891,7 +1903,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   if constexpr (SPLIT) {
     if constexpr (STAMPS) MID_STAMP();
-    xlate |= pair_recv_add(dnb, 2 * Nc, xin + 2 * XS, XTAG + 3, t);
+    xlate |= pair_recv_add(dnb, 2 * Nc, xin + 2 * XS, xtag(epoch, 3), t);
   } else {
     __syncthreads();
   }
@@ -2023,7 +2035,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, XTAG + 5, t);
+  if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, xtag(epoch, 5), t);
   MID_STAMP();
   // ---- M13: reductions over rows: dW1' = [x, E_bar, 1]^T dq (waves 0-3),
   //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8);
@@ -2068,7 +2080,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if (t < 3) pb[NP + 2 + t] = 0.f;                  // trailer / pad
   if constexpr (SPLIT) {                             // the partner half's rho rows
     const int plo = h ? 0 : (Ne + 1) / 2, phi = h ? (Ne + 1) / 2 : Ne;
-    xlate |= pair_recv_add<false>(rho + plo * HS, (phi - plo) * HS, xin + XSLOTS * XS, XTAG + 5, t);
+    xlate |= pair_recv_add<false>(rho + plo * HS, (phi - plo) * HS, xin + XSLOTS * XS,
+                                  xtag(epoch, 5), t);
+    if (h == 0 && t == 0) *xctr = epoch + 1u;     // last exchange of the pair: next epoch
   } else {
     __syncthreads();
   }
@@ -2347,7 +2361,7 @@ Work work_layout(const hdg_shape* s) {
   w.aux = take(8);
   // block-pair inboxes (split mode): [B][2 halves][XSLOTS][NC16*HS] u64 (value, tag) words;
   // zero at allocation, left zero by every completed launch
-  w.xch = take(2 * B * 4 * ((size_t)XSLOTS * NC16 * HS / 2 + XRHO));
+  w.xch = take(2 * B * 4 * ((size_t)XSLOTS * NC16 * HS / 2 + XRHO) + B);   // + epochs
   w.total = o;
   return w;
 }

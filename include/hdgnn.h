@@ -99,12 +99,11 @@ int         hdg_param_count(int32_t variant);
  * np.argmax's tie rule, exact); all-reduce the whole buffer.                       */
 int         hdg_grad_len(int32_t variant);
 /* Scratch the library carves per call (parked node rows, partial gradient rows, the
- * block-pair inboxes of the fused path's split mode).  Allocate it zeroed once and keep
- * it per shape: the inboxes are (value, tag) words that every completed call leaves
- * zero, and a stale word equal to a live tag (0xC0DE0001..4 in its high half) would be
- * taken as the partner's data.  Any other content is overwritten before it is read.
- * Split mode (two blocks per commit) runs whenever 2 * batch <= the device's CU count;
- * the environment variable HDG_FUSED_SPLIT=0 forces one block per commit.            */
+ * block-pair inboxes and per-commit launch epochs of the fused path's split mode).  Keep
+ * it per shape across calls; its initial content does not matter (exchange tags derive
+ * from the epoch word and differ from the word's own bit pattern, everything else is
+ * written before it is read).  Split mode (two blocks per commit) runs whenever
+ * 2 * batch <= the device's CU count; HDG_FUSED_SPLIT=0 forces one block per commit.  */
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
 /* bytes of batch->prep for this shape (0 on a shape error) */
 size_t      hdg_prep_bytes(const hdg_shape* shape);
