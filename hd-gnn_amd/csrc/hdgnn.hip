@@ -1800,31 +1800,35 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  for (int e = t; e < 2 * HS * HS + HS; e += NT_MID) {
-    if (e < HS * HS) {                    // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1)c2[m] sumD[k]
-      const int m = e / HS, k = e - m * HS;
-      float acc = Nc1 * Ws[H1_B2 + m] * sumD[k];
-#pragma unroll
-      for (int l = 0; l < HS; ++l) acc = fmaf(Ws[H1_W2 + l * HS + m], Xm[l * HS + k], acc);
-      pb[H2_W1 + (2 + m) * HS + k] = acc;
-    } else if (e < 2 * HS * HS) {         // dV2[l][m] = sum_k X[l][k] U1e[m][k]
-      const int f = e - HS * HS, l = f / HS, m = f - l * HS;
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < HS; ++k) acc = fmaf(Xm[l * HS + k], Ws[H2_W1 + (2 + m) * HS + k], acc);
-      pb[H1_W2 + f] = acc;
-    } else {                              // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
-      const int m = e - 2 * HS * HS;
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < HS; ++k) acc = fmaf(Ws[H2_W1 + (2 + m) * HS + k], sumD[k], acc);
-      pb[H1_B2 + m] = Nc1 * acc;
-    }
-  }
+  // dU1e = V2^T X + (Nc-1) c2 (x) sumD and dV2 = X U1e^T as 16x16 MFMA tiles (4 each,
+  // tiles 0-7), then dG = Dsig M^T, dH = Dtau M^T (tiles 8..); dc2 on the last wave
   float* dG = G;       // G, H dead once X is formed
   float* dH = Hh;
-  for (int tile = wv; tile < 4 * SMAXC; tile += NT_MID / 64) {   // dG = Dsig M^T, dH = Dtau M^T
-    const int which = tile & 1, row0 = (tile >> 2) * 16, col0 = ((tile >> 1) & 1) * 16;
+  for (int tile = wv; tile < 8 + 4 * SMAXC; tile += NT_MID / 64) {   // wave-uniform
+    if (tile < 8) {
+      const int which = tile >> 2, row0 = ((tile >> 1) & 1) * 16, col0 = (tile & 1) * 16;
+      const int ra = row0 + (lane & 15), cb = col0 + (lane & 15);
+      const f4v c = which == 0
+          ? mfma_tile16_p(ra < HS ? Ws + H1_W2 + ra : kzero, ra < HS ? HS : 0,     // V2^T
+                          cb < HS ? Xm + cb : kzero, cb < HS ? HS : 0, HS, lane)    // X
+          : mfma_tile16_p(ra < HS ? Xm + ra * HS : kzero, ra < HS ? 1 : 0,          // X
+                          cb < HS ? Ws + H2_W1 + (2 + cb) * HS : kzero, cb < HS ? 1 : 0,
+                          HS, lane);                                                  // U1e^T
+      const int cc = col0 + (lane & 15);
+      if (cc < HS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = row0 + 4 * (lane >> 4) + q;
+          if (rr < HS) {
+            if (which == 0) pb[H2_W1 + (2 + rr) * HS + cc] = fmaf(Nc1 * Ws[H1_B2 + rr], sumD[cc], c[q]);
+            else pb[H1_W2 + rr * HS + cc] = c[q];
+          }
+        }
+      }
+      continue;
+    }
+    const int tt = tile - 8;
+    const int which = tt & 1, row0 = (tt >> 2) * 16, col0 = ((tt >> 1) & 1) * 16;
     const float* src = which ? Dtau : Dsig;
     const int pr = row0 + (lane & 15), lc = col0 + (lane & 15);
     const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
@@ -1838,6 +1842,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         dst[pr * HS + l] = pr < Nc ? c[q] : 0.f;
       }
     }
+  }
+  if (wv == NT_MID / 64 - 1 && lane < HS) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < HS; ++k) acc = fmaf(Ws[H2_W1 + (2 + lane) * HS + k], sumD[k], acc);
+    pb[H1_B2 + lane] = Nc1 * acc;
   }
   __syncthreads();
   MID_STAMP();
