@@ -1868,16 +1868,17 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  for (int e = t; e < NC16 * 2; e += NT_MID) {      // dn_c[m], m in {0,1} (x' components)
-    const int c = e >> 1, m = e & 1;
-    float acc = 0.f;
-    if (c < Nc) {
+  if (wv < SMAXC) {   // dn_c[m] = Dalpha_c V1[m] + Dbeta_c V1[4+m], m in {0,1}: MFMA row tiles
+    const int row0 = wv * 16, rr = row0 + (lane & 15), m = lane & 15;
+    const bool rv = rr < Nc, mv = m < 2;
+    const f4v c = mfma_tile16_p(rv ? Dal + rr * HS : kzero, rv ? 1 : 0,
+                                mv ? Ws + H1_W1 + m * HS : kzero, mv ? 1 : 0, HS, lane) +
+                  mfma_tile16_p(rv ? Dbe + rr * HS : kzero, rv ? 1 : 0,
+                                mv ? Ws + H1_W1 + (4 + m) * HS : kzero, mv ? 1 : 0, HS, lane);
+    if (mv) {
 #pragma unroll
-      for (int k = 0; k < HS; ++k)
-        acc = fmaf(Ws[H1_W1 + m * HS + k], Dal[c * HS + k],
-                   fmaf(Ws[H1_W1 + (4 + m) * HS + k], Dbe[c * HS + k], acc));
+      for (int q = 0; q < 4; ++q) dnb[2 * (row0 + 4 * (lane >> 4) + q) + m] = c[q];   // 0 past Nc
     }
-    dnb[e] = acc;
   }
   __syncthreads();
   if constexpr (SPLIT) {
