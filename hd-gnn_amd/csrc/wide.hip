@@ -660,7 +660,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
       }
       const float mx = fmaxf(zz.x, zz.y);
       const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
-      const float inv = 1.f / (e0 + e1);
+      const float inv = __builtin_amdgcn_rcpf(e0 + e1);   // e0 + e1 in [1, 2]: 1-ulp rcp
       p0 = e0 * inv;
       p1 = e1 * inv;
       if (++ejj == Ne - 1) { ejj = 0; ++ei; }
@@ -1597,7 +1597,7 @@ __device__ __forceinline__ void ee_clsb_body(
       }
       const float mx = fmaxf(zz.x, zz.y);
       const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
-      const float iv = 1.f / (e0 + e1);
+      const float iv = __builtin_amdgcn_rcpf(e0 + e1);    // e0 + e1 in [1, 2]: 1-ulp rcp
       const float p0 = e0 * iv, p1 = e1 * iv;
       const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
       const f2 d2 = {d1, d1};
