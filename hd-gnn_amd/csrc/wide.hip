@@ -23,8 +23,8 @@
 //   kw_dn           dn_c (gradient of the cross-graph aggregate)
 //   kw_node_bwd     ENT: dx', E3 and W5 grads, rho = dP
 //   kw_ent_bwd      ENT: first-layer grads of mlp_entity_B1
-//   kw_ee_clsb      EE : classifier backward (column pass: dgam + classifier grads, row
-//                   pass: drho)
+//   kw_ee_clsb      EE : classifier backward, one column pass: dgam + classifier grads,
+//                   per-tile partial rows of drho (wave sums over the tile's columns)
 //   kw_ee_nodeb     EE : dR, dC -> phi, psi; classifier U1e, Q2, q2 grads
 //   kw_ee_firstb    EE : first-layer grads of mlp_entityedge_B1 (shared w1_1)
 //   kw_grad_reduce  fixed-order sum of every per-block partial row -> flat gradient
@@ -59,6 +59,53 @@ __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
+}
+
+// Sums of the 20 values v[k] over the 64 lanes of a wave by a transposed butterfly (one
+// shuffle per pair of values and level instead of six per value); store(k, total) runs
+// on one lane per value.  cnt tracks how many real values a lane's block still holds.
+template <class F>
+__device__ __forceinline__ void wave_sums20(const float (&v)[20], const int lane, F store) {
+  float w1[10], w2[5], w3[3], w4[2];
+  int base = 0, cnt;
+  bool up = lane & 32;                                    // 20 -> 10 | 10
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const float a = v[i], b = v[i + 10];
+    w1[i] = (up ? b : a) + __shfl_xor(up ? a : b, 32);
+  }
+  base += up ? 10 : 0;
+  cnt = 10;
+  up = lane & 16;                                         // 10 -> 5 | 5
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float a = w1[i], b = w1[i + 5];
+    w2[i] = (up ? b : a) + __shfl_xor(up ? a : b, 16);
+  }
+  base += up ? 5 : 0;
+  cnt = 5;
+  up = lane & 8;                                          // 5 -> 3 | 2
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float a = w2[i], b = i + 3 < 5 ? w2[i + 3] : 0.f;
+    w3[i] = (up ? b : a) + __shfl_xor(up ? a : b, 8);
+  }
+  base += up ? 3 : 0;
+  cnt = up ? 2 : 3;
+  up = lane & 4;                                          // 3 -> 2 | 1  (2 -> 2 | 0)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float a = w3[i], b = i + 2 < 3 ? w3[i + 2] : 0.f;
+    w4[i] = (up ? b : a) + __shfl_xor(up ? a : b, 4);
+  }
+  base += up ? 2 : 0;
+  cnt = up ? cnt - 2 : (cnt < 2 ? cnt : 2);
+  up = lane & 2;                                          // 2 -> 1 | 1
+  float w5 = (up ? w4[1] : w4[0]) + __shfl_xor(up ? w4[0] : w4[1], 2);
+  base += up ? 1 : 0;
+  cnt = up ? cnt - 1 : (cnt < 1 ? cnt : 1);
+  w5 += __shfl_xor(w5, 1);
+  if (!(lane & 1) && cnt >= 1) store(base, w5);
 }
 
 __device__ __forceinline__ unsigned long long qfix(float v) {
@@ -1503,11 +1550,13 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ee_clsb  grid (te, B, 2): entity-edge classifier backward (model_4.py:286-304)
+// kw_ee_clsb  grid (te, B): entity-edge classifier backward (model_4.py:286-304)
 //   dp_r[m] = dn[hid i'(r)][2+m] + dn[hid j'(r)][2+m];  dz1 = p0 p1 (dp1 - dp0) = -dz0
 //   g_ijk = [kappa'_ijk > 0] (U2'[k][1] - U2'[k][0]) dz1
-//   z = 0 column pass (lane = column j): dgam_j = sum_i g, classifier partial rows
-//   z = 1 row pass    (lane = row i)   : drho_i = sum_j g
+//   column pass (lane = column j): dgam_j = sum_i g, classifier partial rows, and per row
+//   i the tile's partial of drho_i = sum_j g (wave_sums20 over the 64 column lanes; the
+//   te tile partials are summed in tile order by kw_ee_nodeb).  The row-pass body (z = 1,
+//   lane = row i) is kept for reference but no longer launched.
 //   8 waves; the swept side's operand rows staged in LDS, packed fp32, the class bits read
 //   from the lane's own row of a (row pass) or a^T (column pass).
 //   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
@@ -1555,6 +1604,9 @@ __device__ __forceinline__ void ee_clsb_body(
   // rows that hold relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
   const int Nsw = (Z == 1 && t0 >= rows) ? 0 : (Z ? Ne : rows);   // block-uniform
+  float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // Z = 0: row partials
+  if constexpr (Z == 0)                                   // rows past the relations: 0
+    for (int e = rows * H + threadIdx.x; e < Ne * H; e += NTP) rowp[e] = 0.f;
   for (int c0 = 0; c0 < Nsw; c0 += CHM) {
     const int c1 = c0 + CHM < Nsw ? c0 + CHM : Nsw;
     __syncthreads();
@@ -1601,21 +1653,29 @@ __device__ __forceinline__ void ee_clsb_body(
       const float p0 = e0 * iv, p1 = e1 * iv;
       const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
       const f2 d2 = {d1, d1};
+      float gv[H];
 #pragma unroll
       for (int kk = 0; kk < H2; ++kk) {
         const f2 cd = cE[kk] * d2;
         const f2 g = {pre[kk].x > 0.f ? cd.x : 0.f, pre[kk].y > 0.f ? cd.y : 0.f};
         acc[kk] += g;
+        gv[2 * kk] = g.x;
+        gv[2 * kk + 1] = g.y;
         if constexpr (Z == 0) {
           zk[kk] = fma2(relu2(pre[kk]), d2, zk[kk]);
           ag[kk] = fma2(a2, g, ag[kk]);
         }
       }
-      if constexpr (Z == 0) sdl += d1;
+      if constexpr (Z == 0) {
+        sdl += d1;
+        // the row pass folded in: this tile's 64 columns of row i = m, one partial row
+        // of drho per tile (kw_ee_nodeb sums the te partials in tile order)
+        wave_sums20(gv, lane, [&](int k, float x) { rowp[(size_t)m * H + k] = x; });
+      }
     }
   }
   combine8(acc, sm.buf, sm.res);
-  float* dout = (Z ? drho : dgam) + (size_t)b * Ne * H;
+  float* dout = (Z ? drho : dgam) + (size_t)b * Ne * H;   // (Z = 1 no longer launched)
   for (int e = threadIdx.x; e < TN * H; e += NTP) {
     const int nn = e / H, k = e - nn * H;
     if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = sm.res[nn * HP + k];
@@ -1678,10 +1738,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_clsb(
     sm.dnl[e] = dn[((size_t)b * Nc + e / 2) * 4 + 2 + (e & 1)];
   __syncthreads();
   const int dn1 = n - 1 > 0 ? n - 1 : 1;
-  if (blockIdx.z == 0)
-    ee_clsb_body<0>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
-  else
-    ee_clsb_body<1>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
+  ee_clsb_body<0>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1705,7 +1762,10 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   for (int e = t; e < TN * H; e += NT) {
     const int n = e / H, k = e - n * H;
     const bool in = t0 + n < Ne;
-    A[n * HP + k] = in ? drho[base + e] : 0.f;
+    float dr = 0.f;                                   // the te row partials, tile order
+    if (in)
+      for (int q = 0; q < te; ++q) dr += drho[((size_t)(b * te + q) * Ne + t0) * H + e];
+    A[n * HP + k] = dr;
     Bq[n * HP + k] = in ? dgam[base + e] : 0.f;
     R1t[n * HP + k] = in ? R1[base + e] : 0.f;
     C1t[n * HP + k] = in ? C1[base + e] : 0.f;
@@ -1883,7 +1943,8 @@ WideWork wide_layout(const hdg_shape* s) {
   }
   if (has_ee(v)) {
     w.R1 = take(NEH); w.C1 = take(NEH); w.Rn = take(NEH); w.Cn = take(NEH);
-    w.rho = take(NEH); w.gmm = take(NEH); w.drho = take(NEH); w.dgam = take(NEH);
+    w.rho = take(NEH); w.gmm = take(NEH); w.dgam = take(NEH);
+    w.drho = take(NEH * (size_t)((Ne + TN - 1) / TN));    // one partial per column tile
     w.phi = take(NEH); w.psi = take(NEH);
     w.ncpart = take(B * ((Ne + TN - 1) / TN) * Nc * 4);
   }
@@ -2057,7 +2118,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   if (ee) {
     const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
-    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 2), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
                        bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                        F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
