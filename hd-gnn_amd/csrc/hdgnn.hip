@@ -1285,35 +1285,73 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   const int xwords = (int)pp[PL.xoffc + Ne];
   const bool lfit = xwords <= L.Uwords - NE4 * HS;
   const float* xlistg = reinterpret_cast<const float*>(pp + PL.xl);
+  // every global load of the stage is issued before the first LDS write (one HBM round
+  // trip instead of one per array); Ne, nd < NT_MID and Nc * WC < NT_MID on this path
+  constexpr int WQ = (NP + NT_MID - 1) / NT_MID;
+  constexpr int LQ = 2;                            // x-list float4 per thread in the batch
+  float wr_[WQ];
+#pragma unroll
+  for (int u = 0; u < WQ; ++u) wr_[u] = t + u * NT_MID < NP ? Wg[t + u * NT_MID] : 0.f;
+  float xv = 0.f, xsv = 0.f, xuv = 0.f;
+  int pmv = 0, cmv = 0, orv = 0, ocv = 0;
+  double pxv = 0.0;
+  uint32_t ybv = 0u;
+  if (t < Ne) {
+    xv = x[(size_t)b * Ne + t];
+    xsv = reinterpret_cast<const float*>(pp + PL.xsrt)[t];
+    pmv = reinterpret_cast<const int*>(pp + PL.perm)[t];
+  }
+  if (t <= nd) {
+    if (t < nd) xuv = reinterpret_cast<const float*>(pp + PL.xu)[t];
+    cmv = reinterpret_cast<const int*>(pp + PL.cum)[t];
+    pxv = reinterpret_cast<const double*>(pp + PL.pxd)[t];
+  }
+  if (t <= Ne) {   // x-list offsets (E1); the id offsets for E2 are restaged before E2
+    orv = reinterpret_cast<const int*>(pp + PL.xoffr)[t];
+    ocv = reinterpret_cast<const int*>(pp + PL.xoffc)[t];
+  }
+  if (t < Nc * WC) ybv = ybits[(size_t)b * Nc * WC + t];
+  float4 lv[LQ];
+#pragma unroll
+  for (int u = 0; u < LQ; ++u) {
+    const int w = 4 * (t + u * NT_MID);
+    lv[u] = (lfit && w < xwords) ? *reinterpret_cast<const float4*>(pp + PL.xl + w)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float l2 = 0.f;
-  for (int i = t; i < NP; i += NT_MID) {
-    const float w = Wg[i];
-    Ws[i] = w;
-    l2 = fmaf(w, w, l2);
+#pragma unroll
+  for (int u = 0; u < WQ; ++u) {
+    if (t + u * NT_MID < NP) Ws[t + u * NT_MID] = wr_[u];
+    l2 = fmaf(wr_[u], wr_[u], l2);
   }
   if (aux && b == 0 && h == 0) {           // pre-update loss_para / loss_map / Adam factor
     l2 = wave_sum(l2);
     if (lane == 0) red[wv * 32] = l2;
   }
-  for (int i = t; i < Ne; i += NT_MID) {
-    xs[i] = x[(size_t)b * Ne + i];
-    xsrt[i] = reinterpret_cast<const float*>(pp + PL.xsrt)[i];
-    perm[i] = reinterpret_cast<const int*>(pp + PL.perm)[i];
+  if (t < Ne) {
+    xs[t] = xv;
+    xsrt[t] = xsv;
+    perm[t] = pmv;
   }
-  for (int q = t; q <= nd; q += NT_MID) {
-    if (q < nd) xu[q] = reinterpret_cast<const float*>(pp + PL.xu)[q];
-    cum[q] = reinterpret_cast<const int*>(pp + PL.cum)[q];
-    pxd[q] = reinterpret_cast<const double*>(pp + PL.pxd)[q];
+  if (t <= nd) {
+    if (t < nd) xu[t] = xuv;
+    cum[t] = cmv;
+    pxd[t] = pxv;
   }
-  for (int i = t; i <= Ne; i += NT_MID) {   // x-list offsets (E1); the id offsets for E2
-    offr[i] = reinterpret_cast<const int*>(pp + PL.xoffr)[i];   // are restaged before E2
-    offc[i] = reinterpret_cast<const int*>(pp + PL.xoffc)[i];
+  if (t <= Ne) {
+    offr[t] = orv;
+    offc[t] = ocv;
   }
-  if (lfit)
-    for (int w = 4 * t; w < xwords; w += 4 * NT_MID)
+  if (t < Nc * WC) yb[t] = ybv;
+#pragma unroll
+  for (int u = 0; u < LQ; ++u) {
+    const int w = 4 * (t + u * NT_MID);
+    if (lfit && w < xwords) *reinterpret_cast<float4*>(U + NE4 * HS + w) = lv[u];
+  }
+  if (lfit)                                // the rest of long lists
+    for (int w = 4 * (t + LQ * NT_MID); w < xwords; w += 4 * NT_MID)
       *reinterpret_cast<float4*>(U + NE4 * HS + w) =
           *reinterpret_cast<const float4*>(pp + PL.xl + w);
-  for (int w = t; w < Nc * WC; w += NT_MID) yb[w] = ybits[(size_t)b * Nc * WC + w];
   if (t == 0) { kzero[0] = 0.f; kzero[1] = 1.f; }
   __syncthreads();
   if (aux && b == 0 && h == 0 && t == 0) {   // model_2.py:123-130, 326-333; TF ApplyAdam lr_t
