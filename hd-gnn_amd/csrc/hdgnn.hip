@@ -2012,6 +2012,20 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
+  // E2's row neighbour lists and row CSR offsets: fetched here into registers (one HBM
+  // round trip hidden behind M12 / M13 and the rho exchange), written to LDS after the
+  // exchange (the P slot they go to is read by dW5)
+  const int rl = (int)pp[PL.xoffc];                 // padded row-list length (multiple of 4)
+  const bool rfit = rl / 4 + rl <= NE4 * HS;
+  const int xl2o = (rl / 4 + 3) & ~3;              // staged x values after the ids
+  uint32_t e2id = 0u;
+  float4 e2x = make_float4(0.f, 0.f, 0.f, 0.f);
+  int e2off = 0;
+  if (rfit) {
+    if (t < rl / 4) e2id = pp[PL.lists + t];
+    if (4 * t < rl) e2x = *reinterpret_cast<const float4*>(pp + PL.xl + 4 * t);
+  }
+  if (t <= Ne) e2off = reinterpret_cast<const int*>(pp + PL.offr)[t];
   // row-local chain per 16-row block: dq = [h > 0] w2' do;  dE = dq W1'[1:]^T;
   // rho = dE W5^T (into h's rows, consumed first); partial dw2' / db2' of the block
   for (int rb = (nlo >> 4) + wv; rb <= ((nhi - 1) >> 4); rb += NT_MID / 64) {   // wave-uniform
@@ -2150,17 +2164,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Tx = Tr + HS * TL;                // [HS][TL]
   float* red2 = Tx + HS * TL;              // [16 waves][4][HS]  (ends below rho_off)
   // row neighbour (id, x) lists (padded, offsets xoffr still in offr), staged into the P
-  // slot (dead after dW5) when they fit; offc <- the compact row CSR (degrees)
-  const int rl = (int)pp[PL.xoffc];                 // padded row-list length (multiple of 4)
-  const bool rfit = rl / 4 + rl <= NE4 * HS;
-  const int xl2o = (rl / 4 + 3) & ~3;              // staged x values after the ids
+  // slot (dead after dW5) when they fit (rl <= 4096 < 4 NT_MID: one id word and one x
+  // float4 per thread, fetched before M12); offc <- the compact row CSR (degrees)
   if (rfit) {
-    for (int w = t; w < rl / 4; w += NT_MID) Ps[w] = __builtin_bit_cast(float, pp[PL.lists + w]);
-    for (int w = 4 * t; w < rl; w += 4 * NT_MID)
-      *reinterpret_cast<float4*>(Ps + xl2o + w) =
-          *reinterpret_cast<const float4*>(pp + PL.xl + w);
+    if (t < rl / 4) Ps[t] = __builtin_bit_cast(float, e2id);
+    if (4 * t < rl) *reinterpret_cast<float4*>(Ps + xl2o + 4 * t) = e2x;
   }
-  for (int i = t; i <= Ne; i += NT_MID) offc[i] = reinterpret_cast<const int*>(pp + PL.offr)[i];
+  if (t <= Ne) offc[t] = e2off;
   for (int k = wv; k < HS; k += NT_MID / 64) {        // wave-uniform; both tables of unit k
     const bool suf = Ws[E1_W1 + HS + k] >= 0.f;      // from one gather of rho
     float* T0 = Tr + k * TL;
