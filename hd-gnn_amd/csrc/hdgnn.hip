@@ -1702,7 +1702,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const float mx = fmaxf(z0, z1);
       const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
       const float ssum = e0 + e1;
-      const float inv = 1.f / ssum;
+      const float inv = __builtin_amdgcn_rcpf(ssum);   // ssum in [1, 2]: 1-ulp rcp
       const float p0 = e0 * inv, p1 = e1 * inv;
       ce_acc += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
       corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0

@@ -61,34 +61,50 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, false));
+}
+// v_permlane32_swap / v_permlane16_swap (VALU, no LDS): swap32 trades x's lanes 32-63 for
+// y's lanes 0-31, swap16 x's rows 1, 3 for y's rows 0, 2 (inline asm: the ROCm 7.2
+// builtins mis-assign the two results; two wait states after a VALU write of the operands)
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
 // Sums of the 20 values v[k] over the 64 lanes of a wave by a transposed butterfly (one
-// shuffle per pair of values and level instead of six per value); store(k, total) runs
-// on one lane per value.  cnt tracks how many real values a lane's block still holds.
+// exchange per pair of values and level instead of six per value), all in the VALU:
+// permlane swaps across the 32- and 16-lane halves, then DPP inside a 16-lane row
+// (row_ror:8 = lane ^ 8, row_half_mirror = 7 - lane within 8, quad_perm for ^2, ^1);
+// a lane keeps the first or second half of the values by its lane bit.  store(k, total)
+// runs on one lane per value; cnt tracks how many real values a lane's block holds.
 template <class F>
 __device__ __forceinline__ void wave_sums20(const float (&v)[20], const int lane, F store) {
   float w1[10], w2[5], w3[3], w4[2];
   int base = 0, cnt;
-  bool up = lane & 32;                                    // 20 -> 10 | 10
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const float a = v[i], b = v[i + 10];
-    w1[i] = (up ? b : a) + __shfl_xor(up ? a : b, 32);
+  for (int i = 0; i < 10; ++i) {                          // 20 -> 10 | 10 (lane bit 5)
+    float x = v[i], y = v[i + 10];
+    swap32(x, y);
+    w1[i] = x + y;
   }
-  base += up ? 10 : 0;
-  cnt = 10;
-  up = lane & 16;                                         // 10 -> 5 | 5
+  base += (lane & 32) ? 10 : 0;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const float a = w1[i], b = w1[i + 5];
-    w2[i] = (up ? b : a) + __shfl_xor(up ? a : b, 16);
+  for (int i = 0; i < 5; ++i) {                           // 10 -> 5 | 5 (lane bit 4)
+    float x = w1[i], y = w1[i + 5];
+    swap16(x, y);
+    w2[i] = x + y;
   }
-  base += up ? 5 : 0;
-  cnt = 5;
-  up = lane & 8;                                          // 5 -> 3 | 2
+  base += (lane & 16) ? 5 : 0;
+  bool up = lane & 8;                                     // 5 -> 3 | 2
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float a = w2[i], b = i + 3 < 5 ? w2[i + 3] : 0.f;
-    w3[i] = (up ? b : a) + __shfl_xor(up ? a : b, 8);
+    w3[i] = (up ? b : a) + dppf<0x128>(up ? a : b);
   }
   base += up ? 3 : 0;
   cnt = up ? 2 : 3;
@@ -96,15 +112,15 @@ __device__ __forceinline__ void wave_sums20(const float (&v)[20], const int lane
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const float a = w3[i], b = i + 2 < 3 ? w3[i + 2] : 0.f;
-    w4[i] = (up ? b : a) + __shfl_xor(up ? a : b, 4);
+    w4[i] = (up ? b : a) + dppf<0x141>(up ? a : b);
   }
   base += up ? 2 : 0;
   cnt = up ? cnt - 2 : (cnt < 2 ? cnt : 2);
   up = lane & 2;                                          // 2 -> 1 | 1
-  float w5 = (up ? w4[1] : w4[0]) + __shfl_xor(up ? w4[0] : w4[1], 2);
+  float w5 = (up ? w4[1] : w4[0]) + dppf<0x4E>(up ? w4[0] : w4[1]);
   base += up ? 1 : 0;
   cnt = up ? cnt - 1 : (cnt < 1 ? cnt : 1);
-  w5 += __shfl_xor(w5, 1);
+  w5 += dppf<0xB1>(w5);
   if (!(lane & 1) && cnt >= 1) store(base, w5);
 }
 
@@ -941,7 +957,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
       if (live && q != p) {
         const float mx = fmaxf(z0, z1);
         const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
-        const float ssum = e0 + e1, inv = 1.f / ssum;
+        const float ssum = e0 + e1, inv = __builtin_amdgcn_rcpf(ssum);   // [1, 2]: 1-ulp rcp
         const float p0 = e0 * inv, p1 = e1 * inv;
         const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
         if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
@@ -1569,6 +1585,7 @@ struct EEBwdSmem {
   float* tot;
   int* hl;
   float* dnl;
+  const float* cst;   // U2' (2H) | EE a-offsets d (H) | U2'[k][1] - U2'[k][0] (H): broadcast reads
 };
 
 template <int Z>
@@ -1586,18 +1603,16 @@ __device__ __forceinline__ void ee_clsb_body(
   const float* obase = (Z ? gmm : rho) + (size_t)b * Ne * H;   // swept operand
   const float* own = (Z ? rho : gmm) + ((size_t)b * Ne + ncl) * H;
   const uint32_t* brow = (Z ? abits : aT) + ((size_t)b * Ne + ncl) * WE;
-  f2 ow[H2], dl[H2], cE[H2], acc[H2], zk[H2], ag[H2], u2[H];
+  // the weight constants are LDS broadcast reads in the row loop (sm.cst), not registers:
+  // 80 VGPRs fewer, 4 waves per SIMD instead of 2 (two blocks per CU)
+  f2 ow[H2], acc[H2], zk[H2], ag[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
     ow[kk] = ld2(own + 2 * kk);
-    dl[kk] = ld2(D + D_EED + 2 * kk);
-    cE[kk] = ld2(D + D_EEC + 2 * kk);
     acc[kk] = (f2){0.f, 0.f};
     zk[kk] = acc[kk];
     ag[kk] = acc[kk];
   }
-#pragma unroll
-  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.EC_W2 + 2 * k);
   const f2 bb = ld2(W + o.EC_B2);
   const float inv = 1.f / (float)dn1;
   float sdl = 0.f;
@@ -1633,19 +1648,25 @@ __device__ __forceinline__ void ee_clsb_body(
       }
       const f2 a2 = {af, af};
       const float4* o4 = reinterpret_cast<const float4*>(sm.os_ + (m - c0) * H);
+      int co = 0;                  // opaque 0: keeps the constant reads in the loop (LDS
+      asm volatile("" : "+v"(co)); // broadcast) instead of hoisted into 80 VGPRs
+      const float4* cu2 = reinterpret_cast<const float4*>(sm.cst + co);          // u2 pairs
+      const float4* cdl = reinterpret_cast<const float4*>(sm.cst + co + 2 * H);  // d
+      const float4* ccE = reinterpret_cast<const float4*>(sm.cst + co + 3 * H);  // c
       f2 pre[H2];
       f2 zz = bb;
 #pragma unroll
       for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j: the same sum kw_ee_fwd forms
-        const float4 q = o4[v];
-        pre[2 * v] = fma2(a2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y});
-        pre[2 * v + 1] = fma2(a2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
+        const float4 q = o4[v], dv = cdl[v];
+        pre[2 * v] = fma2(a2, (f2){dv.x, dv.y}, ow[2 * v] + (f2){q.x, q.y});
+        pre[2 * v + 1] = fma2(a2, (f2){dv.z, dv.w}, ow[2 * v + 1] + (f2){q.z, q.w});
       }
 #pragma unroll
       for (int kk = 0; kk < H2; ++kk) {
         const f2 kp = relu2(pre[kk]);
-        zz = fma2((f2){kp.x, kp.x}, u2[2 * kk], zz);
-        zz = fma2((f2){kp.y, kp.y}, u2[2 * kk + 1], zz);
+        const float4 w = cu2[kk];
+        zz = fma2((f2){kp.x, kp.x}, (f2){w.x, w.y}, zz);
+        zz = fma2((f2){kp.y, kp.y}, (f2){w.z, w.w}, zz);
       }
       const float mx = fmaxf(zz.x, zz.y);
       const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
@@ -1656,7 +1677,8 @@ __device__ __forceinline__ void ee_clsb_body(
       float gv[H];
 #pragma unroll
       for (int kk = 0; kk < H2; ++kk) {
-        const f2 cd = cE[kk] * d2;
+        const float4 cv = ccE[kk >> 1];
+        const f2 cd = ((kk & 1) ? (f2){cv.z, cv.w} : (f2){cv.x, cv.y}) * d2;
         const f2 g = {pre[kk].x > 0.f ? cd.x : 0.f, pre[kk].y > 0.f ? cd.y : 0.f};
         acc[kk] += g;
         gv[2 * kk] = g.x;
@@ -1710,7 +1732,7 @@ __device__ __forceinline__ void ee_clsb_body(
   }
 }
 
-__global__ __launch_bounds__(NTP) void kw_ee_clsb(
+__global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void kw_ee_clsb(
     const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
     const int32_t* __restrict__ hidg, const int32_t* __restrict__ nleng,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
@@ -1722,14 +1744,20 @@ __global__ __launch_bounds__(NTP) void kw_ee_clsb(
   __shared__ float res[TN * HP];
   __shared__ float red[NWP * 41];
   __shared__ float tot[41];
+  __shared__ __attribute__((aligned(16))) float cst[4 * H];
   const int b = blockIdx.y;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   const int nrel = n >= 2 ? n * (n - 1) : 0;
   EEBwdSmem sm;
-  sm.os_ = os_; sm.buf = buf; sm.res = res; sm.red = red; sm.tot = tot;
+  sm.os_ = os_; sm.buf = buf; sm.res = res; sm.red = red; sm.tot = tot; sm.cst = cst;
   sm.hl = reinterpret_cast<int*>(dyn);
   sm.dnl = dyn + Ne;
+  if (threadIdx.x < 2 * H) cst[threadIdx.x] = W[o.EC_W2 + threadIdx.x];
+  if (threadIdx.x < H) {
+    cst[2 * H + threadIdx.x] = D[D_EED + threadIdx.x];
+    cst[3 * H + threadIdx.x] = D[D_EEC + threadIdx.x];
+  }
   for (int e = threadIdx.x; e < Ne; e += NTP) {
     const int h = hidg[(size_t)b * Ne + e];
     sm.hl[e] = (h >= 0 && h < Nc) ? h : -1;
