@@ -54,12 +54,6 @@ constexpr double FIX = 4294967296.0;   // 2^32 fixed-point scale of the hunk bin
 __device__ __forceinline__ float relu(float v) { return fmaxf(v, 0.f); }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// wave sum by xor butterfly: every lane ends with the same (fixed-order) total
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -74,6 +68,36 @@ __device__ __forceinline__ void swap32(float& x, float& y) {
 }
 __device__ __forceinline__ void swap16(float& x, float& y) {
   asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+// wave sum by a VALU butterfly (permlane swaps across the 32- / 16-lane halves, DPP inside
+// a row): every lane ends with the same total (each level adds the same two partial
+// sums in every lane, and fp32 addition commutes)
+__device__ __forceinline__ float wsum(float v) {
+  float x = v, y = v;
+  swap32(x, y);
+  v = x + y;
+  x = v;
+  y = v;
+  swap16(x, y);
+  v = x + y;
+  v += dppf<0x128>(v);   // row_ror:8        lane ^ 8
+  v += dppf<0x141>(v);   // row_half_mirror  7 - lane (per 8)
+  v += dppf<0x4E>(v);    // quad_perm        lane ^ 2
+  v += dppf<0xB1>(v);    // quad_perm        lane ^ 1
+  return v;
+}
+// wave sums of two values: lanes 0-31 end with a's total, lanes 32-63 with b's
+__device__ __forceinline__ float wsum2(float a, float b) {
+  swap32(a, b);
+  float v = a + b, x = v, y = v;
+  swap16(x, y);
+  v = x + y;
+  v += dppf<0x128>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0xB1>(v);
+  return v;
 }
 
 // Sums of the 20 values v[k] over the 64 lanes of a wave by a transposed butterfly (one
@@ -730,12 +754,9 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     }
     s0 += p0;
     s1 += p1;
-    const float w0 = wsum(p0), w1 = wsum(p1);
+    const float w01 = wsum2(p0, p1);                 // lane 0: sum p0, lane 32: sum p1
     const int ht = hid[jp];
-    if (lane == 0 && ht >= 0 && ht < Nc) {
-      atomicAdd(&bins[2 * ht], qfix(w0));
-      atomicAdd(&bins[2 * ht + 1], qfix(w1));
-    }
+    if ((lane & 31) == 0 && ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (lane >> 5)], qfix(w01));
   }
   if (live) {
     const int hs = hid[ip];
