@@ -2045,9 +2045,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         v[j] = (ok && k < HS) ? hB[i * HS + k] * d : (k == HS ? d : 0.f);
       }
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {                 // sum over the 16 rows (lane bits 2..5)
-        v[j] += __shfl_xor(v[j], 4);
-        v[j] += __shfl_xor(v[j], 8);
+      for (int j = 0; j < 6; ++j) {                 // sum over the 16 rows (lane bits 2..5):
+        v[j] += dppf<0x124>(v[j]);                  // DPP row_ror:4, row_ror:8 keep lane & 3;
+        v[j] += dppf<0x128>(v[j]);                  // lanes 0-3 (r = 0) hold the stored sums
         v[j] = xrow_sum4(v[j]);
       }
       if (r == 0) {
