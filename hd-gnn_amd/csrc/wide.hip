@@ -1038,9 +1038,13 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     float* __restrict__ Dtau, float* __restrict__ dG, float* __restrict__ dH,
     float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float os_[CHM * H];
-  __shared__ float gt[TN * GTP];
-  __shared__ float buf[NWP * TN * HP];
+  // the swept rows and the gamma tile are dead once the sweep ends: combine8's buffer
+  // overlays them (66 KB of LDS instead of 109: two blocks per CU)
+  constexpr int SWEEP_W = CHM * H + TN * GTP, BUF_W = NWP * TN * HP;
+  __shared__ __attribute__((aligned(16))) float big[SWEEP_W > BUF_W ? SWEEP_W : BUF_W];
+  float* os_ = big;
+  float* gt = big + CHM * H;
+  float* buf = big;
   __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
   __shared__ float X[H * H], sumD[H], ysum[H];
   __shared__ float Wl[3 * H * H + H];
@@ -1100,6 +1104,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
       }
     }
   }
+  __syncthreads();                       // every wave is done with os_ / gt (= buf)
   combine8(acc, buf, res);
   if (z == 0) combine8(ya, buf, yres);
   const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
