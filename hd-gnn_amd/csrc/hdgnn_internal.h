@@ -92,6 +92,50 @@ hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride,
                             int o_kt, int o_ncst, hipStream_t st);
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// ------------------------------------------------------------------------------
+// MFMA 16x16 fp32 tile (v_mfma_f32_16x16x4_f32) used by both paths
+// ------------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// The same tile with strided operands: lane l supplies row r = l & 15 of A as
+// pa[k * sa] and column r of B as pb[k * sb], k < K.  A row / column outside the matrix
+// passes a pointer to a 0.f word with stride 0 (a row of ones: a 1.f word, stride 0), so
+// the K loop carries no bounds logic: one LDS read and one address add per operand.
+__device__ __forceinline__ f4v mfma_tile16_p(const float* pa, const int sa, const float* pb,
+                                             const int sb, const int K, const int lane) {
+  const int q = lane >> 4;
+  const float* a = pa + q * sa;
+  const float* b = pb + q * sb;
+  const int sa4 = 4 * sa, sb4 = 4 * sb;
+  f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  int k = 0;
+  for (; k + 16 <= K; k += 16) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      av[u] = a[u * sa4];
+      bv[u] = b[u * sb4];
+    }
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c1, 0, 0, 0);
+    a += 4 * sa4;
+    b += 4 * sb4;
+  }
+  for (; k + 4 <= K; k += 4) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c0, 0, 0, 0);
+    a += sa4;
+    b += sb4;
+  }
+  if (k < K) {                       // K % 4 tail: entries k + q >= K are selected to zero
+    const bool ok = k + q < K;       // (callers' arrays are padded, the read stays in LDS)
+    const float av = ok ? a[0] : 0.f, bv = ok ? b[0] : 0.f;
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, c0, 0, 0, 0);
+  }
+  return c0 + c1;
+}
+
 }  // namespace hdg
 
 #endif  // HDGNN_INTERNAL_H

@@ -1808,7 +1808,9 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   __shared__ float A[TN * HP], Bq[TN * HP], R1t[TN * HP], C1t[TN * HP], Rt[TN * HP],
       Ct[TN * HP], dR[TN * HP], dC[TN * HP];
   __shared__ float Wl[800];
+  __shared__ float kz[1];                         // 0.f: stride-0 operand of padding tiles
   const float *U1e = Wl, *Q2 = Wl + 400;          // classifier rows 2..21 | EE second layer
+  if (threadIdx.x == 0) kz[0] = 0.f;
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
   const size_t base = ((size_t)b * Ne + t0) * H;
   stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
@@ -1855,26 +1857,33 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   const Seg& s1 = sg.s[SG_ECW1E];
   const Seg& s2 = sg.s[SG_EEW2];
   const float Ne1 = (float)(Ne - 1);
-  for (int e = t; e < 400 + 420; e += NT) {
-    float a = 0.f;
-    if (e < 400) {
-      const int m = e / H, k = e - m * H;
-      for (int n = 0; n < TN; ++n)
-        a = fmaf(Rt[n * HP + m], A[n * HP + k], fmaf(Ct[n * HP + m], Bq[n * HP + k], a));
-      put(part, s1, e, row, a);
-    } else {
-      const int f = e - 400;
-      if (f < 400) {
-        const int l = f / H, m = f - l * H;
-        for (int n = 0; n < TN; ++n)
-          a = fmaf(R1t[n * HP + l], dR[n * HP + m], fmaf(C1t[n * HP + l], dC[n * HP + m], a));
-      } else {
-        const int m = f - 400;
-        for (int n = 0; n < TN; ++n) a += dR[n * HP + m] + dC[n * HP + m];
-        a *= Ne1;
+  // dU1e' = Rt^T A + Ct^T Bq and dQ2 = R1t^T dR + C1t^T dC over the tile's 64 nodes as
+  // 16x16 MFMA tiles (2 x 2 per matrix, one wave per two tiles); dq2 on the VALU
+  const int lane = t & 63;
+  for (int tile = t >> 6; tile < 8; tile += NT / 64) {      // wave-uniform
+    const int which = tile >> 2, row0 = ((tile >> 1) & 1) * 16, col0 = (tile & 1) * 16;
+    const int ra = row0 + (lane & 15), cb = col0 + (lane & 15);
+    const bool rv = ra < H, cv = cb < H;
+    const float* a0 = which ? R1t : Rt;                     // [n][row]
+    const float* b0 = which ? dR : A;                       // [n][col]
+    const float* a1 = which ? C1t : Ct;
+    const float* b1 = which ? dC : Bq;
+    const f4v c = mfma_tile16_p(rv ? a0 + ra : kz, rv ? HP : 0, cv ? b0 + cb : kz, cv ? HP : 0,
+                                TN, lane) +
+                  mfma_tile16_p(rv ? a1 + ra : kz, rv ? HP : 0, cv ? b1 + cb : kz, cv ? HP : 0,
+                                TN, lane);
+    if (cv) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = row0 + 4 * (lane >> 4) + j;
+        if (rr < H) put(part, which ? s2 : s1, rr * H + cb, row, c[j]);
       }
-      put(part, s2, f, row, a);
     }
+  }
+  if (t < H) {
+    float a = 0.f;
+    for (int n = 0; n < TN; ++n) a += dR[n * HP + t] + dC[n * HP + t];
+    put(part, s2, 400 + t, row, a * Ne1);
   }
 }
 
