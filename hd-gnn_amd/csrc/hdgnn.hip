@@ -11,7 +11,7 @@
 //   k_grad_reduce [P/64]    deterministic per-commit partial sum (fixed commit order)
 //   k_adam_tf     [1]       loss_para / loss_map gradients + TF1 ApplyAdam
 //
-// plus, once per uploaded batch, k_prep_sort / k_prep_maps (hdg_prepare): the
+// plus, once per uploaded batch, k_prep_sort / k_prep_counts (hdg_prepare): the
 // parameter-independent tables of a commit (x sort order, transposed class bits,
 // cross-graph count matrices).
 //
@@ -487,7 +487,7 @@ __device__ __forceinline__ int top_pow2(int n) {   // largest power of two <= n 
 //   pxd[NE4+4]   f64 pxd[q] = sum of x over nodes with x < xu[q]      meta[4] = {nd}
 //   offr, offc   CSR offsets of the a = 1 neighbours of each node (rows of a, of a^T)
 //   lists        u8 ids of the row neighbours, padded like the row x-lists (xoffr)
-//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
+//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_counts)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // ------------------------------------------------------------------------------
 using hdg::PrepLayout;
@@ -630,61 +630,118 @@ __global__ __launch_bounds__(256) void k_prep_sort(const float* __restrict__ x,
 // Only x' changes between steps, so
 //   n_c[0] = sum_I ks[c][I] x'_I,  n_c[1] = sum_J kt[c][J] x'_J,  n_c[2:4] = ncst[c]
 // ks[c][I] = #{r in Ne-row I : s_r = c} + #{r in Ne-row I : t_r = c}, kt over Ne-columns.
-// Integer LDS atomics (order-independent) over chunks of CH hunks.
-// The count arrays live at word offsets (o_ks, o_kt, o_ncst) of each commit's prep block
-// of `stride` words (fused layout: prep_layout; general path: its own layout).
-__global__ __launch_bounds__(1024) void k_prep_maps(const uint32_t* __restrict__ abits,
-                                                    const int32_t* __restrict__ hidg,
-                                                    const int32_t* __restrict__ nleng,
-                                                    uint32_t* __restrict__ prep, int Ne, int Nc,
-                                                    int CH, int stride, int o_ks, int o_kt,
-                                                    int o_ncst) {
-  extern __shared__ uint32_t cnt[];   // [2][CH][Ne], then [Nc][2]
-  const int b = blockIdx.x, t = threadIdx.x;
+//
+// k_prep_counts grid (ceil(Ne / TI), B, 2): block (tile, b, z) owns TI Ne-rows (z = 0: ks,
+// plus the class counts) or TI Ne-columns (z = 1: kt) of commit b and visits each of their
+// relations once, counting into an LDS histogram [Nc][TI] (integer, order-independent).
+// Lanes hold consecutive relations of a row (or column), whose hunk ids repeat in runs
+// (s_r is constant over n-1 consecutive relations): each run of equal counter addresses in
+// consecutive lanes is one LDS atomic by its first lane (ballot masks), not a same-address
+// conflict per lane.  The tile's counters are written as coalesced u16 rows; the class
+// counts are summed over tiles with global u32 atomics into ncst (zeroed, then converted to
+// f32 in place by k_prep_ncst).  The count arrays live at word offsets (o_ks, o_kt, o_ncst)
+// of each commit's prep block of `stride` words (fused layout: prep_layout; general path:
+// its own layout).
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ void divmod_exact(int r, int d, float inv, int& q, int& rem) {
+  q = (int)((float)r * inv);
+  rem = r - q * d;
+  while (rem < 0) { --q; rem += d; }
+  while (rem >= d) { ++q; rem -= d; }
+}
+
+// counter[key] += (number of consecutive valid lanes from this lane with the same key),
+// issued by the first lane of each run; invalid lanes end runs.  All 64 lanes take part.
+__device__ __forceinline__ void run_add(uint32_t* counter, int key, bool valid, int lane) {
+  const int kp = __shfl_up(key, 1, 64);
+  const unsigned long long V = __ballot(valid);
+  const bool pv = lane > 0 && ((V >> (lane - 1)) & 1ull);   // previous lane in a run
+  const bool lead = valid && (!pv || kp != key);
+  const unsigned long long L = __ballot(lead);
+  if (lead) {
+    const unsigned long long stop =
+        (L | ~V) & (lane == 63 ? 0ull : (~0ull << (lane + 1)));
+    const int nxt = stop ? __builtin_ctzll(stop) : 64;
+    atomicAdd(&counter[key], (uint32_t)(nxt - lane));
+  }
+}
+
+__global__ __launch_bounds__(512) void k_prep_counts(const uint32_t* __restrict__ abits,
+                                                     const int32_t* __restrict__ hidg,
+                                                     const int32_t* __restrict__ nleng,
+                                                     uint32_t* __restrict__ prep, int Ne, int Nc,
+                                                     int TI, int stride, int o_ks, int o_kt,
+                                                     int o_ncst) {
+  extern __shared__ uint32_t hist[];   // [Nc][TI + 1] | class counts [Nc][2] | hid [Ne] |
+                                       // the tile's a-rows [TI][WE] (z = 0)
+  const int z = blockIdx.z, b = blockIdx.y, L0 = blockIdx.x * TI, t = threadIdx.x;
+  const int lane = t & 63;
   const int WE = (Ne + 31) >> 5;
   uint32_t* pb = prep + (size_t)b * stride;
-  uint16_t* ks = (uint16_t*)(pb + o_ks);
-  uint16_t* kt = (uint16_t*)(pb + o_kt);
-  float* ncst = (float*)(pb + o_ncst);
-  uint32_t* ncl = cnt + 2 * CH * Ne;
-  const int32_t* hid = hidg + (size_t)b * Ne;
-  const uint32_t* ab = abits + (size_t)b * Ne * WE;
+  const int TP = TI + 1;               // odd row stride: the hunks of one row / column of the
+                                       // tile fall in different LDS banks
+  uint32_t* ncl = hist + Nc * TP;
+  int32_t* hid = reinterpret_cast<int32_t*>(ncl + 2 * Nc);   // LDS copies: the per-relation
+  uint32_t* ab = ncl + 2 * Nc + Ne;                          // lookups stay on-chip
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   const int nrel = n >= 2 ? n * (n - 1) : 0;
-  for (int c0 = 0; c0 < Nc; c0 += CH) {
-    for (int e = t; e < 2 * CH * Ne; e += 1024) cnt[e] = 0;
-    if (c0 == 0)
-      for (int e = t; e < 2 * Nc; e += 1024) ncl[e] = 0;
-    __syncthreads();
-    for (int r = t; r < nrel; r += 1024) {
-      const int ip = r / (n - 1), jjp = r - ip * (n - 1);
+  const int n1 = n >= 2 ? n - 1 : 1, Ne1 = Ne - 1;
+  const float invn = 1.f / (float)n1, invE = 1.f / (float)(Ne1 > 0 ? Ne1 : 1);
+  const int nl = Ne - L0 < TI ? Ne - L0 : TI;
+  for (int e = t; e < Ne; e += 512) hid[e] = hidg[(size_t)b * Ne + e];
+  if (z == 0)
+    for (int e = t; e < nl * WE; e += 512) ab[e] = abits[((size_t)b * Ne + L0) * WE + e];
+  for (int e = t; e < Nc * TP + 2 * Nc; e += 512) hist[e] = 0;
+  __syncthreads();
+  const int items = nl * Ne1;
+  for (int e0 = 0; e0 < items; e0 += 512) {   // block-uniform trips: every lane takes part
+    const int e = e0 + t;
+    int li = 0, k = 0, I = 0, jj = 0, J = 0;
+    if (e < items) divmod_exact(e, Ne1, invE, li, k);
+    if (z == 0) { I = L0 + li; jj = k; J = jj + (jj >= I ? 1 : 0); }
+    else { J = L0 + li; I = k + (k >= J ? 1 : 0); jj = J - (J > I ? 1 : 0); }
+    const int r = I * Ne1 + jj;
+    const bool in = e < items && r < nrel;
+    int hs = -1, ht = -1, a = 0;
+    if (in) {
+      int ip, jjp;
+      divmod_exact(r, n1, invn, ip, jjp);
       const int jp = jjp + (jjp >= ip ? 1 : 0);
-      const int I = r / (Ne - 1), jj = r - I * (Ne - 1);
-      const int J = jj + (jj >= I ? 1 : 0);
-      const uint32_t a = (ab[I * WE + (J >> 5)] >> (J & 31)) & 1u;
-      const int hs[2] = {hid[ip], hid[jp]};
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int h = hs[q];
-        if (h < 0 || h >= Nc) continue;
-        if (h >= c0 && h < c0 + CH) {
-          atomicAdd(&cnt[(h - c0) * Ne + I], 1u);
-          atomicAdd(&cnt[(CH + h - c0) * Ne + J], 1u);
-        }
-        if (c0 == 0) atomicAdd(&ncl[2 * h + a], 1u);
-      }
+      hs = hid[ip];
+      ht = hid[jp];
+      if (z == 0) a = (int)((ab[li * WE + (J >> 5)] >> (J & 31)) & 1u);
     }
-    __syncthreads();
-    for (int e = t; e < CH * Ne; e += 1024) {
-      if (c0 + e / Ne < Nc) {
-        ks[(size_t)c0 * Ne + e] = (uint16_t)cnt[e];
-        kt[(size_t)c0 * Ne + e] = (uint16_t)cnt[CH * Ne + e];
-      }
+    const bool vs = hs >= 0 && hs < Nc, vt = ht >= 0 && ht < Nc;
+    run_add(hist, vs ? hs * TP + li : 0, vs, lane);
+    run_add(hist, vt ? ht * TP + li : 0, vt, lane);
+    if (z == 0) {
+      run_add(ncl, vs ? 2 * hs + a : 0, vs, lane);
+      run_add(ncl, vt ? 2 * ht + a : 0, vt, lane);
     }
-    __syncthreads();
   }
-  for (int e = t; e < 2 * Nc; e += 1024) ncst[e] = (float)ncl[e];
+  __syncthreads();
+  uint16_t* out = (uint16_t*)(pb + (z ? o_kt : o_ks));
+  for (int e = t; e < Nc * TI; e += 512) {
+    const int c = e / TI, i = e - c * TI;
+    if (i < nl) out[(size_t)c * Ne + L0 + i] = (uint16_t)hist[c * TP + i];
+  }
+  if (z == 0) {
+    uint32_t* nc = pb + o_ncst;
+    for (int e = t; e < 2 * Nc; e += 512)
+      if (ncl[e]) atomicAdd(&nc[e], ncl[e]);
+  }
+}
+
+// grid (B): mode 0 zeroes the class-count words of each commit, mode 1 turns the summed
+// u32 counts into the f32 values the step kernels read (exact: counts < 2^24)
+__global__ __launch_bounds__(256) void k_prep_ncst(uint32_t* __restrict__ prep, int Nc,
+                                                   int stride, int o_ncst, int mode) {
+  uint32_t* nc = prep + (size_t)blockIdx.x * stride + o_ncst;
+  for (int e = threadIdx.x; e < 2 * Nc; e += 256) {
+    if (mode == 0) nc[e] = 0u;
+    else nc[e] = __float_as_uint((float)nc[e]);
+  }
 }
 
 // ------------------------------------------------------------------------------
@@ -1423,7 +1480,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   MID_STAMP();
 
   // ---- M3: marshalling_B2 (model_2.py:146-150) as two count-matrix matvecs -----------
-  //   n_c = [sum_I ks[c][I] x'_I, sum_J kt[c][J] x'_J, ncst[c][0], ncst[c][1]]  (k_prep_maps)
+  //   n_c = [sum_I ks[c][I] x'_I, sum_J kt[c][J] x'_J, ncst[c][0], ncst[c][1]]  (k_prep_counts)
   {
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
@@ -2389,11 +2446,16 @@ Work work_layout(const hdg_shape* s) {
   return w;
 }
 
-constexpr int PREP_LDS_WORDS = 36 * 1024;   // k_prep_maps count chunk (144 KiB)
-
-int prep_chunk(int ne, int nc) {
-  int ch = (PREP_LDS_WORDS - 2 * nc) / (2 * ne);
-  return ch < nc ? ch : nc;
+// k_prep_counts tile width: TI Ne-rows / -columns per block (<= 64 KiB of counters where
+// possible, two blocks per CU), and the LDS words it needs
+int prep_lds_words(int ne, int nc, int ti) {
+  return (ti + 1) * nc + 2 * nc + ne + ti * ((ne + 31) / 32);
+}
+int prep_tile(int ne, int nc) {
+  int ti = 64;
+  while (ti > 16 && ti * nc > 16384) ti >>= 1;
+  while (ti > 1 && prep_lds_words(ne, nc, ti) > 38 * 1024) ti >>= 1;
+  return ti;
 }
 
 }  // namespace
@@ -2414,16 +2476,22 @@ hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride,
                             int o_kt, int o_ncst, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_prep_maps,
+    const hipError_t e = hipFuncSetAttribute((const void*)k_prep_counts,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int ch = prep_chunk(s->ne, s->nc);
-  const size_t lds = (size_t)(2 * ch * s->ne + 2 * s->nc) * 4;
-  hipLaunchKernelGGL(k_prep_maps, dim3(s->batch), dim3(1024), lds, st, bt->abits, bt->hid,
-                     bt->nlen, (uint32_t*)bt->prep, s->ne, s->nc, ch, stride, o_ks, o_kt, o_ncst);
+  const int ti = prep_tile(s->ne, s->nc);
+  const size_t lds = (size_t)prep_lds_words(s->ne, s->nc, ti) * 4;
+  uint32_t* prep = (uint32_t*)bt->prep;
+  hipLaunchKernelGGL(k_prep_ncst, dim3(s->batch), dim3(256), 0, st, prep, s->nc, stride, o_ncst,
+                     0);
+  hipLaunchKernelGGL(k_prep_counts, dim3((s->ne + ti - 1) / ti, s->batch, 2), dim3(512), lds, st,
+                     bt->abits, bt->hid, bt->nlen, prep, s->ne, s->nc, ti, stride, o_ks, o_kt,
+                     o_ncst);
+  hipLaunchKernelGGL(k_prep_ncst, dim3(s->batch), dim3(256), 0, st, prep, s->nc, stride, o_ncst,
+                     1);
   return hipGetLastError();
 }
 

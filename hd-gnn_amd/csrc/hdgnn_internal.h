@@ -30,7 +30,7 @@ constexpr int HS = 20;   // h_size = De_e = De_er (model_2.py:163, 192, 247, 306
 //   xoffr, xoffc offsets (in elements, multiples of 4) of each node's neighbour list in xl
 //   xl           f32 x_j of the a = 1 neighbours j of each node, row lists then column
 //                lists, each padded with NaN to a multiple of 4 (16-byte vector reads)
-//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_maps)
+//   ks, kt       [Nc][Ne] u16 cross-graph counts (k_prep_counts)
 //   ncst[Nc][2]  f32 count of relations binned to hunk c with a = 0 / a = 1
 // The general path has its own per-commit layout (wide.hip, GenPrep): ks / kt / ncst as
 // here, transposed class bits, and the sorted-x tables without the byte neighbour lists.

@@ -174,7 +174,7 @@ enum : int {
 };
 
 // Prepared batch of the general path, per commit (words): cross-graph counts as in the
-// fused layout, then the sorted-x tables of the entity stages (k_prep_maps, kw_prep_sort):
+// fused layout, then the sorted-x tables of the entity stages (k_prep_counts, kw_prep_sort):
 //   ks, kt [Nc][Ne] u16   ncst [Nc][2] f32   xsrt [NE4] x ascending   perm [NE4] node of slot
 //   xu [NE4] distinct values   cum [NE4+4] #nodes with x < xu[q]   pxd [NE4+4] f64 sums
 //   meta[4] = {nd}

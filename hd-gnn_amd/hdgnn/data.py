@@ -118,7 +118,9 @@ class DeviceBatch:
         nbytes = lib.hdg_prep_bytes(ctypes.byref(shape))
         if nbytes == 0:
             raise ValueError(lib.hdg_last_error().decode())
-        self.prep = torch.empty(nbytes // 4, dtype=torch.int32, device=x.device)
+        # zeroed: words no table covers (padding) are deterministic, so two preparations
+        # of one batch compare bytewise (tools/prep_dump.py)
+        self.prep = torch.zeros(nbytes // 4, dtype=torch.int32, device=x.device)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         _lib.check(lib.hdg_prepare(ctypes.byref(shape), ctypes.byref(self.struct()),
                                    ctypes.c_void_p(stream)))

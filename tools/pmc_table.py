@@ -2,7 +2,7 @@ import csv, glob, os, sys
 from collections import defaultdict
 out = sys.argv[1]
 def short(n):
-    for k in ("k_commit_step", "k_grad_reduce", "k_adam_tf", "k_prep_sort", "k_prep_maps"):
+    for k in ("k_commit_step", "k_grad_reduce", "k_adam_tf", "k_prep_sort", "k_prep_counts"):
         if k in n:
             return k
     return None

@@ -21,7 +21,7 @@ def find(pattern):
 
 
 def short(name):
-    for k in ("k_commit_step", "k_grad_reduce", "k_adam_tf", "k_prep_sort", "k_prep_maps"):
+    for k in ("k_commit_step", "k_grad_reduce", "k_adam_tf", "k_prep_sort", "k_prep_counts"):
         if k in name:
             return k
     return name[:60]
