@@ -2656,6 +2656,22 @@ size_t hdg_prep_bytes(const hdg_shape* shape) {
   return (size_t)shape->batch * prep_layout(shape->ne, shape->nc).words * 4;
 }
 
+int hdg_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
+                           int64_t* ncst) {
+  RESOLVE(s, path);
+  if (!stride || !ks || !kt || !ncst) return fail(HDG_EINVAL, "NULL output pointer");
+  if (path == HDG_PATH_GENERAL) {
+    hdg::wide_prep_counts_layout(s, stride, ks, kt, ncst);
+    return 0;
+  }
+  const PrepLayout L = prep_layout(s->ne, s->nc);
+  *stride = L.words;
+  *ks = L.ks;
+  *kt = L.kt;
+  *ncst = L.ncst;
+  return 0;
+}
+
 int hdg_prepare(const hdg_shape* s, const hdg_batch* bt, void* stream) {
   RESOLVE(s, path);
   if (int rc = check_batch(bt)) return rc;

@@ -81,6 +81,8 @@ Off param_offsets(int variant);   // NP = -1 for an unknown variant
 // general path (wide.hip)
 size_t wide_workspace_bytes(const hdg_shape* s);
 size_t wide_prep_bytes(const hdg_shape* s);
+void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
+                             int64_t* ncst);
 int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
 // train: forward + backward -> grad[NP + 4] (slot NP = CE sum); !train: forward only,
 // CE sum -> *ce_sum (may be NULL).  Outputs as in hdg_fwd_bwd.

@@ -2060,6 +2060,15 @@ WideWork wide_layout(const hdg_shape* s) {
 
 size_t wide_workspace_bytes(const hdg_shape* s) { return wide_layout(s).total * sizeof(float); }
 
+void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
+                             int64_t* ncst) {
+  const GenPrep GP = gen_prep(s->ne, s->nc);
+  *stride = GP.words;
+  *ks = GP.ks;
+  *kt = GP.kt;
+  *ncst = GP.ncst;
+}
+
 size_t wide_prep_bytes(const hdg_shape* s) {
   const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
   return (B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;

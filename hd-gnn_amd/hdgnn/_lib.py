@@ -41,7 +41,7 @@ class Outputs(ctypes.Structure):
 EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count", "hdg_grad_len",
            "hdg_workspace_bytes", "hdg_prep_bytes", "hdg_prepare", "hdg_fwd_bwd",
            "hdg_fwd_bwd_events", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
-           "hdg_debug_step_stamps"]
+           "hdg_debug_step_stamps", "hdg_prep_counts_layout"]
 
 _lib = None
 
@@ -68,6 +68,8 @@ def load(path=None):
     lib.hdg_workspace_bytes.restype = ctypes.c_size_t
     lib.hdg_prep_bytes.argtypes = [P(Shape)]
     lib.hdg_prep_bytes.restype = ctypes.c_size_t
+    lib.hdg_prep_counts_layout.argtypes = [P(Shape)] + [P(ctypes.c_int64)] * 4
+    lib.hdg_prep_counts_layout.restype = ctypes.c_int
     lib.hdg_prepare.argtypes = [P(Shape), P(Batch), vp]
     lib.hdg_fwd_bwd.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp]
     lib.hdg_fwd_bwd_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp, vp]

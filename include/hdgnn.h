@@ -107,6 +107,13 @@ int         hdg_grad_len(int32_t variant);
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
 /* bytes of batch->prep for this shape (0 on a shape error) */
 size_t      hdg_prep_bytes(const hdg_shape* shape);
+/* Where hdg_prepare puts the cross-graph count tables of commit b inside batch->prep
+ * (4-byte words from prep + b * stride_words): K_s at ks, K_t at kt (u16 [Nc][Ne]),
+ * class counts at ncst (f32 [Nc][2]).  K_s = (Esc + Etc) . Es^T and K_t = (Esc + Etc) .
+ * Et^T of utils2.py:111-137 (the marshalling_B2 maps, model_2.py:146-150), so tests can
+ * check the index bookkeeping bit-exactly.  0, or an error code on a shape error.    */
+int         hdg_prep_counts_layout(const hdg_shape* shape, int64_t* stride_words,
+                                   int64_t* ks, int64_t* kt, int64_t* ncst);
 
 /* Build batch->prep from x / abits / hid / nlen (the parameter-independent per-commit
  * tables the step kernel reads).  Call once after uploading a batch, before any step;

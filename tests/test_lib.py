@@ -65,3 +65,22 @@ def test_host_only_entry_points():
     bad_v = _lib.Shape(4, 20, 10, 5, 4, 0)
     assert lib.hdg_workspace_bytes(ctypes.byref(bad_v)) == 0
     assert b"variant" in lib.hdg_last_error()
+
+
+def test_prep_counts_layout_host():
+    """hdg_prep_counts_layout: the count tables sit inside each commit's prep block."""
+    from hdgnn import _lib
+    lib = _lib.load()
+    for v, ne, nc, path in ((2, 200, 74, 0), (2, 250, 150, 0), (4, 200, 74, 0),
+                            (2, 1024, 512, 0), (2, 200, 74, _lib.PATH_GENERAL)):
+        sh = _lib.Shape(8, ne, nc, v, 8, path)
+        st, ks, kt, ncst = (ctypes.c_int64() for _ in range(4))
+        assert lib.hdg_prep_counts_layout(ctypes.byref(sh), ctypes.byref(st), ctypes.byref(ks),
+                                          ctypes.byref(kt), ctypes.byref(ncst)) == 0
+        kw = (nc * ne + 1) // 2                       # u16 [Nc][Ne] in words
+        assert 0 <= ks.value and ks.value + kw <= kt.value or kt.value + kw <= ks.value
+        assert max(ks.value, kt.value) + kw <= st.value and ncst.value + 2 * nc <= st.value
+        assert 8 * st.value * 4 <= lib.hdg_prep_bytes(ctypes.byref(sh))
+    bad = _lib.Shape(4, 5000, 74, 2, 4, 0)
+    z = ctypes.c_int64()
+    assert lib.hdg_prep_counts_layout(ctypes.byref(bad), *(ctypes.byref(z) for _ in range(4))) != 0
