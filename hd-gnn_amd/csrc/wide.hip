@@ -1815,43 +1815,81 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   const size_t base = ((size_t)b * Ne + t0) * H;
   stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
   stage_w(Wl + 400, W + o.EE_W2, 400);
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, k = e - n * H;
+  // staging: every element's loads issued before the first use (NE_IT elements per thread;
+  // the te row partials of drho four tiles at a time, summed in tile order)
+  constexpr int NE_IT = TN * H / NT;
+  static_assert(TN * H % NT == 0, "kw_ee_nodeb staging");
+  float dr[NE_IT];
+#pragma unroll
+  for (int it = 0; it < NE_IT; ++it) {
+    const int e = t + it * NT, n = e / H, k = e - n * H;
     const bool in = t0 + n < Ne;
-    float dr = 0.f;                                   // the te row partials, tile order
-    if (in)
-      for (int q = 0; q < te; ++q) dr += drho[((size_t)(b * te + q) * Ne + t0) * H + e];
-    A[n * HP + k] = dr;
+    dr[it] = 0.f;
     Bq[n * HP + k] = in ? dgam[base + e] : 0.f;
     R1t[n * HP + k] = in ? R1[base + e] : 0.f;
     C1t[n * HP + k] = in ? C1[base + e] : 0.f;
     Rt[n * HP + k] = in ? Rn[base + e] : 0.f;
     Ct[n * HP + k] = in ? Cn[base + e] : 0.f;
   }
-  __syncthreads();
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, m = e - n * H;
-    float a = 0.f, c = 0.f;
-    for (int k = 0; k < H; ++k) {
-      const float u = U1e[m * H + k];
-      a = fmaf(u, A[n * HP + k], a);
-      c = fmaf(u, Bq[n * HP + k], c);
+  {
+    const float* src = drho + ((size_t)b * te * Ne + t0) * H + t;
+    const size_t sq = (size_t)Ne * H;
+    const int nin = (Ne - t0) * H;                    // elements e < nin are in range
+    int q = 0;
+    for (; q + 4 <= te; q += 4) {
+      float v[NE_IT][4];
+#pragma unroll
+      for (int it = 0; it < NE_IT; ++it)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          v[it][u] = (t + it * NT < nin) ? src[(q + u) * sq + it * NT] : 0.f;
+#pragma unroll
+      for (int it = 0; it < NE_IT; ++it)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dr[it] += v[it][u];
     }
-    dR[n * HP + m] = a;
-    dC[n * HP + m] = c;
+    for (; q < te; ++q)
+#pragma unroll
+      for (int it = 0; it < NE_IT; ++it)
+        if (t + it * NT < nin) dr[it] += src[q * sq + it * NT];
+  }
+#pragma unroll
+  for (int it = 0; it < NE_IT; ++it) {
+    const int e = t + it * NT, n = e / H, k = e - n * H;
+    A[n * HP + k] = dr[it];
   }
   __syncthreads();
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, l = e - n * H;
-    if (t0 + n >= Ne) continue;
-    float a = 0.f, c = 0.f;
-    for (int m = 0; m < H; ++m) {
-      const float q = Q2[l * H + m];
-      a = fmaf(q, dR[n * HP + m], a);
-      c = fmaf(q, dC[n * HP + m], c);
+  const int lane = t & 63;
+  // dR = A U1e^T, dC = Bq U1e^T, then phi = dR Q2^T, psi = dC Q2^T over the tile's 64
+  // nodes as 16x16 MFMA tiles (4 node tiles x 2 column tiles per product, K = 20); columns
+  // >= H read the zero word kz with stride 0 and are not stored
+  for (int tile = t >> 6; tile < 16; tile += NT / 64) {     // wave-uniform
+    const int which = tile >> 3, n0 = ((tile >> 1) & 3) * 16, m0 = (tile & 1) * 16;
+    const int mc = m0 + (lane & 15);
+    const bool cv = mc < H;
+    const f4v c = mfma_tile16_p((which ? Bq : A) + (n0 + (lane & 15)) * HP, 1,
+                                cv ? U1e + mc * H : kz, cv ? 1 : 0, H, lane);
+    if (cv) {
+      float* d = which ? dC : dR;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[(n0 + 4 * (lane >> 4) + j) * HP + mc] = c[j];
     }
-    phi[base + e] = a;
-    psi[base + e] = c;
+  }
+  __syncthreads();
+  for (int tile = t >> 6; tile < 16; tile += NT / 64) {
+    const int which = tile >> 3, n0 = ((tile >> 1) & 3) * 16, l0 = (tile & 1) * 16;
+    const int lc = l0 + (lane & 15);
+    const bool cv = lc < H;
+    const f4v c = mfma_tile16_p((which ? dC : dR) + (n0 + (lane & 15)) * HP, 1,
+                                cv ? Q2 + lc * H : kz, cv ? 1 : 0, H, lane);
+    if (cv) {
+      float* d = which ? psi : phi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + 4 * (lane >> 4) + j;
+        if (t0 + n < Ne) d[base + n * H + lc] = c[j];
+      }
+    }
   }
   const int row = b * te + blockIdx.x;
   const Seg& s1 = sg.s[SG_ECW1E];
@@ -1859,7 +1897,6 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   const float Ne1 = (float)(Ne - 1);
   // dU1e' = Rt^T A + Ct^T Bq and dQ2 = R1t^T dR + C1t^T dC over the tile's 64 nodes as
   // 16x16 MFMA tiles (2 x 2 per matrix, one wave per two tiles); dq2 on the VALU
-  const int lane = t & 63;
   for (int tile = t >> 6; tile < 8; tile += NT / 64) {      // wave-uniform
     const int which = tile >> 2, row0 = ((tile >> 1) & 1) * 16, col0 = (tile & 1) * 16;
     const int ra = row0 + (lane & 15), cb = col0 + (lane & 15);
