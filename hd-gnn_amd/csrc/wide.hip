@@ -581,6 +581,24 @@ __global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
 //   EE  (model_4.py:232-243, 282-304): R = R1 Q2 + (Ne-1) q2, C = C1 Q2 + (Ne-1) q2;
 //        classifier first-layer operands rho = R U1e' + U1'[0] + b1', gam = C U1e'
 // ---------------------------------------------------------------------------------
+// 64 x 20 row-block products on MFMA: f(n, k, c) with c = sum_m As[n][m] Wm[m][k] for the
+// tile's 64 rows (As [64][HP] in LDS, Wm [H][H] row-major in LDS); 4 x 2 16x16 tiles over
+// the block's waves; columns >= H read the zero word kz with stride 0 and are not passed on
+template <class F>
+__device__ __forceinline__ void rows_x_w(const float* As, const float* Wm, const float* kz,
+                                         F f) {
+  const int lane = threadIdx.x & 63;
+  for (int tile = threadIdx.x >> 6; tile < 8; tile += NT / 64) {   // wave-uniform
+    const int n0 = (tile >> 1) * 16, kc = (tile & 1) * 16 + (lane & 15);
+    const bool cv = kc < H;
+    const f4v c = mfma_tile16_p(As + (n0 + (lane & 15)) * HP, 1, cv ? Wm + kc : kz, cv ? H : 0,
+                                H, lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f(n0 + 4 * (lane >> 4) + j, kc, c[j]);
+  }
+}
+
 __global__ __launch_bounds__(NT) void kw_node_fwd(
     const float* __restrict__ x, const float* __restrict__ W, Off o, int Ne, int ent,
     const float* __restrict__ P, float* __restrict__ Eb, float* __restrict__ hE,
@@ -589,33 +607,31 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
     float* __restrict__ rho, float* __restrict__ gmm) {
   __shared__ float A[TN * HP], Bs[TN * HP], Cs[TN * HP], Ds[TN * HP];
   __shared__ float Wl[896];                       // the block's weights, staged once
+  __shared__ float kz[1];                         // 0.f: stride-0 operand of padding tiles
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x;
   const int nn = Ne - t0 < TN ? Ne - t0 : TN;
   const size_t base = ((size_t)b * Ne + t0) * H;
   const float Ne1 = (float)(Ne - 1);
+  if (t == 0) kz[0] = 0.f;
+  // rows n >= nn of the LDS tiles are never stored (MFMA rows are independent)
   if (blockIdx.z == 0 && ent) {
     const float *W5 = Wl, *B5 = Wl + 400, *W1e = Wl + 420, *B1e = Wl + 840, *W2e = Wl + 860;
     stage_w(Wl, W + o.E1_W5, 420);                // W5 | b5
     stage_w(Wl + 420, W + o.E3_W1, 461);          // W1' | b1' | w2' | b2'
     for (int e = t; e < nn * H; e += NT) A[(e / H) * HP + e % H] = P[base + e];
     __syncthreads();
-    for (int e = t; e < nn * H; e += NT) {
-      const int n = e / H, k = e - n * H;
-      float acc = 0.f;
-      for (int m = 0; m < H; ++m) acc = fmaf(A[n * HP + m], W5[m * H + k], acc);
-      acc += (2.f * Ne1) * B5[k];
-      Bs[n * HP + k] = acc;
-      Eb[base + e] = acc;
-    }
+    rows_x_w(A, W5, kz, [&](int n, int k, float c) {   // E_bar = P W5 + 2 (Ne-1) b5
+      const float v = c + (2.f * Ne1) * B5[k];
+      Bs[n * HP + k] = v;
+      if (n < nn) Eb[base + n * H + k] = v;
+    });
     __syncthreads();
-    for (int e = t; e < nn * H; e += NT) {
-      const int n = e / H, k = e - n * H;
-      float acc = x[(size_t)b * Ne + t0 + n] * W1e[k];
-      for (int m = 0; m < H; ++m) acc = fmaf(Bs[n * HP + m], W1e[(1 + m) * H + k], acc);
-      const float v = relu(acc + B1e[k]);
+    rows_x_w(Bs, W1e + H, kz, [&](int n, int k, float c) {   // h = relu(x W1'[0] + E_bar W1'[1:] + b1')
+      const float xv = n < nn ? x[(size_t)b * Ne + t0 + n] : 0.f;
+      const float v = relu(fmaf(xv, W1e[k], c) + B1e[k]);
       Cs[n * HP + k] = v;
-      hE[base + e] = v;
-    }
+      if (n < nn) hE[base + n * H + k] = v;
+    });
     __syncthreads();
     for (int n = t; n < nn; n += NT) {
       float acc = Wl[880];
@@ -633,32 +649,23 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
     Bs[(e / H) * HP + e % H] = C1[base + e];
   }
   __syncthreads();
-  for (int e = t; e < nn * H; e += NT) {
-    const int n = e / H, k = e - n * H;
-    float ar = 0.f, ac = 0.f;
-    for (int m = 0; m < H; ++m) {
-      const float q = Q2[m * H + k];
-      ar = fmaf(A[n * HP + m], q, ar);
-      ac = fmaf(Bs[n * HP + m], q, ac);
-    }
-    const float qb = Ne1 * q2[k];
-    Cs[n * HP + k] = ar + qb;
-    Ds[n * HP + k] = ac + qb;
-    Rn[base + e] = ar + qb;
-    Cn[base + e] = ac + qb;
-  }
+  rows_x_w(A, Q2, kz, [&](int n, int k, float c) {      // R = R1 Q2 + (Ne-1) q2
+    const float v = c + Ne1 * q2[k];
+    Cs[n * HP + k] = v;
+    if (n < nn) Rn[base + n * H + k] = v;
+  });
+  rows_x_w(Bs, Q2, kz, [&](int n, int k, float c) {     // C = C1 Q2 + (Ne-1) q2
+    const float v = c + Ne1 * q2[k];
+    Ds[n * HP + k] = v;
+    if (n < nn) Cn[base + n * H + k] = v;
+  });
   __syncthreads();
-  for (int e = t; e < nn * H; e += NT) {
-    const int n = e / H, k = e - n * H;
-    float ar = 0.f, ac = 0.f;
-    for (int m = 0; m < H; ++m) {
-      const float q = P1[(2 + m) * H + k];
-      ar = fmaf(Cs[n * HP + m], q, ar);
-      ac = fmaf(Ds[n * HP + m], q, ac);
-    }
-    rho[base + e] = ar + (P1[k] + p1b[k]);
-    gmm[base + e] = ac;
-  }
+  rows_x_w(Cs, P1 + 2 * H, kz, [&](int n, int k, float c) {   // rho = R U1'[2:] + U1'[0] + b1'
+    if (n < nn) rho[base + n * H + k] = c + (P1[k] + p1b[k]);
+  });
+  rows_x_w(Ds, P1 + 2 * H, kz, [&](int n, int k, float c) {   // gam = C U1'[2:]
+    if (n < nn) gmm[base + n * H + k] = c;
+  });
 }
 
 // ---------------------------------------------------------------------------------
