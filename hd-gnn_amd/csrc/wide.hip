@@ -584,15 +584,17 @@ __global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
 // 64 x 20 row-block products on MFMA: f(n, k, c) with c = sum_m As[n][m] Wm[m][k] for the
 // tile's 64 rows (As [64][HP] in LDS, Wm [H][H] row-major in LDS); 4 x 2 16x16 tiles over
 // the block's waves; columns >= H read the zero word kz with stride 0 and are not passed on
-template <class F>
+// (Wm element (m, k) at Wm[m * SM + k * SK]: SM = H, SK = 1 row-major, SM = 1, SK = H for
+// the transposed weight)
+template <int SM = H, int SK = 1, class F>
 __device__ __forceinline__ void rows_x_w(const float* As, const float* Wm, const float* kz,
                                          F f) {
   const int lane = threadIdx.x & 63;
   for (int tile = threadIdx.x >> 6; tile < 8; tile += NT / 64) {   // wave-uniform
     const int n0 = (tile >> 1) * 16, kc = (tile & 1) * 16 + (lane & 15);
     const bool cv = kc < H;
-    const f4v c = mfma_tile16_p(As + (n0 + (lane & 15)) * HP, 1, cv ? Wm + kc : kz, cv ? H : 0,
-                                H, lane);
+    const f4v c = mfma_tile16_p(As + (n0 + (lane & 15)) * HP, 1, cv ? Wm + kc * SK : kz,
+                                cv ? SM : 0, H, lane);
     if (cv)
 #pragma unroll
       for (int j = 0; j < 4; ++j) f(n0 + 4 * (lane >> 4) + j, kc, c[j]);
@@ -1323,7 +1325,9 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   __shared__ float dxq[NW * TN], xs[TN], dov[TN];
   __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
   __shared__ float Wl[864];
+  __shared__ float kzr[1];                        // 0.f: stride-0 operand of padding tiles
   const float *W1e = Wl, *W2e = Wl + 440, *W5 = Wl + 464;   // W1' (21 x 20) | b1' | w2' | b2' | W5
+  if (threadIdx.x == 0) kzr[0] = 0.f;
   const GenPrep PL = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
   const int lane = t & 63, w = t >> 6;
@@ -1337,11 +1341,28 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     const float* dnb = dn + (size_t)b * Nc * 4;
     const int c0 = (Nc * w) / NW, c1 = (Nc * (w + 1)) / NW;
     float a = 0.f;
-    if (I < Ne)
-      for (int c = c0; c < c1; ++c) {
+    if (I < Ne) {                  // four hunks' counts in flight per step, same fma order
+      int c = c0;
+      for (; c + 4 <= c1; c += 4) {
+        float vs[4], vt[4], d0[4], d1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          vs[u] = (float)ks[(size_t)(c + u) * Ne + I];
+          vt[u] = (float)kt[(size_t)(c + u) * Ne + I];
+          d0[u] = dnb[4 * (c + u)];
+          d1[u] = dnb[4 * (c + u) + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a = fmaf(d0[u], vs[u], a);
+          a = fmaf(d1[u], vt[u], a);
+        }
+      }
+      for (; c < c1; ++c) {
         a = fmaf(dnb[4 * c], (float)ks[(size_t)c * Ne + I], a);
         a = fmaf(dnb[4 * c + 1], (float)kt[(size_t)c * Ne + I], a);
       }
+    }
     dxq[w * TN + lane] = a;
   }
   const size_t base = ((size_t)b * Ne + t0) * H;
@@ -1365,20 +1386,12 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     dq[n * HP + k] = ht[n * HP + k] > 0.f ? W2e[k] * dov[n] : 0.f;
   }
   __syncthreads();
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, m = e - n * H;
-    float a = 0.f;
-    for (int k = 0; k < H; ++k) a = fmaf(dq[n * HP + k], W1e[(1 + m) * H + k], a);
-    dE[n * HP + m] = a;
-  }
+  // dE = dq W1'[1:]^T, rho_E = dE W5^T as MFMA tiles (transposed weights: SM = 1, SK = H)
+  rows_x_w<1, H>(dq, W1e + H, kzr, [&](int n, int m, float c) { dE[n * HP + m] = c; });
   __syncthreads();
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, l = e - n * H;
-    if (t0 + n >= Ne) continue;
-    float a = 0.f;
-    for (int m = 0; m < H; ++m) a = fmaf(dE[n * HP + m], W5[l * H + m], a);
-    rhoE[base + e] = a;
-  }
+  rows_x_w<1, H>(dE, W5, kzr, [&](int n, int l, float c) {
+    if (t0 + n < Ne) rhoE[base + n * H + l] = c;
+  });
   const int row = b * te + blockIdx.x;
   const Seg& s3 = sg.s[SG_E3];
   const Seg& s5 = sg.s[SG_E1W5];
