@@ -1396,13 +1396,30 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   const Seg& s3 = sg.s[SG_E3];
   const Seg& s5 = sg.s[SG_E1W5];
   const float twoNe1 = 2.f * (float)(Ne - 1);
-  for (int e = t; e < 461 + 420; e += NT) {
+  // dW1'[l][k] = sum_n X[n][l] dq[n][k] (X = [x | E_bar], 21 rows) and dW5[l][m] =
+  // sum_n P[n][l] dE[n][m] over the tile's 64 nodes as 16x16 MFMA tiles (2 x 2 each)
+  for (int tile = t >> 6; tile < 8; tile += NT / 64) {      // wave-uniform
+    const int which = tile >> 2, r0 = ((tile >> 1) & 1) * 16, cc = (tile & 1) * 16 + (lane & 15);
+    const int rl = r0 + (lane & 15);
+    const bool cv = cc < H, rv = rl < (which ? H : H + 1);
+    const float* pa = kzr;
+    int sa = 0;
+    if (rv) {
+      if (which) { pa = Pt + rl; sa = HP; }
+      else if (rl == 0) { pa = xs; sa = 1; }
+      else { pa = Et + rl - 1; sa = HP; }
+    }
+    const f4v c = mfma_tile16_p(pa, sa, cv ? (which ? dE : dq) + cc : kzr, cv ? HP : 0, TN, lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = r0 + 4 * (lane >> 4) + j;
+        if (rr < (which ? H : H + 1)) put(part, which ? s5 : s3, rr * H + cc, row, c[j]);
+      }
+  }
+  for (int e = 420 + t; e < 461 + 420; e += NT) {
     float a = 0.f;
-    if (e < 420) {                 // dW1'[l][k]: l = 0 -> x, l >= 1 -> E_bar[l-1]
-      const int l = e / H, k = e - l * H;
-      for (int n = 0; n < TN; ++n) a = fmaf(l ? Et[n * HP + l - 1] : xs[n], dq[n * HP + k], a);
-      put(part, s3, e, row, a);
-    } else if (e < 440) {          // db1'
+    if (e < 440) {                 // db1'
       const int k = e - 420;
       for (int n = 0; n < TN; ++n) a += dq[n * HP + k];
       put(part, s3, e, row, a);
@@ -1415,14 +1432,10 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
       put(part, s3, e, row, a);
     } else {
       const int f = e - 461;
-      if (f < 400) {               // dW5[l][m] = sum_n P[n][l] dE[n][m]
-        const int l = f / H, m = f - l * H;
-        for (int n = 0; n < TN; ++n) a = fmaf(Pt[n * HP + l], dE[n * HP + m], a);
-      } else {                     // db5[m] = 2(Ne-1) sum_n dE[n][m]
-        const int m = f - 400;
-        for (int n = 0; n < TN; ++n) a += dE[n * HP + m];
-        a *= twoNe1;
-      }
+      if (f < 400) continue;       // dW5: MFMA tiles above
+      const int m = f - 400;       // db5[m] = 2(Ne-1) sum_n dE[n][m]
+      for (int n = 0; n < TN; ++n) a += dE[n * HP + m];
+      a *= twoNe1;
       put(part, s5, f, row, a);
     }
   }
