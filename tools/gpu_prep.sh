@@ -1,4 +1,5 @@
-# GPU box: prepared tables of the current build vs a reference build (libhdgnn_old.so),
+# GPU box: prepared tables of the current build vs a reference build (copy the older
+# libhdgnn.so to hd-gnn_amd/csrc/libhdgnn_old.so first),
 # bytewise; then the GPU parity tests and a kernel trace of the stress prepare.
 set -o pipefail
 mkdir -p gpurun_out/prep
