@@ -1057,6 +1057,8 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
   __shared__ float X[H * H], sumD[H], ysum[H];
   __shared__ float Wl[3 * H * H + H];
+  __shared__ float kzh[1];                        // 0.f: stride-0 operand of padding tiles
+  if (threadIdx.x == 0) kzh[0] = 0.f;
   const float *Ml = Wl, *V2 = Wl + H * H, *c2 = Wl + 2 * H * H, *U1e = Wl + 2 * H * H + H;
   stage_w(Wl, D + D_M, H * H);                    // visible after the first chunk barrier
   stage_w(Wl + H * H, W + o.H1_W2, H * H + H);    // V2 | c2
@@ -1136,11 +1138,18 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     for (int k = 0; k < H; ++k) sacc = fmaf(Ml[l * H + k], res[n * HP + k], sacc);
     gout[(t0 + n) * H + l] = sacc;
   }
-  for (int e = threadIdx.x; e < H * H; e += NTP) {    // X_blk = sum_n G_n (x) D_n
-    const int l = e / H, k = e - l * H;
-    float sacc = 0.f;
-    for (int n = 0; n < TN; ++n) sacc = fmaf(Gt[n * HP + l], res[n * HP + k], sacc);
-    X[e] = sacc;
+  if (threadIdx.x < 256) {   // X_blk = sum_n G_n (x) D_n: 2 x 2 16x16 MFMA tiles, K = 64 nodes
+    const int lane = threadIdx.x & 63, tile = threadIdx.x >> 6;   // wave-uniform
+    const int rl = (tile >> 1) * 16 + (lane & 15), kc = (tile & 1) * 16 + (lane & 15);
+    const bool rv = rl < H, cv = kc < H;
+    const f4v c = mfma_tile16_p(rv ? Gt + rl : kzh, rv ? HP : 0, cv ? res + kc : kzh,
+                                cv ? HP : 0, TN, lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = (tile >> 1) * 16 + 4 * (lane >> 4) + j;
+        if (rr < H) X[rr * H + kc] = c[j];
+      }
   }
   if (threadIdx.x < H) {
     const int k = threadIdx.x;
