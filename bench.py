@@ -167,6 +167,7 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
+    eng.check_status()             # a failed launch (exchange timeout) voids the run: raise
     if launched:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

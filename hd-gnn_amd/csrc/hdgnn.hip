@@ -47,8 +47,8 @@ constexpr int H1_W1 = 981, H1_B1 = 1181, H1_W2 = 1201, H1_B2 = 1601;
 constexpr int H2_W1 = 1621, H2_B1 = 2061, H2_W2 = 2081, H2_B2 = 2121;
 constexpr int TH1 = 2123, TH2 = 2125, NP = 2127;
 }  // namespace m2
-constexpr int NPART = 2132;        // per-commit partial row: NP grads + CE sum, padded
-constexpr int GRAD_LEN = m2::NP + 4;
+constexpr int GRAD_LEN = m2::NP + HDG_TRAILER;
+constexpr int NPART = (GRAD_LEN + 3) & ~3;   // per-block partial row: NP grads + trailer
 
 // ------------------------------------------------------------------------------
 // cross-lane helpers (wave64)
@@ -1133,10 +1133,12 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
 // coherent; an agent-scope release writes back the whole dirty L2, 5-11 us,
 // tools/probe/xchg2.hip).  The receiver polls its own inbox with L2-bypassing loads
 // (sc0 sc1) until both tags match (1.6 us per 1480-value exchange measured, hidden behind
-// independent work between send and receive); tags change every launch (xtag).  The pair is co-resident by construction (host:
-// 2 B blocks <= CUs, one block per CU); a partner that never arrives ends the wait after
-// ~20 ms and poisons the CE slot with NaN (loud, no hang).  v must not change between
-// send and receive; n is even.
+// independent work between send and receive); tags change every launch (xtag).  The pair
+// is co-resident on an otherwise idle GPU (host: 2 B blocks <= CUs, one block per CU),
+// which a plain launch does not guarantee (another process, CU masking): a partner that
+// never arrives ends the wait after ~20 ms and the launch is failed loudly (xch_fault:
+// status word, NaN CE / probs / logits, fault slot that makes the Adam kernels skip the
+// update), never a hang.  v must not change between send and receive; n is even.
 // ------------------------------------------------------------------------------
 // tag of exchange slot s (1..5) in the pair's launch epoch e (a per-commit counter the
 // pair reads at its start and block 0 advances after the last exchange): stale words
@@ -1152,6 +1154,9 @@ typedef uint32_t xu4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void xstore(xu4* p, const xu4 w) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ void xstore1(uint32_t* p, const uint32_t w) {
+  asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
 }
 __device__ __forceinline__ xu4 xload(const xu4* p) {
   xu4 w;
@@ -1192,6 +1197,28 @@ __device__ __forceinline__ bool pair_recv_add(float* v, const int n, xu4* __rest
   return late;
 }
 
+// A pair exchange of a forward-only launch timed out (split mode; block-uniform call):
+// fail the launch loudly.  The CE slot and this block's own probs / logits rows
+// (p = rmul r + radd) become NaN and the caller's status word gets HDG_STATUS_XCH_TIMEOUT.
+// Thread 0 wrote pb[NP] before, so program order keeps the poison last.  (Training
+// launches handle a timeout in their tail: CE NaN, fault slot, status.)
+__device__ __forceinline__ void xch_fault(float* __restrict__ pb, uint32_t* __restrict__ status,
+                                       float* __restrict__ probs, float* __restrict__ logits,
+                                       const int b, const int Nc, const int rmul,
+                                       const int radd, const int t) {
+  const float qnan = __builtin_nanf("");
+  if (t == 0) pb[m2::NP + HDG_TR_CE] = qnan;
+  if (t == 0 && status) xstore1(status, HDG_STATUS_XCH_TIMEOUT);
+  const int Nc1 = Nc - 1, Pc = Nc * Nc1;
+  const int rows = (Nc - radd + rmul - 1) / rmul;
+  const size_t base = (size_t)b * 2 * Pc;
+  for (int e = t; e < rows * Nc1; e += NT_MID) {
+    const int r = (rmul * (e / Nc1) + radd) * Nc1 + e % Nc1;
+    if (probs) { probs[base + r] = qnan; probs[base + Pc + r] = qnan; }
+    if (logits) { logits[base + r] = qnan; logits[base + Pc + r] = qnan; }
+  }
+}
+
 template <int SMAXC, bool TRAIN, bool STAMPS = false, bool SPLIT = false>
 __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const float* __restrict__ x, const uint32_t* __restrict__ abits,
@@ -1200,7 +1227,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     float* __restrict__ gamg, float* __restrict__ part, float* __restrict__ probs,
     float* __restrict__ logits, int Ne, int Nc, float ce_scale,
     unsigned long long* __restrict__ stamps, float* __restrict__ aux,
-    const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch) {
+    const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch,
+    uint32_t* __restrict__ status, const uint32_t xfault) {
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
@@ -1230,6 +1258,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
                                                       (size_t)2 * B * XB) + b
                          : nullptr;
   const uint32_t epoch = SPLIT ? *xctr : 0u;
+  // send tags: xtag(epoch, slot) ^ xsend; xsend != 0 only under the HDG_DEBUG_XCH_FAULT
+  // knob (block 1 of every pair sends words its partner never accepts: forced timeouts)
+  const uint32_t xsend = h ? xfault : 0u;
   // Thread ids are re-derived from an opaque copy of threadIdx.x at every phase
   // boundary (PHASE()), so the compiler cannot keep addresses derived from them live
   // across phases: this kernel runs at the 128-VGPR ceiling of 1024-thread blocks.
@@ -1533,7 +1564,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     if constexpr (SPLIT) {
       for (int i = t; i < NE4; i += NT_MID) xsc[2 * Nc + i] = (i >= nlo && i < nhi) ? os[i] : 0.f;
       __syncthreads();
-      pair_send(xsc, 2 * Nc + NE4, xout + 3 * XS, xtag(epoch, 4), t);   // constants overlap
+      pair_send(xsc, 2 * Nc + NE4, xout + 3 * XS, xtag(epoch, 4) ^ xsend, t);   // constants overlap
     }
   }
   // per-block constants: delta, eps, c, M = V2 U1e, sigma/tau offsets
@@ -1610,7 +1641,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     Hh[e] -= dg;
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, xtag(epoch, 1), t);   // received in M6
+  if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, xtag(epoch, 1) ^ xsend, t);   // received in M6
   MID_STAMP();
 
   // ---- M6: classifier first layer on eff = S_p + T_q, S = G V2 + (Nc-1) c2:
@@ -1780,6 +1811,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   if constexpr (!TRAIN) {         // uniform exit: forward-only launch (the H exchange was
     if (SPLIT && h == 0 && t == 0) *xctr = epoch + 1u;   // the pair's last: next epoch)
+    if constexpr (SPLIT) {        // block-wide vote through word 31 of each wave's red row
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own probs stores land first
+      const bool wl = __ballot(xlate) != 0ull;            // (no __syncthreads_or: its
+      if (lane == 0) red[wv * 32 + 31] = wl ? 1.f : 0.f;  // static LDS word would push the
+      __syncthreads();                                     // block past 160 KiB)
+      bool any = false;
+      for (int w = 0; w < NT_MID / 64; ++w) any |= red[w * 32 + 31] != 0.f;
+      if (any) xch_fault(pb, status, probs, logits, b, Nc, rmul, radd, t);
+    }
     return;
   }
 
@@ -1796,7 +1836,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     Dtau[e] *= cvec[k];
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, xtag(epoch, 2), t);   // received in M9
+  if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, xtag(epoch, 2) ^ xsend, t);   // received in M9
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
   //   one MFMA GEMM [G^T; 1; 0 | H^T; 0; 1] (22 x 2Nc) . [Dsig; Dtau] (2Nc x 20): rows
@@ -1941,7 +1981,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   if constexpr (SPLIT) {
-    pair_send(dnb, 2 * Nc, xout + 2 * XS, xtag(epoch, 3), t);   // dV1 overlaps
+    pair_send(dnb, 2 * Nc, xout + 2 * XS, xtag(epoch, 3) ^ xsend, t);   // dV1 overlaps
     // waves 4-15 warm this XCD's L2 with the count matrices (M11 reads every column; M3
     // fetched only the own half) while waves 0-3 run dV1
     if (wv >= 4) {
@@ -2119,7 +2159,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
   }
   __syncthreads();
-  if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, xtag(epoch, 5), t);
+  // trailer zeros (fault slot: t = 2) before the rho send, whose vmcnt(0) completes them:
+  // a late thread's fault store at the end then lands after them
+  if (t < HDG_TRAILER - 2) pb[NP + 2 + t] = 0.f;
+  if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, xtag(epoch, 5) ^ xsend, t);
   MID_STAMP();
   // ---- M13: reductions over rows: dW1' = [x, E_bar, 1]^T dq (waves 0-3),
   //      dW5 = [P, 1]^T dE (waves 4-7; row 20 -> db5 / 2(Ne-1)), dw2' / db2' (wave 8);
@@ -2161,7 +2204,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     pb[lane < HS ? E3_W2 + lane : E3_B2] = acc;
   }
   if (t < 4) pb[TH1 + t] = 0.f;                     // map_theta*: data-independent
-  if (t < 3) pb[NP + 2 + t] = 0.f;                  // trailer / pad
   if constexpr (SPLIT) {                             // the partner half's rho rows
     const int plo = h ? 0 : (Ne + 1) / 2, phi = h ? (Ne + 1) / 2 : Ne;
     xlate |= pair_recv_add<false>(rho + plo * HS, (phi - plo) * HS, xin + XSLOTS * XS,
@@ -2257,7 +2299,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     pb[E1_W1 + 3 * HS + t] = s3;
     pb[E1_B1 + t] = s2;
   }
-  if (SPLIT && xlate) pb[NP] = __builtin_nanf("");    // a pair exchange timed out: loud
+  // a pair exchange timed out: every late thread poisons the CE slot, sets the fault slot
+  // and the status word (identical values; the slots' earlier stores completed at the
+  // pair sends' vmcnt(0)).  No block-wide vote here: the tail sits at the VGPR ceiling.
+  // The step's probs stay as computed; the status word and the NaN CE void them.
+  if (SPLIT && xlate) {
+    pb[NP + HDG_TR_CE] = __builtin_nanf("");
+    pb[NP + HDG_TR_FAULT] = 1.f;
+    if (status) xstore1(status, HDG_STATUS_XCH_TIMEOUT);
+  }
   MID_STAMP();
 #undef MID_STAMP
 }
@@ -2267,15 +2317,25 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
 // 1024-thread block takes RED_P = 16 parameters x 64 row phases (row r -> phase r % 64,
 // fixed order); a thread's <= 4 rows per trip are loaded before they are added (one
 // memory round trip up to 256 rows), the 4 phases of a wave close with two permlane
-// swaps, the 16 waves in a fixed-order LDS sum.  Bitwise reproducible.
+// swaps, the 16 waves in a fixed-order LDS sum.  Bitwise reproducible.  The correct-
+// prediction count (slot NP + HDG_TR_COUNT, an exact integer per row) is summed as an
+// integer alongside and returned in `count` (thread pl of that slot's block).
 // ------------------------------------------------------------------------------
 constexpr int RED_P = 16, RED_PH = NT_MID / RED_P;   // 16 parameters x 64 phases
+constexpr int CNT_SLOT = m2::NP + HDG_TR_COUNT;
+
+struct RedShared {
+  float s[NT_MID / 64][RED_P];
+  uint32_t c[NT_MID / 16];             // per (wave, phase lane group) count partials
+};
 
 __device__ __forceinline__ float reduce_commits(const float* __restrict__ part, int R, int p,
-                                                bool valid, float (*sh)[RED_P]) {
+                                                bool valid, RedShared& sh, uint32_t& count) {
   const int pl = threadIdx.x & (RED_P - 1), ph = threadIdx.x / RED_P;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool isc = p == CNT_SLOT;
   float acc = 0.f;
+  uint32_t accu = 0u;
   if (valid) {
     for (int b0 = ph; b0 < R; b0 += 4 * RED_PH) {
       float v[4];
@@ -2286,26 +2346,45 @@ __device__ __forceinline__ float reduce_commits(const float* __restrict__ part, 
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc += v[u];
+      if (isc) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) accu += (uint32_t)v[u];
+      }
     }
   }
   acc = xrow_sum4(acc);                 // the wave's 4 phases (lanes pl, pl+16, +32, +48)
-  if (lane < RED_P) sh[wv][pl] = acc;
+  if (lane < RED_P) sh.s[wv][pl] = acc;
+  if (isc) sh.c[wv * 4 + (lane >> 4)] = accu;
   __syncthreads();
   float g = 0.f;
+  count = 0u;
   if (threadIdx.x < RED_P) {
 #pragma unroll
-    for (int q = 0; q < NT_MID / 64; ++q) g += sh[q][pl];
+    for (int q = 0; q < NT_MID / 64; ++q) g += sh.s[q][pl];
+    if (isc)
+      for (int q = 0; q < NT_MID / 16; ++q) count += sh.c[q];
   }
   return g;
+}
+
+// the trailer's count slots from the integer total (each part < 2^16: exact under any
+// float all-reduce of up to 256 ranks)
+__device__ __forceinline__ void put_count(float* __restrict__ out, const uint32_t c) {
+  out[0] = (float)(c & 0xFFFFu);
+  out[1] = (float)(c >> 16);
+  out[2] = 0.f;
 }
 
 __global__ __launch_bounds__(1024) void k_grad_reduce(const float* __restrict__ part, int B,
                                                       int p_begin, int p_end,
                                                       float* __restrict__ out) {
-  __shared__ float sh[NT_MID / 64][RED_P];
+  __shared__ RedShared sh;
   const int p = p_begin + blockIdx.x * RED_P + (threadIdx.x & (RED_P - 1));
-  const float g = reduce_commits(part, B, p, p < p_end, sh);
-  if (threadIdx.x < RED_P && p < p_end) out[p - p_begin] = g;
+  uint32_t cnt;
+  const float g = reduce_commits(part, B, p, p < p_end, sh, cnt);
+  if (threadIdx.x >= RED_P || p >= p_end) return;
+  if (p == CNT_SLOT && p + 2 < p_end) put_count(out + (p - p_begin), cnt);
+  else if (p < CNT_SLOT || p > CNT_SLOT + 2) out[p - p_begin] = g;
 }
 
 // Single-process training step tail: the reduction above fused with TF1 Adam for the
@@ -2319,17 +2398,24 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
                                                       float* __restrict__ bpow,
                                                       const float* __restrict__ aux, float lr,
                                                       float inv_pairs, float* __restrict__ stats,
-                                                      float* __restrict__ grad) {
+                                                      float* __restrict__ grad, int fault_rows) {
   using namespace m2;
-  __shared__ float sh[NT_MID / 64][RED_P];
+  __shared__ RedShared sh;
   const int p = blockIdx.x * RED_P + (threadIdx.x & (RED_P - 1));
-  const bool upd = threadIdx.x < RED_P && p < NP;
+  bool upd = threadIdx.x < RED_P && p < NP;
   // the update's operands are fetched before the reduction so both latencies overlap
   const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
   const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
-  const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh);
+  // split mode: any block whose pair exchange timed out voids the whole update
+  bool bad = false;
+  for (int r = threadIdx.x; r < fault_rows; r += NT_MID)
+    bad |= part[(size_t)r * NPART + NP + HDG_TR_FAULT] != 0.f;
+  uint32_t cnt;
+  const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh, cnt);
+  if (fault_rows > 0 && __syncthreads_or(bad)) upd = false;
   if (threadIdx.x >= RED_P) return;
-  if (p < GRAD_LEN) grad[p] = g;
+  if (p == CNT_SLOT) put_count(grad + p, cnt);
+  else if (p < CNT_SLOT || (p > CNT_SLOT + 2 && p < GRAD_LEN)) grad[p] = g;
   if (p == NP) {
     const float ce = g * inv_pairs;
     if (stats) {
@@ -2351,7 +2437,10 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
     vv[p] = v;
     params[p] = w - lr_t * m / (sqrtf(v) + ep);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) { bpow[0] = aux[5]; bpow[1] = aux[6]; }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && upd) {
+    bpow[0] = aux[5];
+    bpow[1] = aux[6];
+  }
 }
 
 // ------------------------------------------------------------------------------
@@ -2402,6 +2491,7 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
     stats[2] = lpara;
     stats[3] = 10.f * ce + 0.1f * lmap + lpara;
   }
+  if (grad[np + HDG_TR_FAULT] != 0.f) return;   // a pair exchange timed out on some rank
   const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
   for (int p = t; p < np; p += 1024) {
     const float w = params[p];
@@ -2565,10 +2655,14 @@ int check_batch(const hdg_batch* bt) {
   const int var = resolve(s);                    \
   if (var < 0) return HDG_EINVAL
 
-// Split mode (two blocks per commit, hunk rows split by parity, three block-pair
-// exchanges) needs every block resident at once: one 1024-thread block per CU, so
-// 2 B <= CUs of the device.  HDG_FUSED_SPLIT=0 forces one block per commit, =1 asks for
-// the split whenever it is safe; default: split when safe.
+// Split mode (two blocks per commit, hunk rows split by parity, block-pair exchanges)
+// needs both blocks of a pair resident at once.  The host asks for it only when the
+// whole grid fits the device at the kernel's occupancy (2 B <= CUs x blocks per CU, one
+// 1024-thread block per CU in practice); that holds on an otherwise idle GPU, and a pair
+// that still cannot meet (another process holding CUs, CU masking) fails its launch
+// loudly (xch_fault) rather than hanging.  A cooperative launch would check residency at
+// launch time but costs +17-20 us per replay (MI355X_MICROARCH price list), a quarter of
+// the step.  HDG_FUSED_SPLIT=0 forces one block per commit.
 int cu_count() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -2576,20 +2670,8 @@ int cu_count() {
   return n;
 }
 
-bool use_split(const hdg_shape* s) {
-  const char* e = getenv("HDG_FUSED_SPLIT");
-  if (e && e[0] == '0') return false;
-  return 2 * s->batch <= cu_count();
-}
-
-int part_rows(const hdg_shape* s, bool split) { return split ? 2 * s->batch : s->batch; }
-
 template <int SMAXC, bool TRAIN, bool STAMPS, bool SPLIT>
-hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
-                       const Work& w, float* probs, float* logits, float ce_scale,
-                       unsigned long long* stamps, const float* bpow, hipStream_t st) {
-  const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
-  const size_t lds = (size_t)L.total * 4;
+hipError_t set_step_attr() {
   static bool attr_set = false;   // the attribute is per function; 160 KiB covers every shape
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_commit_step<SMAXC, TRAIN, STAMPS, SPLIT>,
@@ -2597,25 +2679,90 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  return hipSuccess;
+}
+
+// resident split-mode blocks per CU for this shape (cached per device and tile count)
+template <int SMAXC>
+int split_blocks_per_cu(const hdg_shape* s) {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] == 0) {
+    if (set_step_attr<SMAXC, true, false, true>() != hipSuccess) return 0;
+    // registers / waves from the occupancy query (without dynamic LDS: the query rejects
+    // sizes above the default 64 KiB limit), LDS from the CU's 160 KiB
+    int nb = 0;
+    const size_t lds = (size_t)step_layout(s->ne, s->nc, SMAXC).total * 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, (const void*)k_commit_step<SMAXC, true, false, true>, NT_MID, 0) != hipSuccess) {
+      (void)hipGetLastError();      // leave no sticky error for the launch's check
+      return 0;
+    }
+    const int by_lds = lds > 0 ? (int)((160 * 1024) / lds) : nb;
+    nb = nb < by_lds ? nb : by_lds;
+    cache[dev] = nb > 0 ? nb : -1;
+  }
+  return cache[dev] > 0 ? cache[dev] : 0;
+}
+
+bool use_split(const hdg_shape* s) {
+  const char* e = getenv("HDG_FUSED_SPLIT");
+  if (e && e[0] == '0') return false;
+  int per_cu = 0;
+  switch (smax_c(s->nc)) {
+    case 5: per_cu = split_blocks_per_cu<5>(s); break;
+    case 8: per_cu = split_blocks_per_cu<8>(s); break;
+    default: per_cu = split_blocks_per_cu<10>(s); break;
+  }
+  return 2 * s->batch <= cu_count() * per_cu;
+}
+
+int part_rows(const hdg_shape* s, bool split) { return split ? 2 * s->batch : s->batch; }
+
+// HDG_DEBUG_XCH_FAULT=1 (tests only): block 1 of every pair sends exchange words with a
+// tag its partner never accepts, forcing the timeout path of every exchange
+uint32_t debug_xfault() {
+  const char* e = getenv("HDG_DEBUG_XCH_FAULT");
+  return (e && e[0] && e[0] != '0') ? 0x40000000u : 0u;
+}
+
+struct StepOut {
+  float* probs;
+  float* logits;
+  uint32_t* status;
+};
+StepOut step_out(const hdg_outputs* out) {
+  return out ? StepOut{out->probs, out->logits, out->status} : StepOut{nullptr, nullptr, nullptr};
+}
+
+template <int SMAXC, bool TRAIN, bool STAMPS, bool SPLIT>
+hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
+                       const Work& w, const StepOut& o, float ce_scale,
+                       unsigned long long* stamps, const float* bpow, hipStream_t st) {
+  const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
+  const size_t lds = (size_t)L.total * 4;
+  if (hipError_t e = set_step_attr<SMAXC, TRAIN, STAMPS, SPLIT>(); e != hipSuccess) return e;
   const int grid = SPLIT ? 2 * s->batch : s->batch;
   hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS, SPLIT>), dim3(grid), dim3(NT_MID), lds,
                      st, bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params,
-                     ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, probs, logits,
-                     s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow, s->batch,
-                     (unsigned long long*)(ws + w.xch));
+                     ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, o.probs,
+                     o.logits, s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow,
+                     s->batch, (unsigned long long*)(ws + w.xch), o.status,
+                     SPLIT ? debug_xfault() : 0u);
   return hipGetLastError();
 }
 
 template <bool TRAIN, bool STAMPS = false>
 hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
-                         const Work& w, float* probs, float* logits, float ce_scale,
+                         const Work& w, const StepOut& o, float ce_scale,
                          unsigned long long* stamps, hipStream_t st, bool split,
                          const float* bpow = nullptr) {
 #define HDG_STEP(SM)                                                                              \
-  return split ? launch_step<SM, TRAIN, STAMPS, true>(s, bt, params, ws, w, probs, logits,       \
-                                                      ce_scale, stamps, bpow, st)                 \
-               : launch_step<SM, TRAIN, STAMPS, false>(s, bt, params, ws, w, probs, logits,      \
-                                                       ce_scale, stamps, bpow, st)
+  return split ? launch_step<SM, TRAIN, STAMPS, true>(s, bt, params, ws, w, o, ce_scale, stamps, \
+                                                      bpow, st)                                   \
+               : launch_step<SM, TRAIN, STAMPS, false>(s, bt, params, ws, w, o, ce_scale, stamps,\
+                                                       bpow, st)
   switch (smax_c(s->nc)) {
     case 5: HDG_STEP(5);
     case 8: HDG_STEP(8);
@@ -2639,7 +2786,7 @@ int hdg_resolve_path(const hdg_shape* shape) { return resolve(shape); }
 int hdg_param_count(int32_t variant) { return hdg::param_offsets(variant).NP; }
 int hdg_grad_len(int32_t variant) {
   const int np = hdg::param_offsets(variant).NP;
-  return np < 0 ? -1 : np + 4;
+  return np < 0 ? -1 : np + HDG_TRAILER;
 }
 
 size_t hdg_workspace_bytes(const hdg_shape* shape) {
@@ -2706,9 +2853,8 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
   float* ws = (float*)workspace;
   const bool split = use_split(s);
   HIP_TRY(mark(0));
-  HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, 10.f / pair_count(s), nullptr, st,
-                              split));
+  HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, step_out(out), 10.f / pair_count(s), nullptr,
+                              st, split));
   HIP_TRY(mark(1));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
                      ws + w.part, part_rows(s, split), 0, GRAD_LEN, grad);
@@ -2729,9 +2875,9 @@ int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* 
   if (int rc = check_batch(bt)) return rc;
   if (!stamps || !workspace || !params) return fail(HDG_EINVAL, "NULL stamps/workspace/params");
   const Work w = work_layout(s);
-  const hipError_t e = dispatch_step<true, true>(s, bt, params, (float*)workspace, w, nullptr,
-                                                 nullptr, 1.f, stamps, (hipStream_t)stream,
-                                                 use_split(s));
+  const hipError_t e = dispatch_step<true, true>(s, bt, params, (float*)workspace, w,
+                                                 step_out(nullptr), 1.f, stamps,
+                                                 (hipStream_t)stream, use_split(s));
   HIP_TRY(e);
   return 0;
 }
@@ -2768,12 +2914,12 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
   float* ws = (float*)workspace;
   const float pairs = pair_count(s);
   const bool split = use_split(s);
-  HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, out ? out->probs : nullptr,
-                              out ? out->logits : nullptr, 10.f / pairs, nullptr, st, split,
-                              state->beta_pow));
-  hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st, ws + w.part,
-                     part_rows(s, split), state->params, state->adam_m, state->adam_v, state->beta_pow,
-                     ws + w.aux, lr, 1.f / pairs, out ? out->stats : nullptr, grad);
+  HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, step_out(out), 10.f / pairs, nullptr,
+                              st, split, state->beta_pow));
+  hipLaunchKernelGGL(k_reduce_adam, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
+                     ws + w.part, part_rows(s, split), state->params, state->adam_m,
+                     state->adam_v, state->beta_pow, ws + w.aux, lr, 1.f / pairs,
+                     out ? out->stats : nullptr, grad, split ? part_rows(s, split) : 0);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -2789,8 +2935,7 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
   const bool split = use_split(s);
-  HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, out ? out->probs : nullptr,
-                               out ? out->logits : nullptr, 0.f, nullptr, st, split));
+  HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, step_out(out), 0.f, nullptr, st, split));
   if (ce_sum) {
     hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part,
                        part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);

@@ -1970,19 +1970,39 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
 // kw_grad_reduce  grid (count): one wave per parameter p = p_begin + blockIdx.x; lanes
 // stride over the partial rows of p's segment in a fixed order, xor-butterfly total.
 // Parameters without a segment get 0 (data-independent: map_theta*, model_3's unused
-// entity-edge blocks).
+// entity-edge blocks; the trailer's fault slot: no exchanges on this path).  The correct-
+// prediction count (trailer slot HDG_TR_COUNT, exact integers per row) is summed as an
+// integer and written as the trailer's three 16-bit parts by that slot's wave.
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ part, Segs sg,
-                                                     int p_begin, float* __restrict__ out) {
+                                                     int p_begin, int np,
+                                                     float* __restrict__ out) {
   const int p = p_begin + blockIdx.x, lane = threadIdx.x;
+  const int pc = np + HDG_TR_COUNT;
+  if (p > pc && p <= pc + 2) return;              // written by the count slot's wave
   float a = 0.f;
+  unsigned long long c = 0ull;
   for (int s = 0; s < sg.count; ++s) {
     const Seg& g = sg.s[s];
     if (g.n > 0 && p >= g.p0 && p < g.p0 + g.n) {
       const float* src = part + g.off + (long long)(p - g.p0) * g.rows;
-      for (int r = lane; r < g.rows; r += 64) a += src[r];
+      if (p == pc)
+        for (int r = lane; r < g.rows; r += 64) c += (unsigned long long)src[r];
+      else
+        for (int r = lane; r < g.rows; r += 64) a += src[r];
       break;
     }
+  }
+  if (p == pc) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+    if (lane == 0) {
+      float* o = out + blockIdx.x;
+      o[0] = (float)(c & 0xFFFFull);
+      o[1] = (float)((c >> 16) & 0xFFFFull);
+      o[2] = (float)(c >> 32);
+    }
+    return;
   }
   a = wsum(a);
   if (lane == 0) out[blockIdx.x] = a;
@@ -2234,7 +2254,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
     WTRY(hipGetLastError());
     if (ce_sum) {
-      hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, ce_sum);
+      hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, o.NP,
+                         ce_sum);
       WTRY(hipGetLastError());
     }
     return 0;
@@ -2284,7 +2305,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        w.segs);
     WTRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + 4), dim3(64), 0, st, part, w.segs, 0, grad);
+  hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs, 0,
+                     o.NP, grad);
   WTRY(hipGetLastError());
   return 0;
 }

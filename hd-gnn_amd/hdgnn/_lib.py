@@ -35,7 +35,19 @@ class State(ctypes.Structure):
 
 class Outputs(ctypes.Structure):
     _fields_ = [("probs", ctypes.c_void_p), ("logits", ctypes.c_void_p),
-                ("stats", ctypes.c_void_p)]
+                ("stats", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
+ABI_VERSION = 4
+# gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
+TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
+STATUS_XCH_TIMEOUT = 1
+
+
+def trailer_count(tr):
+    """Correct-prediction count from the trailer's three 16-bit parts (slots 1..3)."""
+    return (int(round(float(tr[TR_COUNT]))) + (int(round(float(tr[TR_COUNT + 1]))) << 16)
+            + (int(round(float(tr[TR_COUNT + 2]))) << 32))
 
 
 EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count", "hdg_grad_len",

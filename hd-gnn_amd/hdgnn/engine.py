@@ -47,16 +47,20 @@ class Engine:
         self.beta_pow = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
         self.grad = torch.zeros(self.glen, dtype=f32, device=dev)
         self.stats = torch.zeros(4, dtype=f32, device=dev)
+        # sticky status word (HDG_STATUS_* bits); check_status() reads it
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ce_sum = torch.zeros(1, dtype=f32, device=dev)
         pc = nc * (nc - 1)
         self.probs = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
         self.logits = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
         self._state = _lib.State(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                  self.beta_pow.data_ptr())
+        st = self.status.data_ptr()
         self._out = _lib.Outputs(self.probs.data_ptr(), self.logits.data_ptr(),
-                                 self.stats.data_ptr())
+                                 self.stats.data_ptr(), st)
         # a training sess.run fetches C_edge_output2 (the probabilities), not the logits
-        self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr())
+        self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr(), st)
+        self._out_none = _lib.Outputs(None, None, None, st)   # status only
 
     # ---- parameters ---------------------------------------------------------
     def set_params(self, flat):
@@ -86,8 +90,31 @@ class Engine:
 
     def _outputs(self, outputs, logits):
         if not outputs:
-            return None
+            return self._out_none
         return self._out if logits else self._out_train
+
+    # ---- status / trailer -----------------------------------------------------
+    def check_status(self):
+        """Raise if any launch since the last clear_status() failed on the device (the
+        sticky status word, include/hdgnn.h).  Synchronises with the device."""
+        st = int(self.status.item())
+        if st & _lib.STATUS_XCH_TIMEOUT:
+            raise RuntimeError(
+                "libhdgnn: a block-pair exchange of the fused split path timed out (the two "
+                "blocks of a commit were not resident together: another process holding "
+                "CUs?); that step's outputs are NaN and its Adam update was skipped. "
+                "HDG_FUSED_SPLIT=0 runs one block per commit.")
+        if st:
+            raise RuntimeError("libhdgnn: device status 0x%x" % st)
+
+    def clear_status(self):
+        self.status.zero_()
+
+    def correct_count(self, trailer=None):
+        """top_ACC numerator of the last fwd_bwd / train step (summed over ranks when the
+        gradient was all-reduced) from the gradient trailer."""
+        tr = (self.grad[self.np:] if trailer is None else trailer)
+        return _lib.trailer_count(tr.cpu().numpy() if hasattr(tr, "cpu") else tr)
 
     def fwd_bwd(self, dbatch, outputs=True, logits=True):
         self._check(dbatch)
@@ -96,7 +123,7 @@ class Engine:
         _lib.check(self.lib.hdg_fwd_bwd(ctypes.byref(self.shape), ctypes.byref(b),
                                         ctypes.c_void_p(self.params.data_ptr()),
                                         ctypes.c_void_p(self.grad.data_ptr()),
-                                        ctypes.byref(out) if out is not None else None,
+                                        ctypes.byref(out),
                                         ctypes.c_void_p(self.workspace.data_ptr()),
                                         self._stream()))
 
@@ -131,7 +158,7 @@ class Engine:
         out = self._outputs(outputs, logits)
         _lib.check(self.lib.hdg_train_step(ctypes.byref(self.shape), ctypes.byref(b),
                                            ctypes.byref(self._state), ctypes.c_float(self.lr),
-                                           ctypes.byref(out) if out is not None else None,
+                                           ctypes.byref(out),
                                            ctypes.c_void_p(self.grad.data_ptr()),
                                            ctypes.c_void_p(self.workspace.data_ptr()),
                                            self._stream()))

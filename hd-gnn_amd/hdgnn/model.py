@@ -30,7 +30,7 @@ import time
 
 import numpy as np
 
-from . import layout, metrics, tfckpt
+from . import _lib, layout, metrics, tfckpt
 from .data import compact_from_read_data, onehot_relations
 
 HS = 20   # De_e = De_er = h_size compiled into the engine
@@ -179,10 +179,13 @@ class graph2graph(object):
             correct = 0
             for j, db in enumerate(batches):
                 eng.train_step(db)
-                # one small copy per step: pre-update losses (like sess.run) and the
-                # on-device top_ACC numerator (gradient trailer slot P+1; already summed
-                # over ranks by the data-parallel all-reduce)
-                host = torch.cat([eng.stats, eng.grad[eng.np:eng.np + 2]]).cpu().numpy()
+                # one small copy per step: pre-update losses (like sess.run), the
+                # on-device top_ACC numerator (gradient trailer count slots; already
+                # summed over ranks by the data-parallel all-reduce) and the status word
+                host = torch.cat([eng.stats, eng.grad[eng.np:eng.np + _lib.TRAILER],
+                                  eng.status.float()]).cpu().numpy()
+                if host[-1] != 0:
+                    eng.check_status()
                 tr_loss_Hedge += float(host[0])
                 tr_loss_map += float(host[1])
                 self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[0]),
@@ -190,7 +193,7 @@ class graph2graph(object):
                                                                       float(host[2]))
                 self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
                 self.C_edge_output2_logits = None          # not fetched in training
-                correct += int(round(float(host[5])))
+                correct += _lib.trailer_count(host[4:4 + _lib.TRAILER])
             torch.cuda.synchronize(eng.device)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
             theta = self.theta.reshape([2])
@@ -279,6 +282,7 @@ class graph2graph(object):
         for db in self._device_batches(test, maps):
             probs, logits, ce_sum = eng.forward(db)
             p = probs.cpu().numpy()
+            eng.check_status()
             ce = self._allsum(float(ce_sum.item())) / (self.mini_batch_num * self.Ncr)
             th1 = self.vars["map_conv/map_theta1:0"].reshape(-1).astype(np.float64)
             th2 = self.vars["map_conv/map_theta2:0"].reshape(-1).astype(np.float64)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 3
+#define HDG_ABI_VERSION 4
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -86,24 +86,46 @@ typedef struct hdg_outputs {
     float* logits;       /* [B][2][nc(nc-1)]  C_edge_output2_logits */
     float* stats;        /* [4] ce (loss_Hedge_mse), loss_map, loss_para, train_loss
                             (pre-update values, as sess.run returns them)              */
+    uint32_t* status;    /* [1] sticky device status word: the library ORs HDG_STATUS_*
+                            bits into it (write-through store) and never clears it; the
+                            caller zeroes it and reads it whenever it synchronises     */
 } hdg_outputs;
+
+/* Status bits (hdg_outputs.status).  HDG_STATUS_XCH_TIMEOUT: in the fused path's split
+ * mode a block waited ~20 ms for its partner block's exchange words and gave up (the pair
+ * was not co-resident: another process holding CUs, CU masking).  The launch's CE sum
+ * is NaN; a forward-only launch also writes NaN over the timed-out block's probs / logits
+ * rows; a training launch's gradient trailer carries the fault count (HDG_TR_FAULT) and
+ * the Adam update of that step is skipped on every rank (parameters, moments and beta
+ * powers unchanged).  Outputs of a launch with this bit set are void.                  */
+#define HDG_STATUS_XCH_TIMEOUT 1u
+
+/* Gradient trailer: hdg_fwd_bwd's grad buffer is [param_count + HDG_TRAILER] floats.
+ * Every slot sums exactly under a float all-reduce (SUM) over up to 256 ranks.          */
+#define HDG_TRAILER 8
+#define HDG_TR_CE 0      /* CE sum over this call's relations                              */
+#define HDG_TR_COUNT 1   /* slots 1..3: number of relations whose argmax prediction equals
+                            the label (EvaluationFuncs.top_ACC numerator, np.argmax tie
+                            rule), as three 16-bit parts: count = s1 + s2 2^16 + s3 2^32  */
+#define HDG_TR_FAULT 4   /* blocks whose pair exchange timed out (0 = clean step)          */
 
 int         hdg_version(void);
 const char* hdg_last_error(void);
 /* the path AUTO resolves to for this shape (HDG_PATH_FUSED / _GENERAL), or -1 */
 int         hdg_resolve_path(const hdg_shape* shape);
 int         hdg_param_count(int32_t variant);
-/* length of the gradient buffer hdg_fwd_bwd fills: param_count + 4 trailer slots
- * (slot P = CE sum over this call's relations, slot P+1 = number of relations whose
- * argmax prediction equals the label, the numerator of EvaluationFuncs.top_ACC with
- * np.argmax's tie rule, exact); all-reduce the whole buffer.                       */
+/* length of the gradient buffer hdg_fwd_bwd fills: param_count + HDG_TRAILER (the
+ * trailer slots above); all-reduce the whole buffer.                                */
 int         hdg_grad_len(int32_t variant);
 /* Scratch the library carves per call (parked node rows, partial gradient rows, the
  * block-pair inboxes and per-commit launch epochs of the fused path's split mode).  Keep
  * it per shape across calls; its initial content does not matter (exchange tags derive
  * from the epoch word and differ from the word's own bit pattern, everything else is
  * written before it is read).  Split mode (two blocks per commit) runs whenever
- * 2 * batch <= the device's CU count; HDG_FUSED_SPLIT=0 forces one block per commit.  */
+ * 2 * batch <= the device's CU count and one 1024-thread block of the step kernel fits
+ * a CU; HDG_FUSED_SPLIT=0 forces one block per commit.  The two blocks of a pair must
+ * run at the same time: plain launches do not guarantee it, so a pair that cannot meet
+ * is detected (HDG_STATUS_XCH_TIMEOUT) instead of producing silent garbage.          */
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
 /* bytes of batch->prep for this shape (0 on a shape error) */
 size_t      hdg_prep_bytes(const hdg_shape* shape);
@@ -136,6 +158,8 @@ int hdg_fwd_bwd_events(const hdg_shape* shape, const hdg_batch* batch, const flo
 int hdg_debug_step_stamps(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                          void* workspace, unsigned long long* stamps, void* stream);
 
+/* TF ApplyAdam from an (all-reduced) gradient buffer; skips the whole update (parameters,
+ * moments, beta powers) when grad[P + HDG_TR_FAULT] != 0.                            */
 int hdg_adam_tf(const hdg_shape* shape, hdg_state* state, const float* grad,
                 float lr, float* stats, void* stream);
 

@@ -99,3 +99,52 @@ def test_gloo_two_rank_step_equals_single_process(tmp_path):
     np.testing.assert_allclose(r[0]["grad"], _flat(g), rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(float(r[0]["ce"]), float(out["ce"]), rtol=1e-12)
     np.testing.assert_allclose(r[0]["theta"], ref_new, rtol=0, atol=1e-12)
+
+
+def _trailer_main(rank, world, port, out_dir):
+    """Each rank's gradient trailer as hdg_fwd_bwd leaves it (include/hdgnn.h): count as
+    three 16-bit parts, rank 1 reports one timed-out block; one fp32 SUM all-reduce."""
+    from hdgnn import _lib
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    count = [(1 << 24) + 12345, (1 << 26) + 777][rank]     # each beyond fp32's 2^24
+    tr = np.zeros(_lib.TRAILER, np.float32)
+    tr[_lib.TR_CE] = 0.5 + rank
+    tr[_lib.TR_COUNT] = count & 0xFFFF
+    tr[_lib.TR_COUNT + 1] = (count >> 16) & 0xFFFF
+    tr[_lib.TR_FAULT] = float(rank == 1)
+    buf = torch.from_numpy(np.concatenate([np.ones(5, np.float32), tr]))
+    dist.all_reduce(buf)
+    np.save(os.path.join(out_dir, "tr%d.npy" % rank), buf.numpy()[5:])
+    dist.destroy_process_group()
+
+
+def test_gloo_trailer_sums_exactly(tmp_path):
+    """The correct-prediction count survives the float all-reduce exactly past 2^24 and a
+    fault on any rank reaches every rank (so every replica skips that Adam update)."""
+    from hdgnn import _lib
+    world = 2
+    mp.spawn(_trailer_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = (1 << 24) + 12345 + (1 << 26) + 777
+    for k in range(world):
+        tr = np.load(os.path.join(tmp_path, "tr%d.npy" % k))
+        assert _lib.trailer_count(tr) == want
+        assert tr[_lib.TR_FAULT] == 1.0
+        assert tr[_lib.TR_CE] == 2.0
+    assert float(np.float32(want)) != want                 # one fp32 slot would round it
+
+
+def test_header_trailer_constants_match_binding():
+    """include/hdgnn.h's trailer / status constants == the Python binding's."""
+    import re
+    from conftest import ROOT
+    from hdgnn import _lib
+    txt = open(os.path.join(ROOT, "include", "hdgnn.h")).read()
+    val = {m.group(1): int(m.group(2)) for m in
+           re.finditer(r"#define (HDG_\w+)\s+(\d+)u?\b", txt)}
+    assert val["HDG_ABI_VERSION"] == _lib.ABI_VERSION
+    assert val["HDG_TRAILER"] == _lib.TRAILER
+    assert (val["HDG_TR_CE"], val["HDG_TR_COUNT"], val["HDG_TR_FAULT"]) == (
+        _lib.TR_CE, _lib.TR_COUNT, _lib.TR_FAULT)
+    assert val["HDG_STATUS_XCH_TIMEOUT"] == _lib.STATUS_XCH_TIMEOUT

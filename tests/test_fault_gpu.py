@@ -1,0 +1,136 @@
+"""Failure path of the fused kernel's split mode (two blocks per commit exchanging partial
+sums through tagged write-through words, csrc/hdgnn.hip pair_send / pair_recv_add).
+
+A pair whose partner never arrives must fail loudly and leave the model untouched:
+  * the sticky status word gets HDG_STATUS_XCH_TIMEOUT and Engine.check_status() raises;
+  * forward-only launches poison the CE sum and the timed-out block's probs / logits rows;
+  * training launches poison the CE, set the gradient trailer's fault slot and skip the
+    Adam update (parameters, moments and beta powers bitwise unchanged), on the fused
+    single-process path (k_reduce_adam) and on the data-parallel split (k_adam_tf);
+  * the next clean launch is correct again (exchange tags are per launch epoch).
+HDG_DEBUG_XCH_FAULT=1 makes block 1 of every pair send words its partner never accepts,
+so block 0 (the even hunk rows) waits out every exchange (~20 ms each).  GPU only.
+"""
+import numpy as np
+import pytest
+import torch
+
+from hdgnn import _lib, layout
+from hdgnn.synth import synth_commits
+
+pytestmark = pytest.mark.gpu
+
+B, NE, NC = 3, 40, 17
+
+
+@pytest.fixture
+def fused_split(monkeypatch):
+    monkeypatch.setenv("HDG_FUSED_SPLIT", "1")
+    from hdgnn.engine import Engine
+    eng = Engine(NE, NC, B, path=_lib.PATH_FUSED)
+    eng.set_params(layout.init_flat(5))
+    return eng, eng.upload(synth_commits(B, NE, NC, 7))
+
+
+def _state(eng):
+    return [t.clone() for t in (eng.params, eng.m, eng.v, eng.beta_pow)]
+
+
+def _even_rows(a):
+    """[B][2][Pc] -> the relations of hunk rows p = 0, 2, 4, ... (block 0's rows)."""
+    r = a.reshape(a.shape[0], 2, NC, NC - 1)
+    return r[:, :, 0::2], r[:, :, 1::2]
+
+
+def test_forward_timeout_poisons_outputs(fused_split, monkeypatch):
+    eng, db = fused_split
+    probs, logits, ce = eng.forward(db)
+    torch.cuda.synchronize()
+    eng.check_status()
+    good = probs.cpu().numpy().copy()
+    monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+    eng.probs.zero_()
+    eng.logits.zero_()
+    eng.forward(db)
+    torch.cuda.synchronize()
+    assert int(eng.status.item()) == _lib.STATUS_XCH_TIMEOUT
+    with pytest.raises(RuntimeError, match="exchange"):
+        eng.check_status()
+    assert np.isnan(eng.ce_sum.item())
+    ev, _ = _even_rows(eng.probs.cpu().numpy())    # block 1's rows are void too (built
+    assert np.isnan(ev).all()                       # from its partner's bad partials)
+    lev, _ = _even_rows(eng.logits.cpu().numpy())
+    assert np.isnan(lev).all()
+    # recovery: the next clean launch is exact again, status stays sticky until cleared
+    monkeypatch.delenv("HDG_DEBUG_XCH_FAULT")
+    eng.forward(db)
+    torch.cuda.synchronize()
+    assert int(eng.status.item()) == _lib.STATUS_XCH_TIMEOUT
+    eng.clear_status()
+    assert np.array_equal(eng.probs.cpu().numpy(), good)
+    eng.check_status()
+
+
+def test_train_timeout_skips_update(fused_split, monkeypatch):
+    eng, db = fused_split
+    before = _state(eng)
+    monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+    eng.train_step(db)                               # hdg_train_step: k_reduce_adam
+    torch.cuda.synchronize()
+    for a, b in zip(before, _state(eng)):
+        assert torch.equal(a, b)
+    tr = eng.grad[eng.np:].cpu().numpy()
+    assert np.isnan(tr[_lib.TR_CE])
+    # block 0 of every pair timed out; block 1 may too (block 0 sends each later exchange
+    # ~20 ms late, after its own wait)
+    assert B <= tr[_lib.TR_FAULT] <= 2 * B
+    assert np.isnan(eng.stats[0].item())
+    with pytest.raises(RuntimeError):
+        eng.check_status()
+    # the data-parallel decomposition (fwd_bwd -> all-reduce -> hdg_adam_tf) skips too
+    eng.clear_status()
+    eng.fwd_bwd(db)
+    eng.adam()
+    torch.cuda.synchronize()
+    for a, b in zip(before, _state(eng)):
+        assert torch.equal(a, b)
+    assert int(eng.status.item()) == _lib.STATUS_XCH_TIMEOUT
+    # clean again: the step equals a fresh engine's first step
+    monkeypatch.delenv("HDG_DEBUG_XCH_FAULT")
+    eng.clear_status()
+    eng.train_step(db)
+    torch.cuda.synchronize()
+    eng.check_status()
+    from hdgnn.engine import Engine
+    ref = Engine(NE, NC, B, path=_lib.PATH_FUSED)
+    ref.set_params(layout.init_flat(5))
+    ref.train_step(ref.upload(synth_commits(B, NE, NC, 7)))
+    torch.cuda.synchronize()
+    assert torch.equal(eng.params, ref.params)
+    assert eng.grad[eng.np + _lib.TR_FAULT].item() == 0.0
+
+
+def test_count_beyond_fp32_integer_range():
+    """top_ACC numerator past 2^24 (B * Nc (Nc - 1) = 19.3 M relations; the classifier
+    reduced to its output bias, so every relation predicts class 0 and the ~90 % with
+    label 0 are correct): exact through the integer trailer parts (it used
+    to be one fp32 slot)."""
+    from hdgnn import metrics
+    from hdgnn.data import onehot_relations
+    from hdgnn.engine import Engine
+    b, ne, nc = 16, 40, 1100
+    cb = synth_commits(b, ne, nc, 11)
+    eng = Engine(ne, nc, b, variant=2, path=_lib.PATH_GENERAL)
+    flat = layout.init_flat(3)
+    offs = layout.offsets(2)
+    for name in ("phi_U_R1/C_edge_w1:0", "phi_U_R1/o1_w2r:0"):
+        o, shp = offs[name]
+        flat[o:o + int(np.prod(shp))] = 0.0
+    off = offs["phi_U_R1/o1_b2r:0"][0]                   # classifier output bias
+    flat[off], flat[off + 1] = 3.0, -3.0
+    eng.set_params(flat)
+    eng.fwd_bwd(eng.upload(cb))
+    torch.cuda.synchronize()
+    want = metrics.top_acc_count(onehot_relations(cb.y), eng.probs.cpu().numpy())
+    assert want > 2 ** 24
+    assert eng.correct_count() == want

@@ -229,7 +229,7 @@ def test_workspace_garbage_does_not_leak(v, path):
 
 @pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN)])
 def test_on_device_correct_count(v, path):
-    """Gradient trailer slot P+1 = EvaluationFuncs.top_ACC numerator on the returned probs
+    """Gradient trailer count slots = EvaluationFuncs.top_ACC numerator on the returned probs
     (np.argmax tie rule), exactly; forward-only leaves the CE slot intact."""
     from hdgnn import metrics
     from hdgnn.data import onehot_relations
@@ -240,4 +240,4 @@ def test_on_device_correct_count(v, path):
     eng.fwd_bwd(eng.upload(cb))
     torch.cuda.synchronize()
     want = metrics.top_acc_count(onehot_relations(cb.y), eng.probs.cpu().numpy())
-    assert eng.grad[eng.np + 1].item() == want
+    assert eng.correct_count() == want

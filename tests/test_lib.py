@@ -35,10 +35,10 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from hdgnn import _lib
     lib = _lib.load()
-    assert lib.hdg_version() == 3
+    assert lib.hdg_version() == _lib.ABI_VERSION == 4
     for v, n in ((1, 1146), (2, 2127), (3, 2148), (4, 3129)):
         assert lib.hdg_param_count(v) == n
-        assert lib.hdg_grad_len(v) == n + 4
+        assert lib.hdg_grad_len(v) == n + _lib.TRAILER
     assert lib.hdg_param_count(5) == -1
     ok = _lib.Shape(100, 200, 74, 2, 100, 0)
     assert lib.hdg_resolve_path(ctypes.byref(ok)) == _lib.PATH_FUSED
