@@ -51,7 +51,7 @@ def hbm_bytes_per_commit(ne, nc):
     inp = 4 * ne + 2 * 4 * ne * we + 4 * nc * wc + 16 * ne
     kmat = 2 * 2 * (2 * nc * ne)
     park = 2 * 3 * 4 * ne * H + 2 * 2 * ne * H
-    return inp + kmat + park + 4 * 2132
+    return inp + kmat + park + 4 * 2136         # + the block's partial-gradient row (NPART)
 
 
 def cpu_baseline(cb, steps, threads):
@@ -201,8 +201,22 @@ def main():
         torch.distributed.destroy_process_group()
         return
     dom = names[0]
-    flops_launch = flops_per_commit(ne, nc, v) * B
-    achieved = flops_launch / (kern_ms[dom] * 1e-3) / 1e12
+    dense_launch = flops_per_commit(ne, nc, v) * B
+    dense_tflops = dense_launch / (kern_ms[dom] * 1e-3) / 1e12
+    # executed FP32 FLOPs of one launch (rocprofv3 PMC, calibrated: tools/flops_summary.py)
+    exec_flops, flops_src = None, None
+    fj = os.path.join(ROOT, "profiles", "r02", "flops_pmc.json")
+    if fused and os.path.exists(fj):
+        with open(fj) as f:
+            pj = json.load(f)
+        if pj["config"] == {"ne": ne, "nc": nc, "batch": B} and v == 2:
+            ks = [k for k in pj["kernels"] if k.startswith(dom)]
+            if ks:
+                exec_flops = pj["kernels"][ks[0]]["executed_flops_per_launch"]
+                flops_src = ("profiles/r02/flops_pmc.json: 64 x SQ_INSTS_VALU_FLOPS_FP32 + 512 x "
+                             "SQ_INSTS_VALU_MFMA_MOPS_F32 per launch, counters calibrated "
+                             "on known instruction streams (tools/probe/flops_cal.hip)")
+    achieved = exec_flops / (kern_ms[dom] * 1e-3) / 1e12 if exec_flops else None
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
@@ -211,24 +225,34 @@ def main():
                 and tj.get("nc") == nc and fused):
             traffic = tj.get("bytes_per_launch")
     executed = None              # executed-instruction view (SQ counters, tools/valu_issue.py)
-    vj = os.path.join(ROOT, "profiles", "r01", "valu_issue.json")
+    vj = os.path.join(ROOT, "profiles", "r02", "valu_issue.json")
     if fused and (ne, nc, B) == (200, 74, 100) and os.path.exists(vj):
         with open(vj) as f:
             ev = json.load(f)
         executed = {"valu_wave_insts_per_launch": ev.get("sq_insts_valu_per_launch"),
                     "issue_frac_chip": round(ev.get("issue_frac_chip", 0.0), 4),
                     "issue_frac_busy_cus": round(ev.get("issue_frac_busy_cus", 0.0), 4),
-                    "source": "profiles/r01/valu_issue.json (rocprofv3 SQ_INSTS_VALU over the "
+                    "source": "profiles/r02/valu_issue.json (rocprofv3 SQ_INSTS_VALU over the "
                               "kernel's rocprof duration; 4 cycles per wave64 VALU op per SIMD)"}
-    roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+    # bound "mfma" = the FP32 compute roof: VALU and MFMA share the 157.3 TFLOP/s peak on
+    # gfx950 (MI355X_MICROARCH.md), and the kernel's FP32 work runs on both
+    roofline = {"bound": "mfma",
+                "achieved": round(achieved, 3) if achieved else None,
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4) if achieved else None,
                 "traffic": traffic, "kernel": dom,
-                "flops_per_launch": flops_launch, "avg_launch_ms": round(kern_ms[dom], 5),
+                "flops_per_launch": exec_flops, "flops_source": flops_src,
+                "avg_launch_ms": round(kern_ms[dom], 5),
                 "algorithmic_bytes_per_launch": hbm_bytes_per_commit(ne, nc) * B,
-                "note": "SURVEY 8(d) dense-graph FLOPs (3 F_fwd per commit) over the measured "
-                        "%s time: work-equivalent, can exceed 1 because the sorted-x / "
-                        "per-node algebra (DESIGN.md 3) does not execute most of them; "
-                        "'executed' is the hardware view (VALU issue-slot utilisation)" % dom,
+                "hbm_frac": (round(traffic / (kern_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if traffic else None),
+                "dense_equivalent": {
+                    "flops_per_launch": dense_launch, "tflops": round(dense_tflops, 3),
+                    "note": "SURVEY 8(d) per-commit figure (3 F_fwd: the TF graph's dense "
+                            "incidence-matrix work) over the same launch time; the engine's "
+                            "sorted-x / per-node algebra (DESIGN.md 3) needs ~13x fewer "
+                            "operations, so this is work-equivalent throughput, not a "
+                            "hardware roofline (no frac)"},
                 "executed": executed}
     cpu = None
     if world == 1 and not args.no_cpu and v == 2:
