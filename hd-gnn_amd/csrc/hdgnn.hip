@@ -264,32 +264,32 @@ __device__ __forceinline__ void pair_tile(
     const int i = rmul * r + radd;
     const bool iv = r < nown;
     p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
-    // rows past the sweep read row 0 and are selected to A = -inf, w = 0 (e = 0): the
-    // sweep may run past the padded buffer when the rows are split by parity
-    const int ib = iv ? i : 0;
+    // rows past the sweep read the first swept row and are masked to A = -inf, w = 0
+    // (e = 0): the sweep may run past the padded buffer when the rows are split by parity
+    const int ib = iv ? i : radd;       // past the sweep: the first swept row (own, finite)
     const float* Ai = A + ib * LD;
-    const float ninf = -INFINITY;
+    // masks applied arithmetically (that row's values are finite): every load of the sweep's
+    // row operands is unconditional, so none of them is sunk into an exec-masked branch
+    // with its own LDS round trip
+    const float addm = iv ? 0.f : -INFINITY, mulm = iv ? 1.f : 0.f;
+    const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      const p2 av = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p);
-      a2[p] = iv ? av : (p2){ninf, ninf};
-      if constexpr (MODE == 1) {
-        const p2 wv2 = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p);
-        rw2[p] = iv ? wv2 : z2;
-      } else {
+      a2[p] = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p) + addm2;
+      if constexpr (MODE == 1)
+        rw2[p] = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p) * mulm2;
+      else
         rw2[p] = z2;
-      }
       racc2[p] = z2;
     }
-    const float at = KT ? (iv ? Ai[ktl] : ninf) : 0.f;
-    const float rwt = (MODE == 1 && KT) ? (iv ? wr[ib * LD + ktl] : 0.f) : 0.f;
+    const float at = KT ? Ai[ktl] + addm : 0.f;
+    const float rwt = (MODE == 1 && KT) ? wr[ib * LD + ktl] * mulm : 0.f;
     float racct = 0.f;
     uint32_t wrow[NW];
+    const uint32_t bmask = iv ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {      // branch-free: clamped load, masked value
-      const uint32_t w = bits[ib * W + (q < W ? q : 0)];
-      wrow[q] = (iv && q < W) ? w : 0u;
-    }
+    for (int q = 0; q < NW; ++q)        // clamped load, masked value
+      wrow[q] = bits[ib * W + (q < W ? q : 0)] & (q < W ? bmask : 0u);
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
