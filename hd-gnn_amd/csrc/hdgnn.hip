@@ -2450,6 +2450,8 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
 //   lr_t = lr sqrt(1-b2^t)/(1-b1^t);  m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 //   var -= lr_t m / (sqrt(v) + eps)     (tensorflow/core/kernels/training_ops.cc ApplyAdam)
 // ------------------------------------------------------------------------------
+constexpr int ADAM_PT = 4;   // parameters per thread: 4 x 1024 >= every variant's count
+
 __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
                                                   float* __restrict__ mm,
                                                   float* __restrict__ vv,
@@ -2461,12 +2463,27 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
   __shared__ float red[16 * 4];
   __shared__ float sh[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // every operand of the thread's parameters is loaded up front: one memory round trip
+  float w[ADAM_PT], g[ADAM_PT], m[ADAM_PT], v[ADAM_PT];
+#pragma unroll
+  for (int u = 0; u < ADAM_PT; ++u) {
+    const int p = t + u * 1024;
+    const bool ok = p < np;
+    w[u] = ok ? params[p] : 0.f;
+    g[u] = ok ? grad[p] : 0.f;
+    m[u] = ok ? mm[p] : 0.f;
+    v[u] = ok ? vv[p] : 0.f;
+  }
+  __shared__ float bp[2];          // beta powers through LDS: only thread 0 touches bpow
+  if (t == 0) { bp[0] = bpow[0]; bp[1] = bpow[1]; }
+  const float ce_sum = grad[np + HDG_TR_CE], fault = grad[np + HDG_TR_FAULT];
   float l2 = 0.f, t1 = 0.f, t2 = 0.f;
-  for (int p = t; p < np; p += 1024) {
-    const float w = params[p];
-    l2 = fmaf(w, w, l2);
-    if (p >= TH1 && p < TH1 + 2) t1 = fmaf(w, w, t1);
-    if (p >= TH2 && p < TH2 + 2) t2 = fmaf(w, w, t2);
+#pragma unroll
+  for (int u = 0; u < ADAM_PT; ++u) {
+    const int p = t + u * 1024;
+    l2 = fmaf(w[u], w[u], l2);
+    if (p >= TH1 && p < TH1 + 2) t1 = fmaf(w[u], w[u], t1);
+    if (p >= TH2 && p < TH2 + 2) t2 = fmaf(w[u], w[u], t2);
   }
   l2 = wave_sum(l2);
   t1 = wave_sum(t1);
@@ -2475,15 +2492,15 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
   __syncthreads();
   if (t < 3) {
     float s = 0.f;
-    for (int w = 0; w < 16; ++w) s += red[w * 4 + t];
+    for (int q = 0; q < 16; ++q) s += red[q * 4 + t];
     sh[t] = s;
   }
   __syncthreads();
   const float n1 = sqrtf(sh[1]), n2 = sqrtf(sh[2]);
-  const float b1p = bpow[0], b2p = bpow[1];
+  const float b1p = bp[0], b2p = bp[1];
   const float lr_t = lr * sqrtf(1.f - b2p) / (1.f - b1p);
   if (t == 0 && stats) {
-    const float ce = grad[np] * inv_pairs;
+    const float ce = ce_sum * inv_pairs;
     const float lmap = 0.01f * (n2 + n1);
     const float lpara = 0.0005f * sh[0];
     stats[0] = ce;
@@ -2491,21 +2508,22 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
     stats[2] = lpara;
     stats[3] = 10.f * ce + 0.1f * lmap + lpara;
   }
-  if (grad[np + HDG_TR_FAULT] != 0.f) return;   // a pair exchange timed out on some rank
+  if (fault != 0.f) return;   // a pair exchange timed out on some rank: no update
   const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
-  for (int p = t; p < np; p += 1024) {
-    const float w = params[p];
-    float g = grad[p] + 0.001f * w;
-    if (p >= TH1 && p < TH1 + 2) g += 0.001f * w / n1;
-    if (p >= TH2 && p < TH2 + 2) g += 0.001f * w / n2;
-    float m = mm[p], v = vv[p];
-    m += (g - m) * (1.f - b1);
-    v += (g * g - v) * (1.f - b2);
-    mm[p] = m;
-    vv[p] = v;
-    params[p] = w - lr_t * m / (sqrtf(v) + ep);
+#pragma unroll
+  for (int u = 0; u < ADAM_PT; ++u) {
+    const int p = t + u * 1024;
+    if (p >= np) break;
+    float gg = g[u] + 0.001f * w[u];
+    if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w[u] / n1;
+    if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w[u] / n2;
+    float mv = m[u], vq = v[u];
+    mv += (gg - mv) * (1.f - b1);
+    vq += (gg * gg - vq) * (1.f - b2);
+    mm[p] = mv;
+    vv[p] = vq;
+    params[p] = w[u] - lr_t * mv / (sqrtf(vq) + ep);
   }
-  __syncthreads();
   if (t == 0) { bpow[0] = b1p * b1; bpow[1] = b2p * b2; }
 }
 
@@ -2886,6 +2904,8 @@ int hdg_adam_tf(const hdg_shape* s, hdg_state* state, const float* grad, float l
                 void* stream) {
   RESOLVE(s, path);
   (void)path;
+  if (hdg::param_offsets(s->variant).NP > ADAM_PT * 1024)
+    return fail(HDG_EINVAL, "k_adam_tf holds at most %d parameters", ADAM_PT * 1024);
   if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow || !grad)
     return fail(HDG_EINVAL, "NULL state/grad pointer");
   hipLaunchKernelGGL(k_adam_tf, dim3(1), dim3(1024), 0, (hipStream_t)stream, state->params,
