@@ -793,7 +793,7 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.red = o;  o += (NT_MID / 64) * 32;
   int u = 3 * NE4 * HS;                                            // P | E_bar | h
   const int uh = nbuf_h(smaxc) * NC16 * HS + NG_MID * cred +      // hunk phases
-                 (gam_lds(smaxc) ? NC16 * NC16 : 0);
+                 (gam_lds(smaxc) ? NC16 * (NC16 + 8) : 0);
   int ueb = 5 * NE4 * HS;                         // E3 bwd: P | E_bar | dq | dE | h/rho
   const int ue2 = 2 * NE4 * HS + 2 * HS * (NE4 + 4) + (NT_MID / 64) * 4 * HS;   // E2 + rho
   if (ue2 > ueb) ueb = ue2;
@@ -1322,6 +1322,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* hEG = EbG + Ne * HS;
   float* pb = part + (size_t)prow * NPART;
   constexpr bool GAML = gam_lds(SMAXC);
+  // LDS gamma row stride: 8 words past NC16 puts rows 2 apart (the two rows a 32-lane
+  // group of pass B reads in split mode) 16 banks apart: no 2-way conflict on its reads
+  constexpr int GLD = GAML ? NC16 + 8 : NC16;
   float* gamG = gamg + (size_t)b * NC16 * NC16;
   uint16_t* rq = rowq + (size_t)b * Ne * HS;
   const float Nc1 = (float)(Nc - 1);
@@ -1706,7 +1709,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
                                        // pass B reads LDS gamma rows unmasked
       for (int e = t; e < ((Nc - radd + rmul - 1) / rmul) * npad; e += NT_MID) {
         const int r2 = e / npad;
-        gam[(rmul * r2 + radd) * NC16 + Nc + (e - r2 * npad)] = 0.f;
+        gam[(rmul * r2 + radd) * GLD + Nc + (e - r2 * npad)] = 0.f;
       }
     }
     for (int el = t; el < Pown; el += NT_MID) {
@@ -1762,9 +1765,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       if (lgb) { lgb[e] = z0; lgb[Pc + e] = z1; }
       if constexpr (TRAIN) {
         if (qq == p || (p == Nc1i && qq == Nc1i - 1))   // defined diagonal, every row
-          gam[p * NC16 + p] = 0.f;
+          gam[p * GLD + p] = 0.f;
         const float gmm = ce_scale * (p1 - yf);   // dL/dz1 = -dL/dz0
-        gam[p * NC16 + q] = gmm;
+        gam[p * GLD + q] = gmm;
         gsum += gmm;
 #pragma unroll
         for (int k = 0; k < HS; k += 2) {       // packed: two hidden units per v_pk_fma
@@ -1828,7 +1831,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* Dsig = sig;
   float* Dtau = tau;
   pair_tile<KK_MID, SMAXC, 2, HS, 0, GAML>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
-                                           nullptr, gam, NC16, Dsig, Dtau, ysumv, credg, rmul,
+                                           nullptr, gam, GLD, Dsig, Dtau, ysumv, credg, rmul,
                                            radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     const int k = e % HS;
