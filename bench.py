@@ -42,16 +42,23 @@ def flops_per_commit(ne, nc, variant=2):
     return 3 * f
 
 
-def hbm_bytes_per_commit(ne, nc):
-    """Bytes one step moves per commit in the engine's compact form: inputs (x, a bits,
-    y bits, prepared tables incl. the two u16 count matrices read twice), the parked
-    P/E_bar/h (written + read back), row boundaries, per-commit gradient row."""
-    H = 20
+def algorithmic_bytes_per_commit(ne, nc):
+    """SURVEY 8(d) / BASELINE.md bytes per commit: 4 Ne^2 + 4 Nc^2 + 4 Pe + 8 Pc (the f32
+    entity adjacency, the f32 label adjacency, int16 src + tgt hunk maps per entity pair,
+    the f32 two-class output per hunk pair)."""
+    pe, pc = ne * (ne - 1), nc * (nc - 1)
+    return 4 * ne * ne + 4 * nc * nc + 4 * pe + 8 * pc
+
+
+def compact_bytes_per_commit(ne, nc):
+    """What the engine's compact form must move per commit and step: inputs (x, a bits and
+    their transpose, y bits, the prepared x tables, the two u16 count matrices), the probs
+    output (C_edge_output2, fetched by the training sess.run) and one partial-gradient row
+    per block (two per commit in split mode)."""
     we, wc = (ne + 31) // 32, (nc + 31) // 32
     inp = 4 * ne + 2 * 4 * ne * we + 4 * nc * wc + 16 * ne
-    kmat = 2 * 2 * (2 * nc * ne)
-    park = 2 * 3 * 4 * ne * H + 2 * 2 * ne * H
-    return inp + kmat + park + 4 * 2136         # + the block's partial-gradient row (NPART)
+    kmat = 2 * (2 * nc * ne)
+    return inp + kmat + 8 * nc * (nc - 1) + 2 * 4 * 2136
 
 
 def cpu_baseline(cb, steps, threads):
@@ -243,7 +250,8 @@ def main():
                 "traffic": traffic, "kernel": dom,
                 "flops_per_launch": exec_flops, "flops_source": flops_src,
                 "avg_launch_ms": round(kern_ms[dom], 5),
-                "algorithmic_bytes_per_launch": hbm_bytes_per_commit(ne, nc) * B,
+                "algorithmic_bytes_per_launch": algorithmic_bytes_per_commit(ne, nc) * B,
+                "compact_bytes_per_launch": compact_bytes_per_commit(ne, nc) * B,
                 "hbm_frac": (round(traffic / (kern_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                              if traffic else None),
                 "dense_equivalent": {

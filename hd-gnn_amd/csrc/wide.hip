@@ -1645,6 +1645,9 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 //   from the lane's own row of a (row pass) or a^T (column pass).
 //   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
 // ---------------------------------------------------------------------------------
+#ifndef EE_ABL          // diagnostic ablation builds only (tools/gpu_eeabl.sh); 0 in the engine
+#define EE_ABL 0
+#endif
 struct EEBwdSmem {
   float* os_;
   float* buf;
@@ -1654,6 +1657,7 @@ struct EEBwdSmem {
   int* hl;
   float* dnl;
   const float* cst;   // U2' (2H) | EE a-offsets d (H) | U2'[k][1] - U2'[k][0] (H): broadcast reads
+  const float* own;   // the 64 lane nodes' own operand rows [TN][H] (read per row, not held)
 };
 
 template <int Z>
@@ -1672,11 +1676,12 @@ __device__ __forceinline__ void ee_clsb_body(
   const float* own = (Z ? rho : gmm) + ((size_t)b * Ne + ncl) * H;
   const uint32_t* brow = (Z ? abits : aT) + ((size_t)b * Ne + ncl) * WE;
   // the weight constants are LDS broadcast reads in the row loop (sm.cst), not registers:
-  // 80 VGPRs fewer, 4 waves per SIMD instead of 2 (two blocks per CU)
-  f2 ow[H2], acc[H2], zk[H2], ag[H2];
+  // 80 VGPRs fewer, 4 waves per SIMD instead of 2 (two blocks per CU); the lane's own
+  // operand row is an LDS read per row too (sm.own): 20 VGPRs fewer, no spills
+  (void)own;
+  f2 acc[H2], zk[H2], ag[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
-    ow[kk] = ld2(own + 2 * kk);
     acc[kk] = (f2){0.f, 0.f};
     zk[kk] = acc[kk];
     ag[kk] = acc[kk];
@@ -1706,7 +1711,7 @@ __device__ __forceinline__ void ee_clsb_body(
       const int r = i * (Ne - 1) + j - (j > i ? 1 : 0);
       const bool valid = nd < Ne && i != j && r < nrel;
       float dp0 = 0.f, dp1 = 0.f;
-      if (valid) {
+      if (valid && !(EE_ABL & 2)) {
         int ip, jj;
         divmod24(r, dn1, inv, ip, jj);
         const int jp = jj + (jj >= ip ? 1 : 0);
@@ -1721,13 +1726,14 @@ __device__ __forceinline__ void ee_clsb_body(
       const float4* cu2 = reinterpret_cast<const float4*>(sm.cst + co);          // u2 pairs
       const float4* cdl = reinterpret_cast<const float4*>(sm.cst + co + 2 * H);  // d
       const float4* ccE = reinterpret_cast<const float4*>(sm.cst + co + 3 * H);  // c
+      const float4* ow4 = reinterpret_cast<const float4*>(sm.own + co + lane * H);
       f2 pre[H2];
       f2 zz = bb;
 #pragma unroll
       for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j: the same sum kw_ee_fwd forms
-        const float4 q = o4[v], dv = cdl[v];
-        pre[2 * v] = fma2(a2, (f2){dv.x, dv.y}, ow[2 * v] + (f2){q.x, q.y});
-        pre[2 * v + 1] = fma2(a2, (f2){dv.z, dv.w}, ow[2 * v + 1] + (f2){q.z, q.w});
+        const float4 q = o4[v], dv = cdl[v], w4 = ow4[v];
+        pre[2 * v] = fma2(a2, (f2){dv.x, dv.y}, (f2){w4.x, w4.y} + (f2){q.x, q.y});
+        pre[2 * v + 1] = fma2(a2, (f2){dv.z, dv.w}, (f2){w4.z, w4.w} + (f2){q.z, q.w});
       }
 #pragma unroll
       for (int kk = 0; kk < H2; ++kk) {
@@ -1736,10 +1742,15 @@ __device__ __forceinline__ void ee_clsb_body(
         zz = fma2((f2){kp.x, kp.x}, (f2){w.x, w.y}, zz);
         zz = fma2((f2){kp.y, kp.y}, (f2){w.z, w.w}, zz);
       }
-      const float mx = fmaxf(zz.x, zz.y);
-      const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
-      const float iv = __builtin_amdgcn_rcpf(e0 + e1);    // e0 + e1 in [1, 2]: 1-ulp rcp
-      const float p0 = e0 * iv, p1 = e1 * iv;
+      float p0, p1;
+      if constexpr (EE_ABL & 4) {
+        p0 = zz.x; p1 = zz.y;
+      } else {
+        const float mx = fmaxf(zz.x, zz.y);
+        const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
+        const float iv = __builtin_amdgcn_rcpf(e0 + e1);    // e0 + e1 in [1, 2]: 1-ulp rcp
+        p0 = e0 * iv; p1 = e1 * iv;
+      }
       const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
       const f2 d2 = {d1, d1};
       float gv[H];
@@ -1760,7 +1771,14 @@ __device__ __forceinline__ void ee_clsb_body(
         sdl += d1;
         // the row pass folded in: this tile's 64 columns of row i = m, one partial row
         // of drho per tile (kw_ee_nodeb sums the te partials in tile order)
-        wave_sums20(gv, lane, [&](int k, float x) { rowp[(size_t)m * H + k] = x; });
+        if constexpr (EE_ABL & 1) {
+          float sgv = 0.f;
+#pragma unroll
+          for (int k = 0; k < H; ++k) sgv += gv[k];
+          if (lane == 0) rowp[(size_t)m * H] = sgv;
+        } else {
+          wave_sums20(gv, lane, [&](int k, float x) { rowp[(size_t)m * H + k] = x; });
+        }
       }
     }
   }
@@ -1813,12 +1831,22 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   __shared__ float red[NWP * 41];
   __shared__ float tot[41];
   __shared__ __attribute__((aligned(16))) float cst[4 * H];
+  __shared__ __attribute__((aligned(16))) float owl[TN * H];
   const int b = blockIdx.y;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   const int nrel = n >= 2 ? n * (n - 1) : 0;
   EEBwdSmem sm;
   sm.os_ = os_; sm.buf = buf; sm.res = res; sm.red = red; sm.tot = tot; sm.cst = cst;
+  sm.own = owl;
+  {                         // the lane nodes' own rows (column pass: gam rows t0 .. t0 + 63)
+    const int t0 = blockIdx.x * TN;
+    const float4* src = reinterpret_cast<const float4*>(gmm + (size_t)b * Ne * H);
+    for (int e = threadIdx.x; e < TN * (H / 4); e += NTP) {
+      const int l = e / (H / 4), node = t0 + l < Ne ? t0 + l : Ne - 1;
+      reinterpret_cast<float4*>(owl)[e] = src[(size_t)node * (H / 4) + e - l * (H / 4)];
+    }
+  }
   sm.hl = reinterpret_cast<int*>(dyn);
   sm.dnl = dyn + Ne;
   if (threadIdx.x < 2 * H) cst[threadIdx.x] = W[o.EC_W2 + threadIdx.x];

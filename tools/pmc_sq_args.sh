@@ -1,0 +1,13 @@
+#!/bin/bash
+# SQ counters per kernel for bench.py with extra arguments (two --pmc passes).
+#   BENCH_ARGS="--variant 4" bash tools/pmc_sq_args.sh <tag>
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/pmc_sq_${1:-x}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -f csv -d $OUT/a -o run -- \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --no-graph $BENCH_ARGS > $OUT/a.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES -f csv -d $OUT/b -o run -- \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --no-graph $BENCH_ARGS > $OUT/b.log 2>&1 || exit $?
+cd $R && python3 tools/pmc_table.py $OUT
