@@ -683,6 +683,9 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
 //   go out as one partial row per tile.
 // ---------------------------------------------------------------------------------
 constexpr int EE_GAM_LDS_MAX = 800;   // Ne up to which the commit's gam table sits in LDS
+#ifndef EE_ABL          // diagnostic ablation builds only (tools/gpu_eeabl.sh); 0 in the engine
+#define EE_ABL 0
+#endif
 
 __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                  const int32_t* __restrict__ hidg,
@@ -730,17 +733,31 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   int cur = ei;
   const f2 bb = ld2(W + o.EC_B2);
   float s0 = 0.f, s1 = 0.f;
+  // class-bit words: the lane's relations walk the a-bit rows in order, so the word index
+  // ei * WE + (j >> 5) grows by at most one per relation; the next word is prefetched
+  // when the current one is taken, so the load's latency is never on the relation chain
+  const uint32_t* ab = abits + (size_t)b * Ne * WE;
+  const int wlast = Ne * WE - 1;
+  int widx = (ei < Ne ? ei : Ne - 1) * WE + ((ejj + (ejj >= ei ? 1 : 0)) >> 5);
+  widx = widx < wlast ? widx : wlast;
+  uint32_t wcur = ab[widx], wnxt = ab[widx + 1 < wlast ? widx + 1 : wlast];
   for (int jp = jlo; jp < jhi; ++jp) {
     const bool valid = live && jp != ip;
     float p0 = 0.f, p1 = 0.f;
     if (valid) {
       const int ej = ejj + (ejj >= ei ? 1 : 0);
-      if (ei != cur) {
+      if (ei != cur && !(EE_ABL & 16)) {
 #pragma unroll
         for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + ei * H + 2 * kk);
         cur = ei;
       }
-      const float af = bitf(abits + ((size_t)b * Ne + ei) * WE, ej);
+      const int nidx = ei * WE + (ej >> 5);
+      if (nidx != widx) {
+        wcur = nidx == widx + 1 ? wnxt : ab[nidx];
+        widx = nidx;
+        wnxt = ab[nidx + 1 < wlast ? nidx + 1 : wlast];
+      }
+      const float af = (EE_ABL & 8) ? 0.f : (((wcur >> (ej & 31)) & 1u) ? 1.f : 0.f);
       const f2 a2 = {af, af};
       const float4* g4 = reinterpret_cast<const float4*>(gt + (size_t)ej * H);
       f2 zz = bb;
@@ -765,7 +782,8 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     s1 += p1;
     const float w01 = wsum2(p0, p1);                 // lane 0: sum p0, lane 32: sum p1
     const int ht = hid[jp];
-    if ((lane & 31) == 0 && ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (lane >> 5)], qfix(w01));
+    if (!(EE_ABL & 32) && (lane & 31) == 0 && ht >= 0 && ht < Nc)
+      atomicAdd(&bins[2 * ht + (lane >> 5)], qfix(w01));
   }
   if (live) {
     const int hs = hid[ip];
@@ -1645,9 +1663,6 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 //   from the lane's own row of a (row pass) or a^T (column pass).
 //   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
 // ---------------------------------------------------------------------------------
-#ifndef EE_ABL          // diagnostic ablation builds only (tools/gpu_eeabl.sh); 0 in the engine
-#define EE_ABL 0
-#endif
 struct EEBwdSmem {
   float* os_;
   float* buf;

@@ -8,10 +8,11 @@ rc=$?; tail -3 gpurun_out/gen_tests.log; [ $rc -ne 0 ] && exit $rc
 R=$(pwd)
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/gen_prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu $BA > $R/gpurun_out/gen_prof.log 2>&1) || exit $?
 python3 - <<'PY'
-import csv, glob, json
+import csv, glob, json, re
 f = sorted(glob.glob("gpurun_out/gen_prof/**/*kernel_stats.csv", recursive=True))[0]
 for r in list(csv.DictReader(open(f)))[:14]:
-    print("%-28s %6s %9.2f us" % (r["Name"].split("(")[0][-28:], r["Calls"], float(r["AverageNs"]) / 1e3))
+    n = re.sub(r"\(.*", "", r["Name"]).replace("void ", "").replace("hdg::", "")
+    print("%-28s %6s %9.2f us" % (n[:28], r["Calls"], float(r["AverageNs"]) / 1e3))
 for l in open("gpurun_out/gen_prof.log"):
     if l.startswith("{"):
         d = json.loads(l); print("bench(traced)", d["value"], d["ms_per_step"])
