@@ -4,8 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-A step = hdg_fwd_bwd + (RCCL all-reduce of the flat gradient when N > 1) + hdg_adam_tf
-on 100 resident synthetic glide-shaped commits per GPU (weak scaling).  Rank 0 prints
+A step = the fused step kernel + the gradient reduction + TF Adam on 100 resident
+synthetic glide-shaped commits per GPU (weak scaling); under torch.distributed.run the
+reduction kernel also all-reduces the flat gradient over xGMI (hdg_train_step_dp; RCCL
+when HDG_DP_ALLREDUCE=rccl or the ranks span hosts).  Rank 0 prints
 one JSON line.  Per-kernel durations come from HIP events recorded on the launch stream;
 the CPU baseline is oracle/literal.py (the TF graph's op sequence on torch-CPU).
 """
@@ -193,7 +195,7 @@ def main():
         bstruct = db.struct()
         _lib.check(eng.lib.hdg_fwd_bwd_events(ctypes.byref(eng.shape), ctypes.byref(bstruct),
                                               ctypes.c_void_p(eng.params.data_ptr()),
-                                              ctypes.c_void_p(eng.grad.data_ptr()),
+                                              ctypes.c_void_p(eng.grad_local.data_ptr()),
                                               ctypes.byref(eng._out),
                                               ctypes.c_void_p(eng.workspace.data_ptr()),
                                               eng._stream(), ev.ev))
@@ -268,7 +270,11 @@ def main():
         cpu = cpu_baseline(cb, args.cpu_steps, threads)
     line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
-            "allreduce": "rccl all_reduce of the flat gradient per step" if launched else None,
+            "allreduce": {"xgmi": "in-kernel xGMI exchange of the flat gradient per step "
+                                  "(hdg_train_step_dp: tagged words into every peer's "
+                                  "mailbox, rank-order sum, TF Adam in the same kernel)",
+                          "rccl": "rccl all_reduce of the flat gradient per step"}.get(
+                              eng.allreduce_kind) if launched else None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)",
             "config": {"workload": "model_%d (%s) train step: fwd+bwd+TF-Adam, %s" % (

@@ -2531,6 +2531,209 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
 }
 
 // ------------------------------------------------------------------------------
+// Data-parallel tail over xGMI (include/hdgnn.h hdg_*_dp).
+// Every rank owns a mailbox of uncached device memory that each peer maps through HIP
+// IPC.  Block k of the tail kernel owns gradient slots [16k, 16k + 16): it forms its
+// local values (the fixed-order sum of the partial rows, or the rank's reduced gradient),
+// writes each as an 8-byte (value, tag) word with a system-scope write-through store into
+// slot (parity, rank, p) of EVERY peer's mailbox (xGMI, one hop, all peers at once; the
+// 8-byte word is single-copy atomic, as in RCCL's LL protocol), polls its own mailbox for
+// the peers' words with L2-bypassing loads, and sums the world's values in rank order
+// 0..W-1: every rank holds the same bits, so the replicas stay bitwise equal.
+//   tag = epoch << 1 | fault: epoch is a per-block launch counter kept in the own mailbox
+//   (all ranks issue the same launches); parity = epoch & 1 double-buffers the words, so
+//   a rank one launch ahead writes over words every peer has already read (it needed the
+//   peers' words of its previous launch, which they sent after reading theirs).  A peer
+//   that never arrives ends the wait after wait_ticks: HDG_STATUS_DP_TIMEOUT, NaN loss,
+//   no update on that block -- never a hang.
+// ------------------------------------------------------------------------------
+namespace dpk {
+constexpr int MAXW = HDG_DP_MAX_WORLD;
+constexpr int GLENP = HDG_DP_MAX_LEN;               // >= every variant's grad length, x16
+constexpr int NBLK = GLENP / RED_P;
+constexpr size_t DATA_WORDS = 2ull * MAXW * GLENP;  // u64 (value, tag) words
+constexpr size_t OFF_EPOCH = DATA_WORDS * 8;        // u32 [256] per-block launch counters
+constexpr size_t OFF_AUX = OFF_EPOCH + 256 * 4;     // f32 [8] loss terms + Adam factor
+constexpr size_t OFF_GLOC = OFF_AUX + 8 * 4;        // f32 [GLENP] the rank's own gradient
+constexpr size_t BYTES = OFF_GLOC + GLENP * 4;      //   (general path, hdg_train_step_dp)
+constexpr unsigned long long WAIT_DEFAULT = 1000000000ull;   // 10 s of s_memrealtime
+static_assert(GLENP % RED_P == 0 && NBLK <= 256, "mailbox layout");
+static_assert(GLENP >= 3129 + HDG_TRAILER, "every variant's gradient fits a mailbox row");
+enum { SUM = 0, PART = 1, GRAD = 2 };
+}  // namespace dpk
+// SUM / GRAD blocks only move 16 words per rank: 256 threads (16 ranks x 16 slots), so
+// the grid stays small and resident even when several ranks share one device (tests);
+// PART runs k_reduce_adam's 1024-thread reduction first
+constexpr int DP_NT_LIGHT = dpk::MAXW * RED_P;
+
+struct DpArgs {
+  uint32_t* box[dpk::MAXW];
+  int rank, world;
+  unsigned long long wait;
+};
+
+typedef uint32_t xu2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void dstore2(uint32_t* p, const xu2 w) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ xu2 dload2(const uint32_t* p) {
+  xu2 w;
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(w) : "v"(p) : "memory");
+  return w;
+}
+__device__ __forceinline__ uint32_t* dp_slot(uint32_t* box, uint32_t par, int src, int p) {
+  return box + 2 * (((size_t)par * dpk::MAXW + src) * dpk::GLENP + p);
+}
+
+// MODE SUM:  gout = world sum of src[0..glen)                       (hdg_dp_allreduce)
+// MODE PART: local = fixed-order sum of R partial rows (k_reduce_adam's reduction), then
+//            world sum -> gout, TF Adam with aux from k_commit_step   (hdg_train_step_dp)
+// MODE GRAD: local = src[0..glen) (a rank's reduced gradient), aux from k_dp_aux (hdg_adam_dp)
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_dp_tail(const float* __restrict__ src, const int R,
+                                                  const int np, const int glen,
+                                                  float* __restrict__ gout,
+                                                  float* __restrict__ params,
+                                                  float* __restrict__ mm, float* __restrict__ vv,
+                                                  float* __restrict__ bpow,
+                                                  const float* __restrict__ aux, const float lr,
+                                                  const float inv_pairs,
+                                                  float* __restrict__ stats,
+                                                  uint32_t* __restrict__ status,
+                                                  const int fault_rows, const DpArgs d) {
+  __shared__ RedShared sh;
+  __shared__ float gl[RED_P];
+  __shared__ float vals[dpk::MAXW][RED_P];
+  __shared__ uint32_t s_ep, s_cnt;
+  const int t = threadIdx.x, blk = blockIdx.x;
+  const int l = t & (RED_P - 1), r = t / RED_P;
+  const int p = blk * RED_P + l;
+  uint32_t* own = d.box[d.rank];
+  uint32_t* ep = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(own) + dpk::OFF_EPOCH);
+  if (t == 0) s_ep = ep[blk] + 1u;
+  // the update's operands are fetched first so their latency overlaps the reduction
+  bool upd = MODE != dpk::SUM && t < RED_P && p < np;
+  const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
+  float g = 0.f;
+  bool bad = false;
+  if constexpr (MODE == dpk::PART) {
+    for (int q = t; q < fault_rows; q += 1024)
+      bad |= src[(size_t)q * NPART + m2::NP + HDG_TR_FAULT] != 0.f;
+    uint32_t cnt;
+    g = reduce_commits(src, R, p, p < glen, sh, cnt);
+    if (t < RED_P && p == CNT_SLOT) s_cnt = cnt;
+  } else {
+    if (t < RED_P && p < glen) g = src[p];
+    if constexpr (MODE == dpk::GRAD) bad = t == 0 && src[np + HDG_TR_FAULT] != 0.f;
+  }
+  bad = __syncthreads_or(bad);               // also publishes s_ep and s_cnt
+  if (t < RED_P) {
+    if (MODE == dpk::PART && p >= CNT_SLOT && p <= CNT_SLOT + 2)   // three 16-bit parts
+      g = p == CNT_SLOT ? (float)(s_cnt & 0xFFFFu) : (p == CNT_SLOT + 1 ? (float)(s_cnt >> 16) : 0.f);
+    gl[l] = g;
+  }
+  __syncthreads();
+  const uint32_t e = s_ep, par = e & 1u;
+  const bool mine = r < d.world && p < glen;
+  if (mine && r != d.rank)                    // to every peer at once
+    dstore2(dp_slot(d.box[r], par, d.rank, p),
+            (xu2){__float_as_uint(gl[l]), (e << 1) | (bad ? 1u : 0u)});
+  bool late = false, rbad = false;
+  if (mine) {
+    float v = gl[l];
+    if (r != d.rank) {
+      const uint32_t* in = dp_slot(own, par, r, p);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      xu2 wd = dload2(in);
+      while ((wd.y >> 1) != (e & 0x7FFFFFFFu)) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > d.wait) { late = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+        wd = dload2(in);
+      }
+      v = __uint_as_float(wd.x);
+      rbad = (wd.y & 1u) != 0u;
+    }
+    vals[r][l] = v;
+  }
+  const bool anylate = __syncthreads_or(late);
+  const bool anybad = __syncthreads_or(rbad) || bad;
+  if (t == 0) ep[blk] = e;                    // this block's launch is consumed
+  if (t >= RED_P || p >= glen) return;
+  float tot = 0.f;
+  for (int q = 0; q < d.world; ++q) tot += vals[q][l];
+  if (MODE != dpk::SUM && p == np + HDG_TR_CE && anylate) tot = __builtin_nanf("");
+  gout[p] = tot;
+  if (anylate && t == 0 && status) xstore1(status, HDG_STATUS_DP_TIMEOUT);
+  if constexpr (MODE == dpk::SUM) return;
+  const int TH1 = np - 4, TH2 = np - 2;
+  if (p == np + HDG_TR_CE && stats) {
+    const float ce = tot * inv_pairs;
+    stats[0] = ce;
+    stats[1] = aux[1];
+    stats[2] = aux[0];
+    stats[3] = 10.f * ce + 0.1f * aux[1] + aux[0];
+  }
+  if (anylate || anybad) upd = false;
+  if (upd) {
+    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+    const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
+    float gg = tot + 0.001f * w;
+    if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / n1;
+    if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / n2;
+    float m = m0, v = v0;
+    m += (gg - m) * (1.f - b1);
+    v += (gg * gg - v) * (1.f - b2);
+    mm[p] = m;
+    vv[p] = v;
+    params[p] = w - lr_t * m / (sqrtf(v) + eps);
+  }
+  if (blk == 0 && t == 0 && upd) {
+    bpow[0] = aux[5];
+    bpow[1] = aux[6];
+  }
+}
+
+// aux for MODE GRAD (k_commit_step's block 0 writes it on the fused path): loss terms of
+// the pre-update parameters (model_2.py:123-130, 326-333) and TF ApplyAdam's lr factor,
+// in k_adam_tf's summation order
+__global__ __launch_bounds__(1024) void k_dp_aux(const float* __restrict__ params, const int np,
+                                                 const float* __restrict__ bpow,
+                                                 float* __restrict__ aux) {
+  const int TH1 = np - 4, TH2 = np - 2;
+  __shared__ float red[16 * 4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float l2 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < ADAM_PT; ++u) {
+    const int p = t + u * 1024;
+    const float w = p < np ? params[p] : 0.f;
+    l2 = fmaf(w, w, l2);
+    if (p >= TH1 && p < TH1 + 2) t1 = fmaf(w, w, t1);
+    if (p >= TH2 && p < TH2 + 2) t2 = fmaf(w, w, t2);
+  }
+  l2 = wave_sum(l2);
+  t1 = wave_sum(t1);
+  t2 = wave_sum(t2);
+  if (lane == 0) { red[wv * 4] = l2; red[wv * 4 + 1] = t1; red[wv * 4 + 2] = t2; }
+  __syncthreads();
+  if (t == 0) {
+    float s[3] = {0.f, 0.f, 0.f};
+    for (int q = 0; q < 16; ++q)
+      for (int c = 0; c < 3; ++c) s[c] += red[q * 4 + c];
+    const float n1 = sqrtf(s[1]), n2 = sqrtf(s[2]);
+    const float b1p = bpow[0], b2p = bpow[1];
+    aux[0] = 0.0005f * s[0];
+    aux[1] = 0.01f * (n2 + n1);
+    aux[2] = n1;
+    aux[3] = n2;
+    aux[4] = sqrtf(1.f - b2p) / (1.f - b1p);
+    aux[5] = b1p * 0.9f;
+    aux[6] = b2p * 0.999f;
+  }
+}
+
+// ------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------
 int smax_c(int nc) { return nc <= 80 ? 5 : (nc <= 128 ? 8 : 10); }
@@ -2964,6 +3167,145 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
                        part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);
     HIP_TRY(hipGetLastError());
   }
+  return 0;
+}
+
+// ---- data parallelism over xGMI ------------------------------------------------
+static_assert(sizeof(hipIpcMemHandle_t) == HDG_DP_HANDLE_BYTES, "IPC handle size");
+
+size_t hdg_dp_mailbox_bytes(void) { return dpk::BYTES; }
+
+int hdg_dp_mailbox_alloc(void** mailbox, void* handle) {
+  if (!mailbox || !handle) return fail(HDG_EINVAL, "NULL mailbox/handle pointer");
+  *mailbox = nullptr;
+  // uncached: the peers' write-through words and this rank's polling loads meet in memory
+  HIP_TRY(hipExtMallocWithFlags(mailbox, dpk::BYTES, hipDeviceMallocUncached));
+  hipIpcMemHandle_t h;
+  hipError_t e = hipMemset(*mailbox, 0, dpk::BYTES);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&h, *mailbox);
+  if (e != hipSuccess) {
+    (void)hipFree(*mailbox);
+    *mailbox = nullptr;
+    return fail((int)e, "mailbox setup: %s", hipGetErrorString(e));
+  }
+  memcpy(handle, &h, sizeof(h));
+  return 0;
+}
+
+int hdg_dp_mailbox_open(const void* handle, void** mailbox) {
+  if (!mailbox || !handle) return fail(HDG_EINVAL, "NULL mailbox/handle pointer");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  *mailbox = nullptr;
+  HIP_TRY(hipIpcOpenMemHandle(mailbox, h, hipIpcMemLazyEnablePeerAccess));
+  return 0;
+}
+
+int hdg_dp_mailbox_close(void* mailbox) {
+  HIP_TRY(hipIpcCloseMemHandle(mailbox));
+  return 0;
+}
+
+int hdg_dp_mailbox_free(void* mailbox) {
+  HIP_TRY(hipFree(mailbox));
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+int dp_args(const hdg_dp* dp, DpArgs& a) {
+  if (!dp) return fail(HDG_EINVAL, "NULL hdg_dp");
+  if (dp->world < 1 || dp->world > HDG_DP_MAX_WORLD || dp->rank < 0 || dp->rank >= dp->world)
+    return fail(HDG_EINVAL, "hdg_dp: rank %d / world %d out of range (world <= %d)", dp->rank,
+                dp->world, HDG_DP_MAX_WORLD);
+  memset(&a, 0, sizeof(a));
+  for (int r = 0; r < dp->world; ++r) {
+    if (!dp->mailbox[r]) return fail(HDG_EINVAL, "hdg_dp: mailbox of rank %d is NULL", r);
+    a.box[r] = (uint32_t*)dp->mailbox[r];
+  }
+  a.rank = dp->rank;
+  a.world = dp->world;
+  a.wait = dp->wait_ticks ? dp->wait_ticks : dpk::WAIT_DEFAULT;
+  return 0;
+}
+float* dp_aux(const hdg_dp* dp) {
+  return (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_AUX);
+}
+}  // namespace
+
+extern "C" {
+
+int hdg_dp_allreduce(const hdg_dp* dp, const float* in, float* out, int32_t n, uint32_t* status,
+                     void* stream) {
+  DpArgs a;
+  if (int rc = dp_args(dp, a)) return rc;
+  if (!in || !out || n < 1 || n > HDG_DP_MAX_LEN)
+    return fail(HDG_EINVAL, "hdg_dp_allreduce: NULL buffer or n=%d outside [1, %d]", n,
+                HDG_DP_MAX_LEN);
+  hipLaunchKernelGGL(k_dp_tail<dpk::SUM>, dim3((n + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT), 0,
+                     (hipStream_t)stream, in, 1, 0, n, out, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, 0.f, 0.f, nullptr, status, 0, a);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int hdg_adam_dp(const hdg_shape* s, hdg_state* state, const float* grad_local, float* grad_out,
+                float lr, float* stats, uint32_t* status, const hdg_dp* dp, void* stream) {
+  RESOLVE(s, path);
+  (void)path;
+  DpArgs a;
+  if (int rc = dp_args(dp, a)) return rc;
+  if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow ||
+      !grad_local || !grad_out)
+    return fail(HDG_EINVAL, "NULL state/grad pointer");
+  const int np = hdg::param_offsets(s->variant).NP, glen = np + HDG_TRAILER;
+  hipStream_t st = (hipStream_t)stream;
+  float* aux = dp_aux(dp);
+  hipLaunchKernelGGL(k_dp_aux, dim3(1), dim3(1024), 0, st, state->params, np, state->beta_pow,
+                     aux);
+  hipLaunchKernelGGL(k_dp_tail<dpk::GRAD>, dim3((glen + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT), 0, st,
+                     grad_local, 1, np, glen, grad_out, state->params, state->adam_m,
+                     state->adam_v, state->beta_pow, aux, lr, 1.f / pair_count(s), stats, status,
+                     0, a);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int hdg_train_step_dp(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, float lr,
+                      hdg_outputs* out, float* grad, void* workspace, const hdg_dp* dp,
+                      void* stream) {
+  if (!state || !state->params || !state->adam_m || !state->adam_v || !state->beta_pow)
+    return fail(HDG_EINVAL, "NULL state pointer");
+  RESOLVE(s, path);
+  if (int rc = check_batch(bt)) return rc;
+  if (!grad || !workspace) return fail(HDG_EINVAL, "NULL grad/workspace");
+  DpArgs a;
+  if (int rc = dp_args(dp, a)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* status = out ? out->status : nullptr;
+  float* stats = out ? out->stats : nullptr;
+  if (path == HDG_PATH_GENERAL) {
+    // the rank's own reduced gradient lands in the mailbox's local scratch (the tail
+    // reads it while other blocks already write the world sums into grad)
+    float* local = (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_GLOC);
+    if (int rc = hdg::wide_run(s, bt, state->params, local, out, nullptr, workspace, true, st))
+      return rc;
+    return hdg_adam_dp(s, state, local, grad, lr, stats, status, dp, stream);
+  }
+  // fused path: k_commit_step (aux from block 0), then the reduction + exchange + Adam
+  const Work w = work_layout(s);
+  float* ws = (float*)workspace;
+  const float pairs = pair_count(s);
+  const bool split = use_split(s);
+  HIP_TRY(dispatch_step<true>(s, bt, state->params, ws, w, step_out(out), 10.f / pairs, nullptr,
+                              st, split, state->beta_pow));
+  hipLaunchKernelGGL(k_dp_tail<dpk::PART>, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0,
+                     st, ws + w.part, part_rows(s, split), m2::NP, GRAD_LEN, grad, state->params,
+                     state->adam_m, state->adam_v, state->beta_pow, ws + w.aux, lr, 1.f / pairs,
+                     stats, status, split ? part_rows(s, split) : 0, a);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

@@ -38,10 +38,18 @@ class Outputs(ctypes.Structure):
                 ("stats", ctypes.c_void_p), ("status", ctypes.c_void_p)]
 
 
-ABI_VERSION = 4
+class Dp(ctypes.Structure):
+    """hdg_dp: this rank's view of the node's xGMI mailboxes (include/hdgnn.h)."""
+    _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("wait_ticks", ctypes.c_uint64), ("mailbox", ctypes.c_void_p * 16)]
+
+
+DP_MAX_WORLD, DP_HANDLE_BYTES, DP_MAX_LEN = 16, 64, 3152
+
+ABI_VERSION = 5
 # gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
 TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
-STATUS_XCH_TIMEOUT = 1
+STATUS_XCH_TIMEOUT, STATUS_DP_TIMEOUT = 1, 2
 
 
 def trailer_count(tr):
@@ -53,7 +61,9 @@ def trailer_count(tr):
 EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count", "hdg_grad_len",
            "hdg_workspace_bytes", "hdg_prep_bytes", "hdg_prepare", "hdg_fwd_bwd",
            "hdg_fwd_bwd_events", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
-           "hdg_debug_step_stamps", "hdg_prep_counts_layout"]
+           "hdg_debug_step_stamps", "hdg_prep_counts_layout", "hdg_dp_mailbox_bytes",
+           "hdg_dp_mailbox_alloc", "hdg_dp_mailbox_open", "hdg_dp_mailbox_close",
+           "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce"]
 
 _lib = None
 
@@ -89,6 +99,15 @@ def load(path=None):
     lib.hdg_adam_tf.argtypes = [P(Shape), P(State), vp, f32, vp, vp]
     lib.hdg_train_step.argtypes = [P(Shape), P(Batch), P(State), f32, P(Outputs), vp, vp, vp]
     lib.hdg_forward.argtypes = [P(Shape), P(Batch), vp, P(Outputs), vp, vp, vp]
+    lib.hdg_dp_mailbox_bytes.restype = ctypes.c_size_t
+    lib.hdg_dp_mailbox_alloc.argtypes = [P(vp), vp]
+    lib.hdg_dp_mailbox_open.argtypes = [vp, P(vp)]
+    lib.hdg_dp_mailbox_close.argtypes = [vp]
+    lib.hdg_dp_mailbox_free.argtypes = [vp]
+    lib.hdg_train_step_dp.argtypes = [P(Shape), P(Batch), P(State), f32, P(Outputs), vp, vp,
+                                      P(Dp), vp]
+    lib.hdg_adam_dp.argtypes = [P(Shape), P(State), vp, vp, f32, vp, vp, P(Dp), vp]
+    lib.hdg_dp_allreduce.argtypes = [P(Dp), vp, vp, i32, vp, vp]
     for name in EXPORTS:
         getattr(lib, name)
     _lib = lib

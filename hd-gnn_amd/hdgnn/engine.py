@@ -2,10 +2,14 @@
 
 Owns the fp32 parameter vector, TF-Adam state, gradient buffer, workspace and
 per-step outputs on one GPU.  One training step = hdg_fwd_bwd -> (all-reduce of
-the flat gradient + CE-sum trailer when world > 1) -> hdg_adam_tf, all enqueued
-on torch's current stream (so a torch.cuda.CUDAGraph can capture it).
+the flat gradient + CE-sum trailer when distributed) -> hdg_adam_tf, all enqueued
+on torch's current stream (so a torch.cuda.CUDAGraph can capture it).  The
+all-reduce is the in-kernel xGMI exchange (hdgnn/xgmi.py, hdg_train_step_dp) when
+every rank is on this node, else torch.distributed (RCCL); HDG_DP_ALLREDUCE or the
+`allreduce` argument ("auto" | "xgmi" | "rccl") overrides the choice.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -16,7 +20,7 @@ from .layout import n_params
 
 class Engine:
     def __init__(self, ne, nc, batch, variant=2, device="cuda", batch_global=None, lr=3e-4,
-                 process_group=None, path=_lib.PATH_AUTO):
+                 process_group=None, path=_lib.PATH_AUTO, allreduce=None):
         """variant: model_<variant>.py (1 HD-GNN/ES, 2 HD-GNN/S, 3 HD-GNN/E, 4 HD-GNN).
         path: PATH_AUTO (fused kernel when it applies, else the general path),
         PATH_FUSED or PATH_GENERAL (include/hdgnn.h)."""
@@ -61,6 +65,21 @@ class Engine:
         # a training sess.run fetches C_edge_output2 (the probabilities), not the logits
         self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr(), st)
         self._out_none = _lib.Outputs(None, None, None, st)   # status only
+        # data parallelism: which all-reduce joins the ranks' gradients
+        self.xgmi, self.allreduce_kind = None, None
+        if self._distributed():
+            mode = allreduce or os.environ.get("HDG_DP_ALLREDUCE", "auto")
+            if mode not in ("auto", "xgmi", "rccl"):
+                raise ValueError("allreduce must be auto, xgmi or rccl (got %r)" % mode)
+            if mode != "rccl":
+                from .xgmi import XgmiGroup
+                self.xgmi = XgmiGroup.create(self.lib, self.pg or torch.distributed.group.WORLD,
+                                             dev, required=mode == "xgmi")
+            self.allreduce_kind = "xgmi" if self.xgmi else "rccl"
+        # hdg_fwd_bwd's own (local) gradient: the xGMI tail reads it while writing the
+        # world sum into self.grad, so the two must not overlap
+        self.grad_local = (torch.zeros(self.glen, dtype=f32, device=dev) if self.xgmi
+                           else self.grad)
 
     # ---- parameters ---------------------------------------------------------
     def set_params(self, flat):
@@ -98,6 +117,11 @@ class Engine:
         """Raise if any launch since the last clear_status() failed on the device (the
         sticky status word, include/hdgnn.h).  Synchronises with the device."""
         st = int(self.status.item())
+        if st & _lib.STATUS_DP_TIMEOUT:
+            raise RuntimeError(
+                "libhdgnn: a peer rank's gradient words did not arrive over xGMI in time (a "
+                "rank stopped or issued a different sequence of steps); that step's loss is "
+                "NaN and its update was skipped on the waiting blocks.")
         if st & _lib.STATUS_XCH_TIMEOUT:
             raise RuntimeError(
                 "libhdgnn: a block-pair exchange of the fused split path timed out (the two "
@@ -122,16 +146,27 @@ class Engine:
         out = self._outputs(outputs, logits)
         _lib.check(self.lib.hdg_fwd_bwd(ctypes.byref(self.shape), ctypes.byref(b),
                                         ctypes.c_void_p(self.params.data_ptr()),
-                                        ctypes.c_void_p(self.grad.data_ptr()),
+                                        ctypes.c_void_p(self.grad_local.data_ptr()),
                                         ctypes.byref(out),
                                         ctypes.c_void_p(self.workspace.data_ptr()),
                                         self._stream()))
 
     def allreduce(self):
-        if self._distributed():
+        """RCCL path: all-reduce the flat gradient in place.  xGMI path: nothing here, the
+        exchange runs inside adam() (hdg_adam_dp)."""
+        if self._distributed() and not self.xgmi:
             torch.distributed.all_reduce(self.grad, group=self.pg)
 
     def adam(self):
+        if self.xgmi:
+            _lib.check(self.lib.hdg_adam_dp(ctypes.byref(self.shape), ctypes.byref(self._state),
+                                            ctypes.c_void_p(self.grad_local.data_ptr()),
+                                            ctypes.c_void_p(self.grad.data_ptr()),
+                                            ctypes.c_float(self.lr),
+                                            ctypes.c_void_p(self.stats.data_ptr()),
+                                            ctypes.c_void_p(self.status.data_ptr()),
+                                            ctypes.byref(self.xgmi.dp), self._stream()))
+            return
         _lib.check(self.lib.hdg_adam_tf(ctypes.byref(self.shape), ctypes.byref(self._state),
                                         ctypes.c_void_p(self.grad.data_ptr()),
                                         ctypes.c_float(self.lr),
@@ -146,8 +181,20 @@ class Engine:
         """sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer]) equivalent:
         outputs land in self.probs / self.stats (pre-update), params updated in place;
         self.logits only with logits=True (the reference's training run does not fetch them).
-        Single process: hdg_train_step (step kernel + fused reduce/Adam).  Data parallel:
-        hdg_fwd_bwd -> all-reduce of the flat gradient -> hdg_adam_tf."""
+        Single process: hdg_train_step (step kernel + fused reduce/Adam).  Data parallel
+        over xGMI: hdg_train_step_dp (the same two kernels, the exchange inside the second).
+        Over RCCL: hdg_fwd_bwd -> all-reduce of the flat gradient -> hdg_adam_tf."""
+        if self.xgmi:
+            self._check(dbatch)
+            b = dbatch.struct()
+            out = self._outputs(outputs, logits)
+            _lib.check(self.lib.hdg_train_step_dp(ctypes.byref(self.shape), ctypes.byref(b),
+                                                  ctypes.byref(self._state),
+                                                  ctypes.c_float(self.lr), ctypes.byref(out),
+                                                  ctypes.c_void_p(self.grad.data_ptr()),
+                                                  ctypes.c_void_p(self.workspace.data_ptr()),
+                                                  ctypes.byref(self.xgmi.dp), self._stream()))
+            return
         if self._distributed():
             self.fwd_bwd(dbatch, outputs, logits)
             self.allreduce()

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 4
+#define HDG_ABI_VERSION 5
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -168,6 +168,58 @@ int hdg_train_step(const hdg_shape* shape, const hdg_batch* batch, hdg_state* st
 
 int hdg_forward(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                 hdg_outputs* out, float* ce_sum, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Data parallelism over xGMI (one all-reduce of the flat gradient per step).
+ *
+ * Instead of an RCCL call between hdg_fwd_bwd and hdg_adam_tf, the step's reduction
+ * kernel exchanges the gradient itself: every rank owns a MAILBOX (uncached device
+ * memory, hdg_dp_mailbox_alloc) that every other rank of the node maps through HIP IPC
+ * (hdg_dp_mailbox_open on the 64-byte handle, exchanged by the caller, e.g. with
+ * torch.distributed.all_gather).  Each block of the tail kernel writes its gradient
+ * slots as tagged words straight into every peer's mailbox over xGMI (one hop), polls
+ * its own mailbox for the peers' words, sums the world's values in rank order (the same
+ * bits on every rank: replicas stay bitwise equal) and applies TF Adam -- one kernel, no
+ * collective launch.  A peer that does not arrive within wait_ticks fails the launch
+ * loudly: HDG_STATUS_DP_TIMEOUT, NaN loss, no update.  All ranks must issue the same
+ * sequence of hdg_*_dp calls (per-block launch counters in the mailbox tag the words).
+ * The mailbox calls are the one place the library allocates device memory (IPC needs an
+ * allocation of its own); everything else stays caller-owned.
+ * --------------------------------------------------------------------------------- */
+#define HDG_DP_MAX_WORLD 16
+#define HDG_DP_HANDLE_BYTES 64
+#define HDG_DP_MAX_LEN 3152          /* longest vector hdg_dp_allreduce accepts          */
+#define HDG_STATUS_DP_TIMEOUT 2u     /* a peer's gradient words never arrived            */
+
+typedef struct hdg_dp {
+    int32_t  rank;        /* this process's rank, 0 <= rank < world                      */
+    int32_t  world;       /* ranks on this node, 1 <= world <= HDG_DP_MAX_WORLD          */
+    uint64_t wait_ticks;  /* 100 MHz ticks a block waits for a peer (0: 10 s)            */
+    void*    mailbox[HDG_DP_MAX_WORLD];  /* rank r's mailbox as mapped in this process   */
+} hdg_dp;
+
+size_t hdg_dp_mailbox_bytes(void);
+/* allocate + zero this rank's mailbox on the current device; handle: 64 bytes out */
+int hdg_dp_mailbox_alloc(void** mailbox, void* handle);
+/* map a peer's mailbox (its handle) into this process; close / free undo the calls */
+int hdg_dp_mailbox_open(const void* handle, void** mailbox);
+int hdg_dp_mailbox_close(void* mailbox);
+int hdg_dp_mailbox_free(void* mailbox);
+
+/* One data-parallel training step: hdg_fwd_bwd -> xGMI all-reduce -> TF Adam with the
+ * exchange inside the reduction kernel.  grad receives the world-summed gradient +
+ * trailer (as hdg_fwd_bwd + all_reduce would leave it); out->stats the world's loss.   */
+int hdg_train_step_dp(const hdg_shape* shape, const hdg_batch* batch, hdg_state* state,
+                      float lr, hdg_outputs* out, float* grad, void* workspace,
+                      const hdg_dp* dp, void* stream);
+/* xGMI all-reduce of a local gradient (hdg_fwd_bwd's buffer) fused with TF Adam:
+ * grad_out = sum over ranks of grad_local (must not overlap), then hdg_adam_tf's update. */
+int hdg_adam_dp(const hdg_shape* shape, hdg_state* state, const float* grad_local,
+                float* grad_out, float lr, float* stats, uint32_t* status, const hdg_dp* dp,
+                void* stream);
+/* out[i] = sum over ranks (rank order) of in[i], n <= HDG_DP_MAX_LEN, in / out disjoint. */
+int hdg_dp_allreduce(const hdg_dp* dp, const float* in, float* out, int32_t n,
+                     uint32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -148,3 +148,23 @@ def test_header_trailer_constants_match_binding():
     assert (val["HDG_TR_CE"], val["HDG_TR_COUNT"], val["HDG_TR_FAULT"]) == (
         _lib.TR_CE, _lib.TR_COUNT, _lib.TR_FAULT)
     assert val["HDG_STATUS_XCH_TIMEOUT"] == _lib.STATUS_XCH_TIMEOUT
+    assert val["HDG_STATUS_DP_TIMEOUT"] == _lib.STATUS_DP_TIMEOUT
+    assert (val["HDG_DP_MAX_WORLD"], val["HDG_DP_HANDLE_BYTES"], val["HDG_DP_MAX_LEN"]) == (
+        _lib.DP_MAX_WORLD, _lib.DP_HANDLE_BYTES, _lib.DP_MAX_LEN)
+
+
+def test_dp_struct_and_mailbox_size():
+    """hdg_dp's ctypes mirror has the C layout (int32 rank, world; u64 wait; 16 pointers)
+    and the mailbox holds two parities x 16 senders x DP_MAX_LEN tagged words."""
+    import ctypes
+    from hdgnn import _lib
+    assert ctypes.sizeof(_lib.Dp) == 4 + 4 + 8 + 8 * _lib.DP_MAX_WORLD
+    assert _lib.Dp.mailbox.offset == 16
+    lib = _lib.load()
+    assert lib.hdg_dp_mailbox_bytes() >= 2 * _lib.DP_MAX_WORLD * _lib.DP_MAX_LEN * 8
+    assert _lib.DP_MAX_LEN >= lib.hdg_grad_len(4) and _lib.DP_MAX_LEN % 16 == 0
+    # argument errors are reported without touching a device
+    dp = _lib.Dp()
+    dp.world, dp.rank = 2, 2
+    rc = lib.hdg_dp_allreduce(ctypes.byref(dp), None, None, 4, None, None)
+    assert rc == 1000 and b"out of range" in lib.hdg_last_error()
