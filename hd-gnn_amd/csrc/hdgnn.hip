@@ -397,6 +397,201 @@ __device__ __forceinline__ void pair_tile(
 }
 
 // ------------------------------------------------------------------------------
+// pair_tile32: the same passes (same arguments, buffers and results as pair_tile) on
+// 8 x 32 thread tiles, for the wide hunk grids (NC16 = 128, 160: Nc in (80, 160]).
+// Thread (ti, tj) = (t>>5, t&31) owns rows i = ti + 8s and columns j = tj + 32c, so a
+// thread holds SMAX16/2 column accumulators per unit instead of SMAX16: the 16-wide
+// tiles' 40-50 accumulators spilled to scratch inside the sweeps (448 B per lane at
+// SMAX16 = 10).  A wave is two tile rows: row sums close with a 16-lane DPP reduction
+// plus one permlane16 swap (the two DPP rows of a half-wave), column partials with one
+// permlane32 swap per pair of values, then the 4 waves through LDS as in pair_tile.
+// ------------------------------------------------------------------------------
+template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false>
+__device__ __forceinline__ void pair_tile32(
+    const int N, const int t, const float* A, const float* Bv, const int k0,
+    const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
+    const float* __restrict__ wr, const float* __restrict__ wc,
+    const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
+    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0) {
+  typedef float p2 __attribute__((ext_vector_type(2)));
+  static_assert(SMAX16 % 2 == 0, "32-wide tiles cover an even count of 16-column tiles");
+  constexpr int NP16 = 16 * SMAX16;
+  constexpr int SMAX = SMAX16 / 2;
+  constexpr int KP = KK / 2, KT = KK & 1;
+  const int tj = t & 31, ti = t >> 5, lane = t & 63, wv = t >> 6;
+  const int kpb = k0 + (k0 & 1);
+  const int ktl = (k0 & 1) ? k0 : k0 + KK - 1;
+  auto kof = [&](const int k) { return k < 2 * KP ? kpb + k : ktl; };
+  const int nown = (N - radd + rmul - 1) / rmul;
+  const int S = (nown + 7) >> 3;
+  const p2 z2 = {0.f, 0.f};
+
+  p2 cacc2[SMAX][KP > 0 ? KP : 1];
+  float cacct[SMAX];
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c) {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) cacc2[c][p] = z2;
+    cacct[c] = 0.f;
+  }
+  p2 yacc2[KP > 0 ? KP : 1], dk2[KP > 0 ? KP : 1];
+  float yacct = 0.f, dkt = KT ? dl[ktl] : 0.f;
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
+    yacc2[p] = z2;
+    dk2[p] = *reinterpret_cast<const p2*>(dl + kpb + 2 * p);
+  }
+
+  for (int s = 0; s < S; ++s) {
+    const int r = ti + 8 * s;
+    const int i = rmul * r + radd;
+    const bool iv = r < nown;
+    p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
+    const int ib = iv ? i : radd;       // past the sweep: the first swept row (own, finite)
+    const float* Ai = A + ib * LD;
+    const float addm = iv ? 0.f : -INFINITY, mulm = iv ? 1.f : 0.f;
+    const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      a2[p] = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p) + addm2;
+      if constexpr (MODE == 1)
+        rw2[p] = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p) * mulm2;
+      else
+        rw2[p] = z2;
+      racc2[p] = z2;
+    }
+    const float at = KT ? Ai[ktl] + addm : 0.f;
+    const float rwt = (MODE == 1 && KT) ? wr[ib * LD + ktl] * mulm : 0.f;
+    float racct = 0.f;
+    uint32_t wrow[SMAX];
+    const uint32_t bmask = iv ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int q = 0; q < SMAX; ++q)      // clamped load, masked value
+      wrow[q] = bits[ib * W + (q < W ? q : 0)] & (q < W ? bmask : 0u);
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) {
+      const int j = tj + 32 * c;
+      const float af = (float)((wrow[c] >> tj) & 1u);
+      const p2 af2 = {af, af};
+      float g = 0.f;
+      if constexpr (MODE == 2 && GFULL) {
+        g = gam[(iv ? i : radd) * gld + j];
+      } else if constexpr (MODE == 2) {
+        const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;
+        const float gl = gam[ic * gld + jc];
+        g = (iv && j < N && j != i) ? gl : 0.f;
+      }
+      const float* Bj = Bv + j * LD;
+#pragma unroll
+      for (int p = 0; p < KP; ++p) {
+        const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
+        const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
+        p2 e;
+        if constexpr (MODE == 0) {
+          e = __builtin_elementwise_max(z, z2);
+        } else {
+          p2 w;
+          if constexpr (MODE == 1) {
+            w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
+          } else {
+            w = (p2){g, g};
+          }
+          e = step2(z) * w;
+          yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
+        }
+        racc2[p] += e;
+        cacc2[c][p] += e;
+      }
+      if constexpr (KT) {
+        const float z = at + fmaf(af, dkt, Bj[ktl]);
+        float e;
+        if constexpr (MODE == 0) {
+          e = reluf(z);
+        } else {
+          const float w = (MODE == 1) ? (rwt + wc[j * LD + ktl]) : g;
+          e = (z > 0.f) ? w : 0.f;
+          yacct = fmaf(af, e, yacct);
+        }
+        racct += e;
+        cacct[c] += e;
+      }
+    }
+    float rs[KK];
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      rs[2 * p] = racc2[p].x;
+      rs[2 * p + 1] = racc2[p].y;
+    }
+    if constexpr (KT) rs[KK - 1] = racct;
+    row16_sums(rs);
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {    // + the other DPP row of the half-wave
+      float x = rs[k], y = rs[k];
+      swap16(x, y);
+      rs[k] = x + y;
+    }
+    if (tj == 0 && iv) {
+#pragma unroll
+      for (int k = 0; k < KK; ++k) Rout[i * LD + kof(k)] = rs[k];
+    }
+  }
+  float cf[SMAX * KK], yacc[KK];
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c) {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      cf[c * KK + 2 * p] = cacc2[c][p].x;
+      cf[c * KK + 2 * p + 1] = cacc2[c][p].y;
+    }
+    if constexpr (KT) cf[c * KK + KK - 1] = cacct[c];
+  }
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
+    yacc[2 * p] = yacc2[p].x;
+    yacc[2 * p + 1] = yacc2[p].y;
+  }
+  if constexpr (KT) yacc[KK - 1] = yacct;
+  float* credy = cred + 4 * NP16 * KK;
+  {   // the wave's two tile rows: value n in lanes 0-31, value n + HV in lanes 32-63
+    constexpr int NV = SMAX * KK, HV = (NV + 1) / 2;
+    float* cw = cred + wv * NP16 * KK;
+#pragma unroll
+    for (int q = 0; q < HV; ++q) {
+      float x = cf[q], y = (q + HV < NV) ? cf[q + HV] : 0.f;
+      swap32(x, y);
+      const float v = x + y;
+      const int n = lane < 32 ? q : q + HV;
+      if (n < NV) {
+        const int c = n / KK, k = n - c * KK;
+        cw[(tj + 32 * c) * KK + k] = v;
+      }
+    }
+  }
+  if constexpr (MODE != 0) {
+    wave_sums(yacc, lane, [&](int k, float x) { credy[wv * KK + k] = x; });
+  }
+  __syncthreads();
+  for (int e = t; e < NP16 * KK; e += 256) {
+    const int j = e / KK, k = e - j * KK;
+    const float v = cred[e] + cred[e + NP16 * KK] + cred[e + 2 * NP16 * KK] + cred[e + 3 * NP16 * KK];
+    if (j < N) Cout[j * LD + kof(k)] = v;
+  }
+  if constexpr (MODE != 0) {
+    if (t < KK) ysum[kof(t)] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
+  }
+  __syncthreads();
+}
+
+// the hunk pair passes: 16 x 16 thread tiles up to NC16 = 80 (glide), 8 x 32 beyond
+template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false, class... Args>
+__device__ __forceinline__ void pair_pass(Args... args) {
+  if constexpr (SMAX16 > 5)
+    pair_tile32<KK, SMAX16, MODE, LD, GFULL>(args...);
+  else
+    pair_tile<KK, SMAX16, MODE, LD, 0, GFULL>(args...);
+}
+
+// ------------------------------------------------------------------------------
 // scans / searches
 // ------------------------------------------------------------------------------
 template <class T>
@@ -1635,7 +1830,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M5: hunk pair sums G_p = sum_q g1_pq, H_q = sum_p g1_pq (model_2.py:260-275) ---
   float* G = Bf[2];
   float* Hh = Bf[3];
-  pair_tile<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
+  pair_pass<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
                                   nullptr, 0, G, Hh, nullptr, credg, rmul, radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     if (SPLIT && ((e / HS) & 1) != h) continue;       // the diagonal of the own rows
@@ -1830,7 +2025,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
-  pair_tile<KK_MID, SMAXC, 2, HS, 0, GAML>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
+  pair_pass<KK_MID, SMAXC, 2, HS, GAML>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
                                            nullptr, gam, GLD, Dsig, Dtau, ysumv, credg, rmul,
                                            radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
@@ -1957,7 +2152,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M10: hunk pair backward: dgamma = [g1 > 0](dG_p + dH_q) -----------------------
   float* Dal = Bf[4];   // Dsig/Dtau dead after dG/dH
   float* Dbe = Bf[5];
-  pair_tile<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
+  pair_pass<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
                                   Dal, Dbe, ysumv, credg, rmul, radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
     if (SPLIT && ((e / HS) & 1) != h) {             // partner's rows: no D_alpha here

@@ -11,7 +11,10 @@ from hdgnn import _lib, layout  # noqa: E402
 from hdgnn.engine import Engine  # noqa: E402
 from hdgnn.synth import synth_commits  # noqa: E402
 
-B, ne, nc = 100, 200, 74
+# python tools/mid_phases.py [ne nc [B]]  (default glide 200 74 100)
+ne = int(sys.argv[1]) if len(sys.argv) > 2 else 200
+nc = int(sys.argv[2]) if len(sys.argv) > 2 else 74
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 100
 cb = synth_commits(B, ne, nc, 1)
 db = cb.to_device()
 eng = Engine(ne, nc, B)
