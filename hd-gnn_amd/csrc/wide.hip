@@ -468,6 +468,33 @@ __device__ __forceinline__ void for_bits(const uint32_t* row, int WE, int i, F f
   }
 }
 
+// a = 1 correction of one neighbour as ONE clamped fma per hidden unit (the fused path's
+// entity_fwd form): z0 = A x_j + B is affine in x_j, and
+//   relu(z0 + d) - relu(z0) = d clamp((s z0 + t) / d, 0, 1),  (s, t) = (1, d) for d >= 0,
+//   (-1, 0) for d < 0,
+// so the correction sum is d * sum_j clamp(x_j ca + cb, 0, 1) with ca = s A / d,
+// cb = (s B + t) / d; |d| < 2^-100 counts as d = 0 (below the sum's rounding)
+struct ClampCoef {
+  float ca, cb;
+};
+__device__ __forceinline__ ClampCoef clamp_coef(const float A, const float B, const float d) {
+  const float sg = d >= 0.f ? 1.f : -1.f, tg = d >= 0.f ? d : 0.f;
+  const float rd = fabsf(d) >= 0x1p-100f ? 1.f / d : 0.f;
+  return {sg * A * rd, fmaf(sg, B, tg) * rd};
+}
+__device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) {
+  f2 xx;
+  xx.x = x;
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(r) : "v"(xx), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float clamp_fma1(const float x, const float a, const float b) {
+  float r;
+  asm("v_fma_f32 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(x), "v"(a), "v"(b));
+  return r;
+}
+
 // MODE 0 (E1, model_2.py:161-188): P_i = sum_{j!=i} relu(z_ij) + relu(z_ji)
 // MODE 1 (EE, model_4.py:206-243): R1_i = sum_{j!=i} relu(z'_ij), C1_i = sum relu(z'_ji)
 template <int MODE>
@@ -531,23 +558,53 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
     s1[kk] = 0.f;
     s2[kk] = 0.f;
   }
-  // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i))
-  for_bits(rowb, WE, i, [&](int j) {
-    const float xj = xb[j];
+  // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i)), one clamped
+  // packed fma per two hidden units and neighbour (clamp_coef); KPW = 5: two packed
+  // pairs + one scalar unit
+  static_assert(KPW == 5, "packed correction layout");
+  {
+    f2 ra[2], rb2[2], ca[2], cb[2];
+    float rat, rbt, cat, cbt;
+    ClampCoef q[KPW], qc[KPW];
 #pragma unroll
     for (int kk = 0; kk < KPW; ++kk) {
-      const float z0 = MODE == 0 ? u[kk] + xj * wb[kk] : fmaf(xj, wa[kk], u[kk]);
-      s1[kk] += relu(z0 + dd[kk]) - relu(z0);
+      // row form z0 = u + x_j w1 (MODE 0) / x_j w + u (MODE 1); column form
+      // z0 = x_j w0 + c0 + v (MODE 0) / x_j w + u (MODE 1)
+      q[kk] = clamp_coef(MODE == 0 ? wb[kk] : wa[kk], u[kk], dd[kk]);
+      qc[kk] = clamp_coef(wa[kk], MODE == 0 ? c0[kk] + v[kk] : u[kk], dd[kk]);
     }
-  });
-  for_bits(colb, WE, i, [&](int j) {
-    const float xj = xb[j];
 #pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const float z0 = MODE == 0 ? fmaf(xj, wa[kk], c0[kk]) + v[kk] : fmaf(xj, wa[kk], u[kk]);
-      s2[kk] += relu(z0 + dd[kk]) - relu(z0);
+    for (int h = 0; h < 2; ++h) {
+      ra[h] = (f2){q[2 * h].ca, q[2 * h + 1].ca};
+      rb2[h] = (f2){q[2 * h].cb, q[2 * h + 1].cb};
+      ca[h] = (f2){qc[2 * h].ca, qc[2 * h + 1].ca};
+      cb[h] = (f2){qc[2 * h].cb, qc[2 * h + 1].cb};
     }
-  });
+    rat = q[4].ca; rbt = q[4].cb; cat = qc[4].ca; cbt = qc[4].cb;
+    f2 sr[2] = {(f2){0.f, 0.f}, (f2){0.f, 0.f}}, sc[2] = {sr[0], sr[1]};
+    float srt = 0.f, sct = 0.f;
+    for_bits(rowb, WE, i, [&](int j) {
+      const float xj = xb[j];
+      sr[0] += clamp_fma2(xj, ra[0], rb2[0]);
+      sr[1] += clamp_fma2(xj, ra[1], rb2[1]);
+      srt += clamp_fma1(xj, rat, rbt);
+    });
+    for_bits(colb, WE, i, [&](int j) {
+      const float xj = xb[j];
+      sc[0] += clamp_fma2(xj, ca[0], cb[0]);
+      sc[1] += clamp_fma2(xj, ca[1], cb[1]);
+      sct += clamp_fma1(xj, cat, cbt);
+    });
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      s1[2 * h] = sr[h].x * dd[2 * h];
+      s1[2 * h + 1] = sr[h].y * dd[2 * h + 1];
+      s2[2 * h] = sc[h].x * dd[2 * h];
+      s2[2 * h + 1] = sc[h].y * dd[2 * h + 1];
+    }
+    s1[4] = srt * dd[4];
+    s2[4] = sct * dd[4];
+  }
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     const size_t gi = ((size_t)b * Ne + i) * H + g * KPW + kk;
