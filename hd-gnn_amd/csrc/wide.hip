@@ -329,6 +329,12 @@ constexpr int H2 = H / 2;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
+// [z > 0] on both halves in one op: clamp(z * 2^126, 0, 1) (exact for normal z; -0, NaN -> 0)
+__device__ __forceinline__ f2 step2(f2 z) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(z), "v"((f2){0x1p126f, 0x1p126f}));
+  return r;
+}
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 ld2(const float* p) { return (f2){p[0], p[1]}; }
 
@@ -401,6 +407,7 @@ struct SortTabs {
   const int* cum;
   const double* pxd;
   int nd;
+  const float* xs;    // the commit's x staged in LDS (stage_tabs with xg)
 };
 
 __device__ __forceinline__ SortTabs sort_tabs(const uint32_t* prep, const GenPrep& GP, int b) {
@@ -410,34 +417,39 @@ __device__ __forceinline__ SortTabs sort_tabs(const uint32_t* prep, const GenPre
   T.cum = reinterpret_cast<const int*>(pp + GP.cum);
   T.pxd = reinterpret_cast<const double*>(pp + GP.pxd);
   T.nd = (int)pp[GP.meta];
+  T.xs = nullptr;
   return T;
 }
 
 // the commit's sorted tables copied into LDS (dynamic, sort_lds_bytes); all threads
 __device__ __forceinline__ SortTabs stage_tabs(const uint32_t* prep, const GenPrep& GP, int b,
-                                               int Ne, void* lds) {
+                                               int Ne, void* lds, const float* xg = nullptr) {
   const SortTabs G = sort_tabs(prep, GP, b);
   const int NE4 = (Ne + 3) & ~3;
   double* pxd = reinterpret_cast<double*>(lds);
   int* cum = reinterpret_cast<int*>(pxd + NE4 + 4);
   float* xu = reinterpret_cast<float*>(cum + NE4 + 4);
+  float* xs = xu + NE4;
   for (int e = threadIdx.x; e <= G.nd; e += blockDim.x) {
     pxd[e] = G.pxd[e];
     cum[e] = G.cum[e];
     if (e < G.nd) xu[e] = G.xu[e];
   }
+  if (xg)   // the neighbour walks read x_j from LDS, not one dependent HBM load each
+    for (int e = threadIdx.x; e < Ne; e += blockDim.x) xs[e] = xg[e];
   __syncthreads();
   SortTabs T;
   T.xu = xu;
   T.cum = cum;
   T.pxd = pxd;
   T.nd = G.nd;
+  T.xs = xg ? xs : nullptr;
   return T;
 }
 
 __host__ __device__ inline size_t sort_lds_bytes(int Ne) {
   const size_t NE4 = (Ne + 3) & ~3;
-  return (NE4 + 4) * 8 + (NE4 + 4) * 4 + NE4 * 4;
+  return (NE4 + 4) * 8 + (NE4 + 4) * 4 + 2 * NE4 * 4;   // pxd, cum, xu, x
 }
 
 __device__ __forceinline__ int top_pow2(int n) { return 1 << (31 - __builtin_clz((unsigned)n)); }
@@ -511,10 +523,10 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
   const int i = t0 + lane;
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
-  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds);
+  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
   if (i >= Ne) return;   // no barriers below
   const int WE = (Ne + 31) >> 5;
-  const float* xb = x + (size_t)b * Ne;
+  const float* xb = T.xs;
   const float xi = xb[i];
   const uint32_t* rowb = abits + ((size_t)b * Ne + i) * WE;
   const uint32_t* colb = aT + ((size_t)b * Ne + i) * WE;
@@ -1608,8 +1620,8 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
   const int ic = live ? i : Ne - 1;
   const int WE = (Ne + 31) >> 5;
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
-  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds);
-  const float* xb = x + (size_t)b * Ne;
+  const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
+  const float* xb = T.xs;
   const float xi = xb[ic];
   const float* rbb = rb + (size_t)b * Ne * H;
   float S0[KPW], S1[KPW], S2[KPW], S3[KPW], u[KPW], wb[KPW], dd[KPW], ri[KPW];
@@ -1656,22 +1668,51 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
   float cs[KPW];                                  // sum of the corrections' dm
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) cs[kk] = 0.f;
-  if (live) {
+  if (live) {   // units (0,1), (2,3) as packed pairs, unit 4 scalar; [z > 0] g as step2(z) g
+    static_assert(KPW == 5, "packed correction layout");
+    f2 u2[2], wb2[2], dd2[2], ri2[2], cs2[2], s12[2], s32[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u2[h] = (f2){u[2 * h], u[2 * h + 1]};
+      wb2[h] = (f2){wb[2 * h], wb[2 * h + 1]};
+      dd2[h] = (f2){dd[2 * h], dd[2 * h + 1]};
+      ri2[h] = (f2){ri[2 * h], ri[2 * h + 1]};
+      cs2[h] = (f2){0.f, 0.f};
+      s12[h] = (f2){S1[2 * h], S1[2 * h + 1]};
+      s32[h] = (f2){0.f, 0.f};
+    }
+    float cst = 0.f, s1t = S1[4], s3t = 0.f;
     for_bits(abits + ((size_t)b * Ne + i) * WE, WE, i, [&](int j) {
       const float xj = xb[j];
       const float* qj = rbb + (size_t)j * H + g * KPW;
+      const f2 xx = {xj, xj};
 #pragma unroll
-      for (int kk = 0; kk < KPW; ++kk) {
-        const float z0 = MODE == 0 ? u[kk] + xj * wb[kk] : fmaf(xj, wb[kk], u[kk]);
-        const float z1 = z0 + dd[kk];
-        const float gg = ri[kk] + qj[kk];
-        const float m1 = z1 > 0.f ? gg : 0.f, m0 = z0 > 0.f ? gg : 0.f;
-        const float dm = m1 - m0;
-        cs[kk] += dm;
-        S1[kk] = fmaf(xj, dm, S1[kk]);
-        S3[kk] += m1;
+      for (int h = 0; h < 2; ++h) {
+        const f2 z0 = MODE == 0 ? u2[h] + xx * wb2[h] : fma2(xx, wb2[h], u2[h]);
+        const f2 z1 = z0 + dd2[h];
+        const f2 gg = ri2[h] + (f2){qj[2 * h], qj[2 * h + 1]};   // finite
+        const f2 m1 = step2(z1) * gg, m0 = step2(z0) * gg;
+        const f2 dm = m1 - m0;
+        cs2[h] += dm;
+        s12[h] = fma2(xx, dm, s12[h]);
+        s32[h] += m1;
       }
+      const float z0 = MODE == 0 ? u[4] + xj * wb[4] : fmaf(xj, wb[4], u[4]);
+      const float z1 = z0 + dd[4];
+      const float gg = ri[4] + qj[4];
+      const float m1 = z1 > 0.f ? gg : 0.f, m0 = z0 > 0.f ? gg : 0.f;
+      const float dm = m1 - m0;
+      cst += dm;
+      s1t = fmaf(xj, dm, s1t);
+      s3t += m1;
     });
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      cs[2 * h] = cs2[h].x; cs[2 * h + 1] = cs2[h].y;
+      S1[2 * h] = s12[h].x; S1[2 * h + 1] = s12[h].y;
+      S3[2 * h] = s32[h].x; S3[2 * h + 1] = s32[h].y;
+    }
+    cs[4] = cst; S1[4] = s1t; S3[4] = s3t;
   }
   float v[4 * KPW];
 #pragma unroll
