@@ -15,6 +15,7 @@ allocated, every peer handle opened, and a self-test all-reduce through the mail
 returns the exact sums.  Otherwise it returns None (auto mode: the caller all-reduces
 through torch.distributed / RCCL) or raises (mode "xgmi").
 """
+import contextlib
 import ctypes
 import socket
 import sys
@@ -58,7 +59,8 @@ class XgmiGroup:
         dist.all_gather_object(hosts, socket.gethostname(), group=pg)
         if not agree(world <= _lib.DP_MAX_WORLD and len(set(hosts)) == 1):
             return give_up("ranks span several hosts or world > %d" % _lib.DP_MAX_WORLD)
-        with torch.cuda.device(device):
+        dctx = torch.cuda.device(device) if device.type == "cuda" else contextlib.nullcontext()
+        with dctx:
             own = ctypes.c_void_p()
             h = (ctypes.c_ubyte * _lib.DP_HANDLE_BYTES)()
             ok = lib.hdg_dp_mailbox_alloc(ctypes.byref(own), h) == 0
