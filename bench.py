@@ -186,8 +186,12 @@ def main():
 
     # per-kernel durations (HIP events on the launch stream), separate instrumented pass
     ev = _lib.HipEvents(3)
-    fused = eng.path == _lib.PATH_FUSED
-    names = ["k_commit_step", "k_grad_reduce"] if fused else ["general_fwd_bwd", "none"]
+    # model_2 on the fused path: the step kernel and the reduction timed apart; model_4 on
+    # the fused path (entity-edge stage on general-path kernels around the step kernel) and
+    # the general path: the whole fwd+bwd
+    fused = eng.path == _lib.PATH_FUSED and v == 2
+    names = (["k_commit_step", "k_grad_reduce"] if fused else
+             ["hybrid_fwd_bwd" if eng.path == _lib.PATH_FUSED else "general_fwd_bwd", "none"])
     acc = dict.fromkeys(names, 0.0)
     nev = max(10, min(args.steps, 50))
     import ctypes
@@ -280,7 +284,9 @@ def main():
             "config": {"workload": "model_%d (%s) train step: fwd+bwd+TF-Adam, %s" % (
                            v, {1: "HD-GNN/ES", 2: "HD-GNN/S", 3: "HD-GNN/E", 4: "HD-GNN"}[v],
                            "glide step=2" if (ne, nc) == (200, 74) else "Ne=%d Nc=%d" % (ne, nc)),
-                       "engine_path": "fused" if fused else "general",
+                       "engine_path": {_lib.PATH_FUSED: "fused", _lib.PATH_GENERAL: "general"}[
+                           eng.path] + (" (entity-edge stage on general kernels)"
+                                        if eng.path == _lib.PATH_FUSED and v == 4 else ""),
                        "launch": "eager" if args.no_graph else
                                  "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,

@@ -69,24 +69,45 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // row16_sum of N values as fused v_add_f32_dpp (one VALU op per value and step; the
-// compiler otherwise splits some into v_mov_dpp + v_add).  Steps run over all N values
-// in turn, so each DPP read is >= N-1 >= 2 instructions after the write it depends on;
-// one s_nop covers the producers before the first step.
-#define HDG_DPP_ADD(v, ctl) asm volatile("v_add_f32_dpp %0, %0, %0 " ctl : "+v"(v))
+// compiler otherwise splits some into v_mov_dpp + v_add).  A DPP read needs 2 wait states
+// after the VALU write of its operand, and the compiler's hazard recognizer does not look
+// inside inline asm: it may schedule a producer (or a register copy) right before any asm
+// statement.  So each group of 3-4 values is reduced by ONE asm block that opens with the
+// s_nop covering its producers; inside, the steps run over the group's values in turn
+// (each DPP read >= 2 instructions after the write it depends on).
+#define HDG_DPP_STEP(ctl, n) "v_add_f32_dpp %" #n ", %" #n ", %" #n " " ctl \
+  " row_mask:0xf bank_mask:0xf\n\t"
+#define HDG_DPP_STEP3(ctl) HDG_DPP_STEP(ctl, 0) HDG_DPP_STEP(ctl, 1) HDG_DPP_STEP(ctl, 2)
+#define HDG_DPP_STEP4(ctl) HDG_DPP_STEP3(ctl) HDG_DPP_STEP(ctl, 3)
+#define HDG_DPP_STEP5(ctl) HDG_DPP_STEP4(ctl) HDG_DPP_STEP(ctl, 4)
+#define HDG_DPP_BLOCK(S) "s_nop 1\n\t" S("row_mirror") S("row_half_mirror") \
+  S("quad_perm:[2,3,0,1]") S("quad_perm:[1,0,3,2]")
+__device__ __forceinline__ void row16_sum3(float* v) {
+  asm volatile(HDG_DPP_BLOCK(HDG_DPP_STEP3) : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]));
+}
+__device__ __forceinline__ void row16_sum4(float* v) {
+  asm volatile(HDG_DPP_BLOCK(HDG_DPP_STEP4) : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+__device__ __forceinline__ void row16_sum5(float* v) {
+  asm volatile(HDG_DPP_BLOCK(HDG_DPP_STEP5)
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]));
+}
+#undef HDG_DPP_BLOCK
+#undef HDG_DPP_STEP5
+#undef HDG_DPP_STEP4
+#undef HDG_DPP_STEP3
+#undef HDG_DPP_STEP
+// N = 3 G + R (R < 3): G - 1 groups of 3 and one of 3 + R
 template <int N>
 __device__ __forceinline__ void row16_sums(float (&v)[N]) {
-  static_assert(N >= 3, "row16_sums needs >= 3 independent values (DPP hazard spacing)");
-  asm volatile("s_nop 1" ::);
+  static_assert(N >= 3, "row16_sums needs >= 3 values (groups of 3-5 per asm block)");
+  constexpr int G = N / 3, R = N % 3;
 #pragma unroll
-  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "row_mirror row_mask:0xf bank_mask:0xf");
-#pragma unroll
-  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "row_half_mirror row_mask:0xf bank_mask:0xf");
-#pragma unroll
-  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf");
-#pragma unroll
-  for (int k = 0; k < N; ++k) HDG_DPP_ADD(v[k], "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf");
+  for (int g = 0; g + 1 < G; ++g) row16_sum3(v + 3 * g);
+  if constexpr (R == 0) row16_sum3(v + 3 * (G - 1));
+  else if constexpr (R == 1) row16_sum4(v + 3 * (G - 1));
+  else row16_sum5(v + 3 * (G - 1));
 }
-#undef HDG_DPP_ADD
 
 // Sum over the 4 DPP rows of a wave for every lane column: lane l gets
 // v[l] + v[l^16] + v[l^32] + v[l^48].  v_permlane{32,16}_swap in the VALU (no LDS);
@@ -1423,7 +1444,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     float* __restrict__ logits, int Ne, int Nc, float ce_scale,
     unsigned long long* __restrict__ stamps, float* __restrict__ aux,
     const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch,
-    uint32_t* __restrict__ status, const uint32_t xfault) {
+    uint32_t* __restrict__ status, const uint32_t xfault, const int ee_ins,
+    const float* __restrict__ ncls, float* __restrict__ dnout) {
+  // model_4 on this kernel (hdg hybrid path): ee_ins = the entity-edge parameter block's
+  // length in the flat vector (the model_2-shaped parameters after it are staged at their
+  // model_2 offsets); ncls [B][Nc][2] = the entity-edge aggregate n_c[2:4] replacing the
+  // static class counts (model_4.py:95-97); dnout [B][Nc][4] receives dn for the
+  // entity-edge backward.  model_2: 0, nullptr, nullptr.
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
@@ -1541,7 +1568,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   constexpr int LQ = 2;                            // x-list float4 per thread in the batch
   float wr_[WQ];
 #pragma unroll
-  for (int u = 0; u < WQ; ++u) wr_[u] = t + u * NT_MID < NP ? Wg[t + u * NT_MID] : 0.f;
+  for (int u = 0; u < WQ; ++u) {
+    const int q = t + u * NT_MID;
+    wr_[u] = q < NP ? Wg[q + (q >= H1_W1 ? ee_ins : 0)] : 0.f;
+  }
   float xv = 0.f, xsv = 0.f, xuv = 0.f;
   int pmv = 0, cmv = 0, orv = 0, ocv = 0;
   double pxv = 0.0;
@@ -1755,9 +1785,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         }
       });
     }
+    const float* ncl = ncls ? ncls + (size_t)b * 2 * Nc : ncst;   // model_4: the EE aggregate
     for (int c = t; c < Nc; c += NT_MID) {
-      nb[4 * c + 2] = ncst[2 * c];
-      nb[4 * c + 3] = ncst[2 * c + 1];
+      nb[4 * c + 2] = ncl[2 * c];
+      nb[4 * c + 3] = ncl[2 * c + 1];
     }
     if constexpr (SPLIT) {
       for (int i = t; i < NE4; i += NT_MID) xsc[2 * Nc + i] = (i >= nlo && i < nhi) ? os[i] : 0.f;
@@ -2165,21 +2196,28 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  if (wv < SMAXC) {   // dn_c[m] = Dalpha_c V1[m] + Dbeta_c V1[4+m], m in {0,1}: MFMA row tiles
+  // dn_c[m] = Dalpha_c V1[m] + Dbeta_c V1[4+m]: m in {0,1} (x' parts) for M11, m in {2,3}
+  // (class parts, [NC16][2] in the pair-tile scratch: dead after M10, below M11's dx'
+  // partials) only when model_4's entity-edge backward needs them
+  const int ndm = dnout ? 4 : 2;
+  float* dnc = U + NBUF_H * NC16 * HS;
+  if (wv < SMAXC) {   // MFMA row tiles
     const int row0 = wv * 16, rr = row0 + (lane & 15), m = lane & 15;
-    const bool rv = rr < Nc, mv = m < 2;
+    const bool rv = rr < Nc, mv = m < ndm;
     const f4v c = mfma_tile16_p(rv ? Dal + rr * HS : kzero, rv ? 1 : 0,
                                 mv ? Ws + H1_W1 + m * HS : kzero, mv ? 1 : 0, HS, lane) +
                   mfma_tile16_p(rv ? Dbe + rr * HS : kzero, rv ? 1 : 0,
                                 mv ? Ws + H1_W1 + (4 + m) * HS : kzero, mv ? 1 : 0, HS, lane);
     if (mv) {
+      float* dst = m < 2 ? dnb + m : dnc + (m - 2);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dnb[2 * (row0 + 4 * (lane >> 4) + q) + m] = c[q];   // 0 past Nc
+      for (int q = 0; q < 4; ++q) dst[2 * (row0 + 4 * (lane >> 4) + q)] = c[q];   // 0 past Nc
     }
   }
   __syncthreads();
   if constexpr (SPLIT) {
     pair_send(dnb, 2 * Nc, xout + 2 * XS, xtag(epoch, 3) ^ xsend, t);   // dV1 overlaps
+    if (dnout) pair_send(dnc, 2 * Nc, xout + 2 * XS + Nc, xtag(epoch, 3) ^ xsend, t);
     // waves 4-15 warm this XCD's L2 with the count matrices (M11 reads every column; M3
     // fetched only the own half) while waves 0-3 run dV1
     if (wv >= 4) {
@@ -2212,7 +2250,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if constexpr (SPLIT) {
     if constexpr (STAMPS) MID_STAMP();
     xlate |= pair_recv_add(dnb, 2 * Nc, xin + 2 * XS, xtag(epoch, 3), t);
+    if (dnout) xlate |= pair_recv_add(dnc, 2 * Nc, xin + 2 * XS + Nc, xtag(epoch, 3), t);
   } else {
+    __syncthreads();
+  }
+  if (dnout) {                                 // the whole dn for the entity-edge backward
+    if (h == 0)
+      for (int e = t; e < 4 * Nc; e += NT_MID) {
+        const int c = e >> 2, m = e & 3;
+        dnout[(size_t)b * 4 * Nc + e] = m < 2 ? dnb[2 * c + m] : dnc[2 * c + m - 2];
+      }
     __syncthreads();
   }
   MID_STAMP();
@@ -3033,7 +3080,7 @@ namespace {
 using hdg::fail;
 
 bool fused_fits(const hdg_shape* s) {
-  if (s->variant != 2 || s->ne > 256 || s->nc > 160) return false;
+  if ((s->variant != 2 && s->variant != 4) || s->ne > 256 || s->nc > 160) return false;
   const StepLayout L = step_layout(s->ne, s->nc, smax_c(s->nc));
   return (size_t)L.total * 4 <= 160 * 1024;
 }
@@ -3050,8 +3097,9 @@ int resolve(const hdg_shape* s) {
   const bool fits = fused_fits(s);
   if (s->path == HDG_PATH_FUSED) {
     if (!fits)
-      return fail(HDG_EINVAL, "the fused path runs model_2 with ne <= 256, nc <= 160 "
-                              "(got variant %d, ne=%d, nc=%d)", s->variant, s->ne, s->nc), -1;
+      return fail(HDG_EINVAL, "the fused path runs model_2 / model_4 with ne <= 256, "
+                              "nc <= 160 (got variant %d, ne=%d, nc=%d)", s->variant, s->ne,
+                  s->nc), -1;
     return HDG_PATH_FUSED;
   }
   if (s->path != HDG_PATH_AUTO) return fail(HDG_EINVAL, "unknown path %d", s->path), -1;
@@ -3155,10 +3203,18 @@ StepOut step_out(const hdg_outputs* out) {
   return out ? StepOut{out->probs, out->logits, out->status} : StepOut{nullptr, nullptr, nullptr};
 }
 
+// model_4 hooks of the step kernel (k_commit_step's ee_ins / ncls / dnout); all zero for model_2
+struct Hyb {
+  int ins;
+  const float* ncls;
+  float* dnout;
+};
+
 template <int SMAXC, bool TRAIN, bool STAMPS, bool SPLIT>
 hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                        const Work& w, const StepOut& o, float ce_scale,
-                       unsigned long long* stamps, const float* bpow, hipStream_t st) {
+                       unsigned long long* stamps, const float* bpow, hipStream_t st,
+                       const Hyb& hy) {
   const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
   const size_t lds = (size_t)L.total * 4;
   if (hipError_t e = set_step_attr<SMAXC, TRAIN, STAMPS, SPLIT>(); e != hipSuccess) return e;
@@ -3168,7 +3224,7 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
                      ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, o.probs,
                      o.logits, s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow,
                      s->batch, (unsigned long long*)(ws + w.xch), o.status,
-                     SPLIT ? debug_xfault() : 0u);
+                     SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncls, hy.dnout);
   return hipGetLastError();
 }
 
@@ -3176,12 +3232,12 @@ template <bool TRAIN, bool STAMPS = false>
 hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                          const Work& w, const StepOut& o, float ce_scale,
                          unsigned long long* stamps, hipStream_t st, bool split,
-                         const float* bpow = nullptr) {
+                         const float* bpow = nullptr, const Hyb& hy = Hyb{0, nullptr, nullptr}) {
 #define HDG_STEP(SM)                                                                              \
   return split ? launch_step<SM, TRAIN, STAMPS, true>(s, bt, params, ws, w, o, ce_scale, stamps, \
-                                                      bpow, st)                                   \
+                                                      bpow, st, hy)                               \
                : launch_step<SM, TRAIN, STAMPS, false>(s, bt, params, ws, w, o, ce_scale, stamps,\
-                                                       bpow, st)
+                                                       bpow, st, hy)
   switch (smax_c(s->nc)) {
     case 5: HDG_STEP(5);
     case 8: HDG_STEP(8);
@@ -3193,6 +3249,86 @@ hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* p
 float pair_count(const hdg_shape* s) {
   const int bg = s->batch_global > 0 ? s->batch_global : s->batch;
   return (float)bg * (float)(s->nc * (s->nc - 1));
+}
+
+// ---- model_4 on the fused path ("hybrid"): the entity-edge stage runs on the general
+// path's kernels (hdg::wide_ee_fwd / wide_ee_bwd) around k_commit_step, which runs the
+// model_2-shaped rest of the step (entity pair MLP, E3, cross-graph, hunk stage,
+// classifier, their backward) with model_4's parameters, the entity-edge aggregate as
+// the class part of n_c and dn exported for the entity-edge backward.  model_4 is model_2
+// plus that stage (model_4.py:92-97): the two meet only at n_c[2:4] and dn_c[2:4].
+// prep = [fused prep | general prep]; workspace = [fused | general | ncls [B][Nc][2]].
+bool is_hybrid(const hdg_shape* s, int path) { return path == HDG_PATH_FUSED && s->variant == 4; }
+
+size_t fused_prep_bytes(const hdg_shape* s) {
+  return (size_t)s->batch * prep_layout(s->ne, s->nc).words * 4;
+}
+
+struct HybWork {
+  size_t wide, ncls, total;   // float offsets
+};
+HybWork hyb_layout(const hdg_shape* s) {
+  HybWork h;
+  auto up = [](size_t n) { return (n + 63) & ~(size_t)63; };
+  h.wide = up(work_layout(s).total);
+  h.ncls = h.wide + up(hdg::wide_workspace_bytes(s) / 4);
+  h.total = h.ncls + up((size_t)s->batch * s->nc * 2);
+  return h;
+}
+
+hdg_batch wide_half(const hdg_batch* bt, const hdg_shape* s) {
+  hdg_batch bw = *bt;
+  bw.prep = (char*)bt->prep + fused_prep_bytes(s);
+  return bw;
+}
+
+// train: grad = the full model_4 gradient + trailer (the fused rows' model_2-layout slots
+// mapped past the entity-edge block, the EE block from the general path's rows);
+// !train: forward only, CE sum -> *ce_sum.  events[0..2] as hdg_fwd_bwd_events.
+int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
+               hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st,
+               void* const* events) {
+  const HybWork hw = hyb_layout(s);
+  float* ws = (float*)workspace;
+  float* wws = ws + hw.wide;
+  float* ncls = ws + hw.ncls;
+  const hdg_batch bw = wide_half(bt, s);
+  const int ins = hdg::param_offsets(4).H1_W1 - m2::H1_W1;   // the entity-edge block (1002)
+  auto mark = [&](int k) -> hipError_t {
+    return events ? hipEventRecord((hipEvent_t)events[k], st) : hipSuccess;
+  };
+  HIP_TRY(mark(0));
+  if (int rc = hdg::wide_ee_fwd(s, &bw, params, wws, ncls, st)) return rc;
+  const Work w = work_layout(s);
+  const bool split = use_split(s);
+  const float pairs = pair_count(s);
+  const Hyb hy{ins, ncls, train ? hdg::wide_dn(s, wws) : nullptr};
+  if (!train) {
+    HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, step_out(out), 0.f, nullptr, st, split,
+                                 nullptr, hy));
+    if (ce_sum) {
+      hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part,
+                         part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(mark(1));
+    HIP_TRY(mark(2));
+    return 0;
+  }
+  HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, step_out(out), 10.f / pairs, nullptr, st,
+                              split, nullptr, hy));
+  const int R = part_rows(s, split);
+  // the fused rows: [0, H1_W1) in place, [H1_W1, GRAD_LEN) past the entity-edge block
+  hipLaunchKernelGGL(k_grad_reduce, dim3((m2::H1_W1 + RED_P - 1) / RED_P), dim3(1024), 0, st,
+                     ws + w.part, R, 0, m2::H1_W1, grad);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN - m2::H1_W1 + RED_P - 1) / RED_P), dim3(1024),
+                     0, st, ws + w.part, R, m2::H1_W1, GRAD_LEN, grad + m2::H1_W1 + ins);
+  HIP_TRY(hipGetLastError());
+  if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st)) return rc;
+  HIP_TRY(mark(1));
+  HIP_TRY(mark(2));
+  return 0;
 }
 
 }  // namespace
@@ -3212,6 +3348,7 @@ size_t hdg_workspace_bytes(const hdg_shape* shape) {
   const int path = resolve(shape);
   if (path < 0) return 0;
   if (path == HDG_PATH_GENERAL) return hdg::wide_workspace_bytes(shape);
+  if (is_hybrid(shape, path)) return hyb_layout(shape).total * sizeof(float);
   return work_layout(shape).total * sizeof(float);
 }
 
@@ -3219,7 +3356,8 @@ size_t hdg_prep_bytes(const hdg_shape* shape) {
   const int path = resolve(shape);
   if (path < 0) return 0;
   if (path == HDG_PATH_GENERAL) return hdg::wide_prep_bytes(shape);
-  return (size_t)shape->batch * prep_layout(shape->ne, shape->nc).words * 4;
+  if (is_hybrid(shape, path)) return fused_prep_bytes(shape) + hdg::wide_prep_bytes(shape);
+  return fused_prep_bytes(shape);
 }
 
 int hdg_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
@@ -3248,6 +3386,10 @@ int hdg_prepare(const hdg_shape* s, const hdg_batch* bt, void* stream) {
   HIP_TRY(hipGetLastError());
   const PrepLayout L = prep_layout(s->ne, s->nc);
   HIP_TRY(hdg::launch_prep_maps(s, bt, L.words, L.ks, L.kt, L.ncst, st));
+  if (is_hybrid(s, path)) {        // + the general path's tables for the entity-edge stage
+    const hdg_batch bw = wide_half(bt, s);
+    return hdg::wide_prepare(s, &bw, st);
+  }
   return 0;
 }
 
@@ -3268,6 +3410,7 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
     HIP_TRY(mark(2));
     return 0;
   }
+  if (is_hybrid(s, path)) return hybrid_run(s, bt, params, grad, out, nullptr, workspace, true, st, events);
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
   const bool split = use_split(s);
@@ -3290,7 +3433,8 @@ int hdg_fwd_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, fl
 int hdg_debug_step_stamps(const hdg_shape* s, const hdg_batch* bt, const float* params,
                           void* workspace, unsigned long long* stamps, void* stream) {
   RESOLVE(s, path);
-  if (path != HDG_PATH_FUSED) return fail(HDG_EINVAL, "phase stamps exist on the fused path only");
+  if (path != HDG_PATH_FUSED || s->variant != 2)
+    return fail(HDG_EINVAL, "phase stamps exist on the fused path for model_2 only");
   if (int rc = check_batch(bt)) return rc;
   if (!stamps || !workspace || !params) return fail(HDG_EINVAL, "NULL stamps/workspace/params");
   const Work w = work_layout(s);
@@ -3324,9 +3468,11 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
   if (int rc = check_batch(bt)) return rc;
   if (!grad || !workspace) return fail(HDG_EINVAL, "NULL grad/workspace");
   hipStream_t st = (hipStream_t)stream;
-  if (path == HDG_PATH_GENERAL) {
-    if (int rc = hdg::wide_run(s, bt, state->params, grad, out, nullptr, workspace, true, st))
-      return rc;
+  if (path == HDG_PATH_GENERAL || is_hybrid(s, path)) {
+    const int rc = path == HDG_PATH_GENERAL
+        ? hdg::wide_run(s, bt, state->params, grad, out, nullptr, workspace, true, st)
+        : hybrid_run(s, bt, state->params, grad, out, nullptr, workspace, true, st, nullptr);
+    if (rc) return rc;
     return hdg_adam_tf(s, state, grad, lr, out ? out->stats : nullptr, stream);
   }
   // single process, fused path: k_commit_step (+ loss stats / Adam factor from block 0),
@@ -3353,6 +3499,8 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
   hipStream_t st = (hipStream_t)stream;
   if (path == HDG_PATH_GENERAL)
     return hdg::wide_run(s, bt, params, nullptr, out, ce_sum, workspace, false, st);
+  if (is_hybrid(s, path))
+    return hybrid_run(s, bt, params, nullptr, out, ce_sum, workspace, false, st, nullptr);
   const Work w = work_layout(s);
   float* ws = (float*)workspace;
   const bool split = use_split(s);
@@ -3481,12 +3629,14 @@ int hdg_train_step_dp(const hdg_shape* s, const hdg_batch* bt, hdg_state* state,
   hipStream_t st = (hipStream_t)stream;
   uint32_t* status = out ? out->status : nullptr;
   float* stats = out ? out->stats : nullptr;
-  if (path == HDG_PATH_GENERAL) {
+  if (path == HDG_PATH_GENERAL || is_hybrid(s, path)) {
     // the rank's own reduced gradient lands in the mailbox's local scratch (the tail
     // reads it while other blocks already write the world sums into grad)
     float* local = (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_GLOC);
-    if (int rc = hdg::wide_run(s, bt, state->params, local, out, nullptr, workspace, true, st))
-      return rc;
+    const int rc = path == HDG_PATH_GENERAL
+        ? hdg::wide_run(s, bt, state->params, local, out, nullptr, workspace, true, st)
+        : hybrid_run(s, bt, state->params, local, out, nullptr, workspace, true, st, nullptr);
+    if (rc) return rc;
     return hdg_adam_dp(s, state, local, grad, lr, stats, status, dp, stream);
   }
   // fused path: k_commit_step (aux from block 0), then the reduction + exchange + Adam

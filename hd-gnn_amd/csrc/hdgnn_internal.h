@@ -88,6 +88,17 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
 // CE sum -> *ce_sum (may be NULL).  Outputs as in hdg_fwd_bwd.
 int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
              hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st);
+// model_4 on the fused path: the entity-edge stage on the general path's kernels around
+// the fused step kernel.  wide_ee_fwd: EE first layer, node products, classifier over the
+// mapped relations -> ncls [B][Nc][2] (n_c[2:4] of marshalling_B2, model_4.py:95-97);
+// wide_ee_bwd: from dn (wide_dn, [B][Nc][4], written by the step kernel) the EE backward
+// and the reduction of the EE parameters' gradient rows into grad[EE_W11 .. EC_B2 + 2).
+// bt->prep, workspace: this path's layouts (wide_prep_bytes / wide_workspace_bytes).
+float* wide_dn(const hdg_shape* s, void* workspace);
+int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
+                float* ncls, hipStream_t st);
+int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
+                float* grad, hipStream_t st);
 
 // fused path pieces the general path reuses (hdgnn.hip)
 hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,

@@ -923,6 +923,18 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
   }
 }
 
+// kw_ee_bins  grid (ceil(2 Nc / NT), B): the EE aggregate n_c[2:4] as floats, summed over
+// the kw_ee_fwd tile partials exactly as kw_cross_fwd does (the fused step kernel's class
+// part for model_4, hdgnn.hip hybrid path)
+__global__ __launch_bounds__(NT) void kw_ee_bins(const unsigned long long* __restrict__ ncpart,
+                                                 int nt, int Nc, float* __restrict__ ncls) {
+  const int b = blockIdx.y, e = blockIdx.x * NT + threadIdx.x;
+  if (e >= 2 * Nc) return;
+  unsigned long long a = 0ull;
+  for (int tl = 0; tl < nt; ++tl) a += ncpart[((size_t)b * nt + tl) * 2 * Nc + e];
+  ncls[(size_t)b * 2 * Nc + e] = (float)((double)a * (1.0 / FIX));
+}
+
 // ---------------------------------------------------------------------------------
 // Hunk pair passes (tile of 64 hunks = lanes, 8 waves split the swept index m).  The
 // swept side's node vectors are staged in LDS in chunks of CHM rows and read as
@@ -2296,9 +2308,96 @@ WideWork wide_layout(const hdg_shape* s) {
     if (e_ != hipSuccess) return fail((int)e_, "%s: %s", #expr, hipGetErrorString(e_));   \
   } while (0)
 
+int set_wide_attrs() {
+  static bool attr_set = false;   // > 64 KiB of dynamic LDS for Ne > 4000
+  if (!attr_set) {
+    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<0>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             96 * 1024));
+    attr_set = true;
+  }
+  return 0;
+}
+
 }  // namespace
 
 size_t wide_workspace_bytes(const hdg_shape* s) { return wide_layout(s).total * sizeof(float); }
+
+// ---- model_4 on the fused path (hdgnn.hip): the entity-edge stage on this path's kernels
+// around the fused step kernel, which runs the model_2-shaped rest of the step ----------
+float* wide_dn(const hdg_shape* s, void* workspace) {
+  return (float*)workspace + wide_layout(s).dn;
+}
+
+int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
+                float* ncls, hipStream_t st) {
+  const int B = s->batch, Ne = s->ne, Nc = s->nc;
+  const Off o = param_offsets(s->variant);
+  const WideWork w = wide_layout(s);
+  float* ws = (float*)workspace;
+  auto F = [&](size_t off) { return ws + off; };
+  const uint32_t* prep = (const uint32_t*)bt->prep;
+  const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
+  const int te = (Ne + TN - 1) / TN;
+  if (int rc = set_wide_attrs()) return rc;
+  hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, ws + w.D);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+                     bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1));
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, 1), dim3(NT), 0, st, bt->x, params, o, Ne, 0,
+                     F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.R1), F(w.C1), F(w.Rn),
+                     F(w.Cn), F(w.rho), F(w.gmm));
+  WTRY(hipGetLastError());
+  unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
+  const size_t elds = (size_t)((2 * Nc + 1) & ~1) * 8 +
+                      (Ne <= EE_GAM_LDS_MAX ? (size_t)Ne * H * 4 : 0);
+  hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NTP), elds, st, bt->abits, bt->hid, bt->nlen,
+                     params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), ncpart);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_ee_bins, dim3((2 * Nc + NT - 1) / NT, B), dim3(NT), 0, st, ncpart, te, Nc,
+                     ncls);
+  WTRY(hipGetLastError());
+  return 0;
+}
+
+int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
+                float* grad, hipStream_t st) {
+  const int B = s->batch, Ne = s->ne, Nc = s->nc;
+  const Off o = param_offsets(s->variant);
+  const WideWork w = wide_layout(s);
+  float* ws = (float*)workspace;
+  auto F = [&](size_t off) { return ws + off; };
+  const uint32_t* prep = (const uint32_t*)bt->prep;
+  const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
+  const int te = (Ne + TN - 1) / TN;
+  float* part = ws;
+  const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
+  hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
+                     bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
+                     F(w.dgam), part, w.segs);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
+                     F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
+                     F(w.psi), (double*)F(w.tab));
+  WTRY(hipGetLastError());
+  hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+                     bt->abits, prep, params, o, Ne, Nc, F(w.phi), F(w.psi),
+                     (const double*)F(w.tab), part, w.segs);
+  WTRY(hipGetLastError());
+  // the entity-edge parameters [EE_W11, EC_B2 + 2): one contiguous block of the flat vector
+  const int p0 = o.EE_W11, n = o.EC_B2 + 2 - o.EE_W11;
+  hipLaunchKernelGGL(kw_grad_reduce, dim3(n), dim3(64), 0, st, part, w.segs, p0, o.NP, grad + p0);
+  WTRY(hipGetLastError());
+  return 0;
+}
 
 void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
                              int64_t* ncst) {
@@ -2347,18 +2446,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   auto F = [&](size_t off) { return ws + off; };
 
   const size_t tlds = sort_lds_bytes(Ne);
-  static bool attr_set = false;   // > 64 KiB of dynamic LDS for Ne > 4000
-  if (!attr_set) {
-    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<0>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             96 * 1024));
-    attr_set = true;
-  }
+  if (int rc = set_wide_attrs()) return rc;
   hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D);
   WTRY(hipGetLastError());
   // ---- entity side ----

@@ -110,6 +110,43 @@ def test_variant_matches_oracle(v, B, ne, nc, seed):
     _run_and_check(synth_commits(B, ne, nc, seed), v, seed)
 
 
+FUS = _lib.PATH_FUSED
+
+
+@pytest.mark.parametrize("B,ne,nc,seed", SHAPES + [(1, 256, 160, 6), (2, 120, 100, 8)])
+def test_model2_fused_path_matches_oracle(B, ne, nc, seed):
+    """the fused path over every tile width of its hunk passes (NC16 = 16 .. 160)"""
+    _run_and_check(synth_commits(B, ne, nc, seed), 2, seed, FUS)
+
+
+@pytest.mark.parametrize("B,ne,nc,seed", SHAPES + [(1, 256, 160, 6)])
+def test_model4_fused_path_matches_oracle(B, ne, nc, seed):
+    """model_4 on the fused path: the entity-edge stage on the general kernels around the
+    fused step kernel (class part of n_c in, dn out), up to the fused engine's limits."""
+    _run_and_check(synth_commits(B, ne, nc, seed), 4, seed, FUS)
+
+
+def test_model4_fused_equals_general():
+    B, ne, nc, v = 3, 200, 74, 4
+    cb = synth_commits(B, ne, nc, 13)
+    flat = layout.init_flat(2, v)
+    outs = []
+    for path in (FUS, GEN):
+        eng = _engine(B, ne, nc, v, path)
+        assert eng.path == path
+        eng.set_params(flat)
+        eng.fwd_bwd(eng.upload(cb))
+        torch.cuda.synchronize()
+        outs.append((eng.logits.cpu().numpy().astype(np.float64),
+                     eng.grad.cpu().numpy().astype(np.float64)))
+    (l1, g1), (l2, g2) = outs
+    scale = np.maximum(1.0, np.abs(l1).max())
+    assert np.abs(l1 - l2).max() <= 1e-4 * scale
+    np_ = layout.n_params(v)
+    _grad_close(g2[:np_], g1[:np_], v)
+    assert _lib.trailer_count(g1[np_:]) == _lib.trailer_count(g2[np_:])
+
+
 @pytest.mark.parametrize("v", [2, 4])
 def test_stress_shape_matches_oracle(v):
     """BASELINE config 5 shapes (Ne=1024, Nc=512): beyond the fused kernel's LDS budget."""
@@ -151,17 +188,19 @@ EDGE = {
 }
 
 
+@pytest.mark.parametrize("path", [GEN, FUS])
 @pytest.mark.parametrize("case", sorted(EDGE))
-def test_model4_edge_cases(case):
+def test_model4_edge_cases(case, path):
     cb = EDGE[case](synth_commits(2, 70, 13, 7))
-    _run_and_check(cb, 4, 7)
+    _run_and_check(cb, 4, 7, path)
 
 
-def test_model4_train_steps_match_oracle_adam():
+@pytest.mark.parametrize("path", [GEN, FUS])
+def test_model4_train_steps_match_oracle_adam(path):
     B, ne, nc, seed, v = 2, 45, 17, 5, 4
     cb = synth_commits(B, ne, nc, seed)
     flat = layout.init_flat(seed, v)
-    eng = _engine(B, ne, nc, v)
+    eng = _engine(B, ne, nc, v, path)
     eng.set_params(flat)
     db = eng.upload(cb)
     theta = flat.astype(np.float64)
@@ -188,11 +227,12 @@ def test_general_deterministic_bitwise():
     assert torch.equal(g1, eng.grad) and torch.equal(p1, eng.probs)
 
 
-def test_general_graph_replay_equals_eager():
+@pytest.mark.parametrize("path", [GEN, FUS])
+def test_general_graph_replay_equals_eager(path):
     B, ne, nc, v = 3, 50, 30, 4
     cb = synth_commits(B, ne, nc, 4)
     flat = layout.init_flat(3, v)
-    e1, e2 = _engine(B, ne, nc, v), _engine(B, ne, nc, v)
+    e1, e2 = _engine(B, ne, nc, v, path), _engine(B, ne, nc, v, path)
     e1.set_params(flat)
     e2.set_params(flat)
     db = e1.upload(cb)
@@ -204,7 +244,8 @@ def test_general_graph_replay_equals_eager():
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.probs, e2.probs)
 
 
-@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN), (1, GEN)])
+@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN), (4, _lib.PATH_FUSED),
+                                    (1, GEN)])
 def test_workspace_garbage_does_not_leak(v, path):
     """Every workspace word a step reads it wrote first: prefilling the caller's workspace,
     gradient and outputs with NaN / Inf / huge values must not change one bit (a kernel that
@@ -227,7 +268,7 @@ def test_workspace_garbage_does_not_leak(v, path):
         assert torch.equal(e.grad, g0) and torch.equal(e.probs, p0), "fill %g" % fill
 
 
-@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN)])
+@pytest.mark.parametrize("v,path", [(2, _lib.PATH_FUSED), (2, GEN), (4, GEN), (4, _lib.PATH_FUSED)])
 def test_on_device_correct_count(v, path):
     """Gradient trailer count slots = EvaluationFuncs.top_ACC numerator on the returned probs
     (np.argmax tie rule), exactly; forward-only leaves the CE slot intact."""

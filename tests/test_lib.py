@@ -49,11 +49,21 @@ def test_host_only_entry_points():
         assert lib.hdg_resolve_path(ctypes.byref(sh)) == _lib.PATH_FUSED
         assert lib.hdg_workspace_bytes(ctypes.byref(sh)) > 0, lib.hdg_last_error()
     # beyond the fused kernel (stress shape, other variants): the general path
-    for v, ne, nc in ((2, 1024, 512), (2, 300, 74), (1, 200, 74), (3, 200, 74), (4, 200, 74)):
+    for v, ne, nc in ((2, 1024, 512), (2, 300, 74), (1, 200, 74), (3, 200, 74), (4, 300, 74),
+                      (4, 1024, 512)):
         sh = _lib.Shape(32, ne, nc, v, 256, 0)
         assert lib.hdg_resolve_path(ctypes.byref(sh)) == _lib.PATH_GENERAL
         assert lib.hdg_workspace_bytes(ctypes.byref(sh)) > 0, lib.hdg_last_error()
         assert lib.hdg_prep_bytes(ctypes.byref(sh)) > 0
+    # model_4 within the fused engine's limits: the fused path with the entity-edge stage on
+    # the general kernels; its prep / workspace hold both paths' parts
+    m4 = _lib.Shape(100, 200, 74, 4, 100, 0)
+    assert lib.hdg_resolve_path(ctypes.byref(m4)) == _lib.PATH_FUSED
+    m4g = _lib.Shape(100, 200, 74, 4, 100, _lib.PATH_GENERAL)
+    m2 = _lib.Shape(100, 200, 74, 2, 100, 0)
+    assert lib.hdg_prep_bytes(ctypes.byref(m4)) == (lib.hdg_prep_bytes(ctypes.byref(m2)) +
+                                                     lib.hdg_prep_bytes(ctypes.byref(m4g)))
+    assert lib.hdg_workspace_bytes(ctypes.byref(m4)) > lib.hdg_workspace_bytes(ctypes.byref(m4g))
     forced = _lib.Shape(4, 200, 74, 2, 4, _lib.PATH_GENERAL)
     assert lib.hdg_resolve_path(ctypes.byref(forced)) == _lib.PATH_GENERAL
     bad = _lib.Shape(100, 300, 74, 2, 100, _lib.PATH_FUSED)
