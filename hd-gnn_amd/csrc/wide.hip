@@ -170,7 +170,9 @@ enum : int {
   D_DLT = 480,             // V1[9] - V1[8]
   D_EED = 500,             // EE classifier P1[1] - P1[0]
   D_EEC = 520,             // EE classifier U2'[:,1] - U2'[:,0]
-  D_WORDS = 544
+  D_EECQ = 544,            // -log2(e) (U2'[:,1] - U2'[:,0])    (kw_ee_clsb: e = 2^delta')
+  D_EEBQ = 564,            // -log2(e) (b2'[1] - b2'[0])
+  D_WORDS = 576
 };
 
 // Prepared batch of the general path, per commit (words): cross-graph counts as in the
@@ -264,6 +266,8 @@ __global__ __launch_bounds__(NT) void kw_derive(const float* __restrict__ W, Off
     if (o.EC_W1 >= 0) {
       D[D_EED + t] = W[o.EC_W1 + H + t] - W[o.EC_W1 + t];
       D[D_EEC + t] = W[o.EC_W2 + 2 * t + 1] - W[o.EC_W2 + 2 * t];
+      D[D_EECQ + t] = -1.4426950408889634f * D[D_EEC + t];
+      if (t == 0) D[D_EEBQ] = -1.4426950408889634f * (W[o.EC_B2 + 1] - W[o.EC_B2]);
     }
   }
 }
@@ -1762,184 +1766,93 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ee_clsb  grid (te, B): entity-edge classifier backward (model_4.py:286-304)
-//   dp_r[m] = dn[hid i'(r)][2+m] + dn[hid j'(r)][2+m];  dz1 = p0 p1 (dp1 - dp0) = -dz0
-//   g_ijk = [kappa'_ijk > 0] (U2'[k][1] - U2'[k][0]) dz1
-//   column pass (lane = column j): dgam_j = sum_i g, classifier partial rows, and per row
-//   i the tile's partial of drho_i = sum_j g (wave_sums20 over the 64 column lanes; the
-//   te tile partials are summed in tile order by kw_ee_nodeb).  The row-pass body (z = 1,
-//   lane = row i) is kept for reference but no longer launched.
-//   8 waves; the swept side's operand rows staged in LDS, packed fp32, the class bits read
-//   from the lane's own row of a (row pass) or a^T (column pass).
-//   dynamic LDS: hid[Ne] (int), dn class part [Nc][2]
+// kw_ee_clsb  grid (te, B), 8 waves: entity-edge classifier backward (model_4.py:286-304)
+//   dz1 = p0 p1 (dp1 - dp0) = -dz0, dp_r[m] = dn[hid i'(r)][2+m] + dn[hid j'(r)][2+m]
+//   (relation r -> index pair (i', j') on the n-grid, the stride quirk of utils2.py:121-137);
+//   the two-class softmax as a sigmoid of the logit difference: with
+//   c = U2'[:,1] - U2'[:,0], delta = (b2'[1] - b2'[0]) + sum_k relu(kappa_k) c_k,
+//   e = exp(-delta) = 2^delta' (delta' from the prescaled D_EECQ / D_EEBQ), p1 = 1 / (1 + e),
+//   p0 p1 = e p1^2;  g_k = [kappa_k > 0] c_k dz1 = c_k s_k: the pair loop sums
+//   s_k = [kappa_k > 0] dz1 and c scales the sums once.
+//   Lane = column j, the waves share the rows i (rho rows staged in LDS, broadcast reads; the
+//   lane's gam row from LDS too, conflict-free [v][lane] 16-byte reads).  Per row the 64
+//   lanes' s-vectors are summed across the wave: this tile's partial row of drho / c
+//   (kw_ee_nodeb sums the te partials in tile order and scales by c);
+//   per lane over the rows: dgam_j.  The weight constants are wave-uniform scalar loads
+//   (no LDS traffic, no VGPRs).  dynamic LDS: Eq[Ne] = dn[hid q][3] - dn[hid q][2].
 // ---------------------------------------------------------------------------------
-struct EEBwdSmem {
-  float* os_;
-  float* buf;
-  float* res;
-  float* red;
-  float* tot;
-  int* hl;
-  float* dnl;
-  const float* cst;   // U2' (2H) | EE a-offsets d (H) | U2'[k][1] - U2'[k][0] (H): broadcast reads
-  const float* own;   // the 64 lane nodes' own operand rows [TN][H] (read per row, not held)
-};
+// q = r / d, rem = r % d for 0 <= r < 2^24, 1 <= d < 2^12: float estimate, one select
+// correction each way (the estimate is within one of q), no branches
+__device__ __forceinline__ void divmod_sel(int r, int d, float inv, int& q, int& rem) {
+  const int q0 = (int)((float)r * inv);
+  const int r0 = r - q0 * d;
+  const bool lo = r0 < 0, hi = r0 >= d;
+  q = lo ? q0 - 1 : (hi ? q0 + 1 : q0);
+  rem = lo ? r0 + d : (hi ? r0 - d : r0);
+}
 
-template <int Z>
-__device__ __forceinline__ void ee_clsb_body(
-    const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
-    const float* __restrict__ W, const Off& o, const float* __restrict__ D, int Ne, int nrel,
-    int dn1, const float* __restrict__ rho, const float* __restrict__ gmm,
-    float* __restrict__ drho, float* __restrict__ dgam, float* __restrict__ part, const Segs& sg,
-    const EEBwdSmem& sm) {
-#pragma clang fp contract(off)
-  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+__device__ __forceinline__ void ee_clsb_rows(
+    const int lo, const int hi, const int c0, const float* os_, const uint32_t* abl,
+    const int Ne, const int jn, const bool live, const int nrel, const int dn1, const float inv,
+    const bool aligned, const float* Eq, const float Ej, const float4* gl,
+    const float* __restrict__ D, float* rowp, f2 (&acc)[H2], f2 (&ag)[H2], float& sdl,
+    float& zr, int& kst) {
   const int lane = threadIdx.x & 63;
-  const int WE = (Ne + 31) >> 5;
-  const int nd = t0 + lane, ncl = nd < Ne ? nd : Ne - 1;
-  const float* obase = (Z ? gmm : rho) + (size_t)b * Ne * H;   // swept operand
-  const float* own = (Z ? rho : gmm) + ((size_t)b * Ne + ncl) * H;
-  const uint32_t* brow = (Z ? abits : aT) + ((size_t)b * Ne + ncl) * WE;
-  // the weight constants are LDS broadcast reads in the row loop (sm.cst), not registers:
-  // 80 VGPRs fewer, 4 waves per SIMD instead of 2 (two blocks per CU); the lane's own
-  // operand row is an LDS read per row too (sm.own): 20 VGPRs fewer, no spills
-  (void)own;
-  f2 acc[H2], zk[H2], ag[H2];
-#pragma unroll
-  for (int kk = 0; kk < H2; ++kk) {
-    acc[kk] = (f2){0.f, 0.f};
-    zk[kk] = acc[kk];
-    ag[kk] = acc[kk];
-  }
-  const f2 bb = ld2(W + o.EC_B2);
-  const float inv = 1.f / (float)dn1;
-  float sdl = 0.f;
-  // rows that hold relations r < nrel
-  const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
-  const int Nsw = (Z == 1 && t0 >= rows) ? 0 : (Z ? Ne : rows);   // block-uniform
-  float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // Z = 0: row partials
-  if constexpr (Z == 0)                                   // rows past the relations: 0
-    for (int e = rows * H + threadIdx.x; e < Ne * H; e += NTP) rowp[e] = 0.f;
-  for (int c0 = 0; c0 < Nsw; c0 += CHM) {
-    const int c1 = c0 + CHM < Nsw ? c0 + CHM : Nsw;
-    __syncthreads();
-    stage_rows(sm.os_, obase, c0, c1);
-    __syncthreads();
-    int lo, hi;
-    wave_share(c0, c1, lo, hi);
-    int wi = -1;
-    uint32_t word = 0;
-    for (int m = lo; m < hi; ++m) {
-      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
-      const float af = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
-      const int i = Z ? ncl : m, j = Z ? m : ncl;
-      const int r = i * (Ne - 1) + j - (j > i ? 1 : 0);
-      const bool valid = nd < Ne && i != j && r < nrel;
-      float dp0 = 0.f, dp1 = 0.f;
-      if (valid && !(EE_ABL & 2)) {
-        int ip, jj;
-        divmod24(r, dn1, inv, ip, jj);
-        const int jp = jj + (jj >= ip ? 1 : 0);
-        const int hs = sm.hl[ip], ht = sm.hl[jp];
-        if (hs >= 0) { dp0 += sm.dnl[2 * hs]; dp1 += sm.dnl[2 * hs + 1]; }
-        if (ht >= 0) { dp0 += sm.dnl[2 * ht]; dp1 += sm.dnl[2 * ht + 1]; }
-      }
-      const f2 a2 = {af, af};
-      const float4* o4 = reinterpret_cast<const float4*>(sm.os_ + (m - c0) * H);
-      int co = 0;                  // opaque 0: keeps the constant reads in the loop (LDS
-      asm volatile("" : "+v"(co)); // broadcast) instead of hoisted into 80 VGPRs
-      const float4* cu2 = reinterpret_cast<const float4*>(sm.cst + co);          // u2 pairs
-      const float4* cdl = reinterpret_cast<const float4*>(sm.cst + co + 2 * H);  // d
-      const float4* ccE = reinterpret_cast<const float4*>(sm.cst + co + 3 * H);  // c
-      const float4* ow4 = reinterpret_cast<const float4*>(sm.own + co + lane * H);
-      f2 pre[H2];
-      f2 zz = bb;
-#pragma unroll
-      for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j: the same sum kw_ee_fwd forms
-        const float4 q = o4[v], dv = cdl[v], w4 = ow4[v];
-        pre[2 * v] = fma2(a2, (f2){dv.x, dv.y}, (f2){w4.x, w4.y} + (f2){q.x, q.y});
-        pre[2 * v + 1] = fma2(a2, (f2){dv.z, dv.w}, (f2){w4.z, w4.w} + (f2){q.z, q.w});
-      }
-#pragma unroll
-      for (int kk = 0; kk < H2; ++kk) {
-        const f2 kp = relu2(pre[kk]);
-        const float4 w = cu2[kk];
-        zz = fma2((f2){kp.x, kp.x}, (f2){w.x, w.y}, zz);
-        zz = fma2((f2){kp.y, kp.y}, (f2){w.z, w.w}, zz);
-      }
-      float p0, p1;
-      if constexpr (EE_ABL & 4) {
-        p0 = zz.x; p1 = zz.y;
-      } else {
-        const float mx = fmaxf(zz.x, zz.y);
-        const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
-        const float iv = __builtin_amdgcn_rcpf(e0 + e1);    // e0 + e1 in [1, 2]: 1-ulp rcp
-        p0 = e0 * iv; p1 = e1 * iv;
-      }
-      const float d1 = valid ? p0 * p1 * (dp1 - dp0) : 0.f;
-      const f2 d2 = {d1, d1};
-      float gv[H];
-#pragma unroll
-      for (int kk = 0; kk < H2; ++kk) {
-        const float4 cv = ccE[kk >> 1];
-        const f2 cd = ((kk & 1) ? (f2){cv.z, cv.w} : (f2){cv.x, cv.y}) * d2;
-        const f2 g = {pre[kk].x > 0.f ? cd.x : 0.f, pre[kk].y > 0.f ? cd.y : 0.f};
-        acc[kk] += g;
-        gv[2 * kk] = g.x;
-        gv[2 * kk + 1] = g.y;
-        if constexpr (Z == 0) {
-          zk[kk] = fma2(relu2(pre[kk]), d2, zk[kk]);
-          ag[kk] = fma2(a2, g, ag[kk]);
-        }
-      }
-      if constexpr (Z == 0) {
-        sdl += d1;
-        // the row pass folded in: this tile's 64 columns of row i = m, one partial row
-        // of drho per tile (kw_ee_nodeb sums the te partials in tile order)
-        if constexpr (EE_ABL & 1) {
-          float sgv = 0.f;
-#pragma unroll
-          for (int k = 0; k < H; ++k) sgv += gv[k];
-          if (lane == 0) rowp[(size_t)m * H] = sgv;
-        } else {
-          wave_sums20(gv, lane, [&](int k, float x) { rowp[(size_t)m * H + k] = x; });
-        }
-      }
+  const float bq = D[D_EEBQ];
+  int wi = -1;
+  uint32_t word = 0;
+  for (int m = lo; m < hi; ++m) {
+    if ((m >> 5) != wi) { wi = m >> 5; word = abl[wi * TN]; }
+    const float af = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+    const f2 a2 = {af, af};
+    const int r = m * (Ne - 1) + jn - (jn > m ? 1 : 0);
+    const bool valid = live && m != jn && r < nrel;
+    float dp;
+    if (aligned) {                     // n = Ne: (i', j') = (i, j)   (block-uniform branch)
+      dp = Eq[m] + Ej;
+    } else {
+      int ip, jj;
+      divmod_sel(r < nrel ? r : 0, dn1, inv, ip, jj);
+      dp = Eq[ip] + Eq[jj + (jj >= ip ? 1 : 0)];
     }
-  }
-  combine8(acc, sm.buf, sm.res);
-  float* dout = (Z ? drho : dgam) + (size_t)b * Ne * H;   // (Z = 1 no longer launched)
-  for (int e = threadIdx.x; e < TN * H; e += NTP) {
-    const int nn = e / H, k = e - nn * H;
-    if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = sm.res[nn * HP + k];
-  }
-  if constexpr (Z == 0) {   // classifier partial rows
-    float v[41];
+    const float* orow = os_ + (m - c0) * H;
+    const float4* o4 = reinterpret_cast<const float4*>(orow);
+    f2 pre[H2], st[H2];
+#pragma unroll
+    for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + gam_j + a d: the sum kw_ee_fwd forms
+      const float4 q = o4[v], g = gl[v * TN];
+      pre[2 * v] = fma2(a2, ld2(D + D_EED + 4 * v), (f2){g.x, g.y} + (f2){q.x, q.y});
+      pre[2 * v + 1] = fma2(a2, ld2(D + D_EED + 4 * v + 2), (f2){g.z, g.w} + (f2){q.z, q.w});
+    }
+    f2 dz = {bq, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < H2; ++kk) {  // relu(kappa) = kappa [kappa > 0]
+      st[kk] = step2(pre[kk]);
+      dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
+    }
+    const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
+    const float p1 = __builtin_amdgcn_rcpf(1.f + e);
+    const float d1 = valid ? (e * p1) * (p1 * dp) : 0.f;
+    const f2 d2 = {d1, d1};
+    sdl += d1;
+    float sv[H];
 #pragma unroll
     for (int kk = 0; kk < H2; ++kk) {
-      v[2 * kk] = zk[kk].x; v[2 * kk + 1] = zk[kk].y;
-      v[H + 2 * kk] = ag[kk].x; v[H + 2 * kk + 1] = ag[kk].y;
+      const f2 sd = st[kk] * d2;
+      acc[kk] += sd;
+      ag[kk] = fma2(a2, sd, ag[kk]);
+      sv[2 * kk] = sd.x;
+      sv[2 * kk + 1] = sd.y;
     }
-    v[40] = sdl;
-    block_sum8<41>(v, sm.red, sm.tot);
-    const int row = b * te + blockIdx.x;
-    const int t = threadIdx.x;
-    if (t < H) {
-      float sg_ = 0.f;   // sum of g over the tile = sum of the combined column sums
-      for (int nn = 0; nn < TN; ++nn) sg_ += (t0 + nn < Ne) ? sm.res[nn * HP + t] : 0.f;
-      const Seg& sa = sg.s[SG_ECW1A];
-      const Seg& sb = sg.s[SG_ECB1];
-      put(part, sa, t, row, sg_ - sm.tot[H + t]);       // P1[0] ([a = 0] input)
-      put(part, sa, H + t, row, sm.tot[H + t]);         // P1[1] ([a = 1] input)
-      put(part, sb, t, row, sg_);                       // p1 bias
-      put(part, sb, H + 2 * t, row, -sm.tot[t]);        // U2'[k][0]
-      put(part, sb, H + 2 * t + 1, row, sm.tot[t]);     // U2'[k][1]
-    }
-    if (t == 0) {
-      const Seg& sb = sg.s[SG_ECB1];
-      put(part, sb, 3 * H, row, -sm.tot[40]);
-      put(part, sb, 3 * H + 1, row, sm.tot[40]);
-    }
+    // the row's sums over the tile: this tile's drho partial (without c: kw_ee_nodeb scales
+    // the summed partials) and, for the classifier's second layer,
+    // sum_j relu(kappa) dz1 = sum_j kappa s dz1: its rho part rho_i . (row sum) here, the gam
+    // and a d parts from the column sums after the loop
+    wave_sums20(sv, lane, [&](int k, float x) {
+      rowp[(size_t)m * H + k] = x;
+      zr = fmaf(orow[k], x, zr);
+      kst = k;
+    });
   }
 }
 
@@ -1949,45 +1862,117 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
     const float* __restrict__ rho, const float* __restrict__ gmm, const float* __restrict__ dn,
     float* __restrict__ drho, float* __restrict__ dgam, float* __restrict__ part, Segs sg) {
-  extern __shared__ float dyn[];
+#pragma clang fp contract(off)
+  (void)abits;
+  (void)W;
+  extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][64]
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
   __shared__ float buf[NWP * TN * HP];
   __shared__ float res[TN * HP];
-  __shared__ float red[NWP * 41];
-  __shared__ float tot[41];
-  __shared__ __attribute__((aligned(16))) float cst[4 * H];
-  __shared__ __attribute__((aligned(16))) float owl[TN * H];
-  const int b = blockIdx.y;
+  __shared__ float red[NWP * 21];
+  __shared__ float tot[21];
+  __shared__ float cl[H];
+  __shared__ float zred[NWP * H];
+  __shared__ float4 gl4[(H / 4) * TN];            // the lane columns' gam rows, [v][lane]
+  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   const int nrel = n >= 2 ? n * (n - 1) : 0;
-  EEBwdSmem sm;
-  sm.os_ = os_; sm.buf = buf; sm.res = res; sm.red = red; sm.tot = tot; sm.cst = cst;
-  sm.own = owl;
-  {                         // the lane nodes' own rows (column pass: gam rows t0 .. t0 + 63)
-    const int t0 = blockIdx.x * TN;
-    const float4* src = reinterpret_cast<const float4*>(gmm + (size_t)b * Ne * H);
-    for (int e = threadIdx.x; e < TN * (H / 4); e += NTP) {
-      const int l = e / (H / 4), node = t0 + l < Ne ? t0 + l : Ne - 1;
-      reinterpret_cast<float4*>(owl)[e] = src[(size_t)node * (H / 4) + e - l * (H / 4)];
-    }
-  }
-  sm.hl = reinterpret_cast<int*>(dyn);
-  sm.dnl = dyn + Ne;
-  if (threadIdx.x < 2 * H) cst[threadIdx.x] = W[o.EC_W2 + threadIdx.x];
-  if (threadIdx.x < H) {
-    cst[2 * H + threadIdx.x] = D[D_EED + threadIdx.x];
-    cst[3 * H + threadIdx.x] = D[D_EEC + threadIdx.x];
-  }
-  for (int e = threadIdx.x; e < Ne; e += NTP) {
-    const int h = hidg[(size_t)b * Ne + e];
-    sm.hl[e] = (h >= 0 && h < Nc) ? h : -1;
-  }
-  for (int e = threadIdx.x; e < 2 * Nc; e += NTP)
-    sm.dnl[e] = dn[((size_t)b * Nc + e / 2) * 4 + 2 + (e & 1)];
-  __syncthreads();
   const int dn1 = n - 1 > 0 ? n - 1 : 1;
-  ee_clsb_body<0>(abits, aT, W, o, D, Ne, nrel, dn1, rho, gmm, drho, dgam, part, sg, sm);
+  const int WE = (Ne + 31) >> 5;
+  float* Eq = dyn;
+  uint32_t* abl = reinterpret_cast<uint32_t*>(dyn + Ne);
+  for (int e = t; e < Ne; e += NTP) {
+    const int h = hidg[(size_t)b * Ne + e];
+    const float* d = dn + ((size_t)b * Nc + (h >= 0 && h < Nc ? h : 0)) * 4;
+    Eq[e] = (h >= 0 && h < Nc) ? d[3] - d[2] : 0.f;
+  }
+  for (int e = t; e < WE * TN; e += NTP) {        // a^T rows of the tile's columns: bit m = a[m][j]
+    const int w = e / TN, l = e - w * TN, node = t0 + l < Ne ? t0 + l : Ne - 1;
+    abl[e] = aT[((size_t)b * Ne + node) * WE + w];
+  }
+  if (t < H) cl[t] = D[D_EEC + t];
+  for (int e = t; e < (H / 4) * TN; e += NTP) {   // [v][lane]: conflict-free 16-B reads
+    const int v = e / TN, l = e - v * TN, node = t0 + l < Ne ? t0 + l : Ne - 1;
+    gl4[e] = reinterpret_cast<const float4*>(gmm + ((size_t)b * Ne + node) * H)[v];
+  }
+  const int jn = t0 + lane, jc = jn < Ne ? jn : Ne - 1;
+  const bool live = jn < Ne;
+  f2 acc[H2], ag[H2];
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    acc[kk] = (f2){0.f, 0.f};
+    ag[kk] = acc[kk];
+  }
+  float sdl = 0.f, zr = 0.f;
+  int kst = -1;
+  // rows holding relations r < nrel
+  const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
+  float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // this tile's partial rows
+  for (int e = rows * H + t; e < Ne * H; e += NTP) rowp[e] = 0.f;   // rows past the relations
+  const float* rb = rho + (size_t)b * Ne * H;
+  const float inv = 1.f / (float)dn1;
+  const bool aligned = n == Ne;
+  __syncthreads();                                 // Eq, abl, cl, gl4
+  const float Ej = Eq[jc];
+  for (int c0 = 0; c0 < rows; c0 += CHM) {
+    const int c1 = c0 + CHM < rows ? c0 + CHM : rows;
+    __syncthreads();
+    stage_rows(os_, rb, c0, c1);
+    __syncthreads();
+    int lo, hi;
+    wave_share(c0, c1, lo, hi);
+    ee_clsb_rows(lo, hi, c0, os_, abl + lane, Ne, jn, live, nrel, dn1, inv, aligned, Eq, Ej,
+                 gl4 + lane, D, rowp, acc, ag, sdl, zr, kst);
+  }
+  if (lane < H) zred[wv * H + lane] = 0.f;
+  __syncthreads();
+  if (kst >= 0) zred[wv * H + kst] = zr;           // one storing lane per (wave, unit)
+  combine8(acc, buf, res);                         // sum over the waves' row shares (barriers)
+  float* dout = dgam + (size_t)b * Ne * H;
+  for (int e = t; e < TN * H; e += NTP) {
+    const int nn = e / H, k = e - nn * H;
+    if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = res[nn * HP + k] * cl[k];
+  }
+  float v[21];                                     // classifier partial rows
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    v[2 * kk] = ag[kk].x;
+    v[2 * kk + 1] = ag[kk].y;
+  }
+  v[20] = sdl;
+  block_sum8<21>(v, red, tot);
+  const int row = b * te + blockIdx.x;
+  if (t < H) {
+    // sum_pairs relu(kappa_k) dz1 = sum_i rho_ik R_ik + sum_j gam_jk C_jk + d_k sum_{a=1} s_k dz1
+    // (kappa = rho + gam + a d; R, C the row / column sums of s dz1)
+    float sc = 0.f, zg = 0.f;
+    const float* glf = reinterpret_cast<const float*>(gl4);
+    for (int nn = 0; nn < TN; ++nn) {
+      if (t0 + nn >= Ne) break;
+      const float cs = res[nn * HP + t];
+      sc += cs;
+      zg = fmaf(glf[((t >> 2) * TN + nn) * 4 + (t & 3)], cs, zg);
+    }
+    float zw = 0.f;
+    for (int w = 0; w < NWP; ++w) zw += zred[w * H + t];
+    const float zk = (zw + zg) + D[D_EED + t] * tot[t];
+    const float sg_ = sc * cl[t];                    // sum of g over the tile
+    const float a1 = tot[t] * cl[t];
+    const Seg& sa = sg.s[SG_ECW1A];
+    const Seg& sb = sg.s[SG_ECB1];
+    put(part, sa, t, row, sg_ - a1);                 // P1[0] ([a = 0] input)
+    put(part, sa, H + t, row, a1);                   // P1[1] ([a = 1] input)
+    put(part, sb, t, row, sg_);                      // p1 bias
+    put(part, sb, H + 2 * t, row, -zk);              // U2'[k][0]
+    put(part, sb, H + 2 * t + 1, row, zk);           // U2'[k][1]
+  }
+  if (t == 0) {
+    const Seg& sb = sg.s[SG_ECB1];
+    put(part, sb, 3 * H, row, -tot[20]);
+    put(part, sb, 3 * H + 1, row, tot[20]);
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1996,7 +1981,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
 // dQ2 = sum R1 (x) dR + C1 (x) dC, dq2 = (Ne-1) sum (dR + dC)
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void kw_ee_nodeb(
-    const float* __restrict__ W, Off o, int Ne, const float* __restrict__ R1,
+    const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, const float* __restrict__ R1,
     const float* __restrict__ C1, const float* __restrict__ Rn, const float* __restrict__ Cn,
     const float* __restrict__ drho, const float* __restrict__ dgam, float* __restrict__ phi,
     float* __restrict__ psi, float* __restrict__ part, Segs sg) {
@@ -2051,7 +2036,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
 #pragma unroll
   for (int it = 0; it < NE_IT; ++it) {
     const int e = t + it * NT, n = e / H, k = e - n * H;
-    A[n * HP + k] = dr[it];
+    A[n * HP + k] = dr[it] * D[D_EEC + k];   // kw_ee_clsb's row partials leave c out
   }
   __syncthreads();
   const int lane = t & 63;
@@ -2377,12 +2362,12 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const int te = (Ne + TN - 1) / TN;
   float* part = ws;
-  const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
+  const size_t lds = (size_t)(Ne + TN * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
   hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
                      bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                      F(w.dgam), part, w.segs);
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
+  hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne, F(w.R1), F(w.C1),
                      F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
@@ -2518,12 +2503,12 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     WTRY(hipGetLastError());
   }
   if (ee) {
-    const size_t lds = (size_t)(Ne + 2 * Nc) * 4;
+    const size_t lds = (size_t)(Ne + TN * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
     hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
                        bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                        F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, Ne, F(w.R1), F(w.C1),
+    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne, F(w.R1), F(w.C1),
                        F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,

@@ -1,5 +1,5 @@
 # GPU box: bench.py over the BASELINE configs / variants / engine paths (one JSON line each)
-# + a kernel trace of the general path (model_4, glide) for the per-kernel split.
+# + a kernel trace of model_4 at glide (fused step kernel + entity-edge general kernels).
 set -o pipefail
 mkdir -p gpurun_out/matrix
 run() {   # run <tag> <bench args...>
@@ -16,9 +16,11 @@ run m2_general_glide --path 2
 run m1_glide --variant 1
 run m3_glide --variant 3
 run m4_glide --variant 4
+run m4_general_glide --variant 4 --path 2
 run m2_fused_s3 --ne 250 --nc 114
 run m2_fused_s5 --ne 250 --nc 150
 run m4_s5 --variant 4 --ne 250 --nc 150
+run m4_general_s5 --variant 4 --ne 250 --nc 150 --path 2
 run m2_stress --ne 1024 --nc 512 --batch 32
 run m4_stress --variant 4 --ne 1024 --nc 512 --batch 32
 cd /tmp && export TMPDIR=/tmp
