@@ -87,6 +87,14 @@ __device__ __forceinline__ float wsum(float v) {
   v += dppf<0xB1>(v);    // quad_perm        lane ^ 1
   return v;
 }
+// sum over a 16-lane DPP row; every lane of the row receives the total
+__device__ __forceinline__ float row_total16(float v) {
+  v += dppf<0x128>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0xB1>(v);
+  return v;
+}
 // wave sums of two values: lanes 0-31 end with a's total, lanes 32-63 with b's
 __device__ __forceinline__ float wsum2(float a, float b) {
   swap32(a, b);
@@ -146,6 +154,50 @@ __device__ __forceinline__ void wave_sums20(const float (&v)[20], const int lane
   cnt = up ? cnt - 1 : (cnt < 1 ? cnt : 1);
   w5 += dppf<0xB1>(w5);
   if (!(lane & 1) && cnt >= 1) store(base, w5);
+}
+
+// Sums of the 20 values v[k] over each 32-lane half of a wave (lanes 0-31 and 32-63 kept
+// apart) by the same transposed butterfly: a permlane16 swap across the half's two DPP
+// rows, then DPP inside a row (row_ror:8, row_half_mirror, quad_perm ^2, ^1).
+// store(half, k, total) runs on one lane per half and value.
+template <class F>
+__device__ __forceinline__ void half_sums20(const float (&v)[20], const int lane, F store) {
+  float w1[10], w2[5], w3[3], w4[2];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {                          // 20 -> 10 | 10 (lane bit 4)
+    float x = v[i], y = v[i + 10];
+    swap16(x, y);
+    w1[i] = x + y;
+  }
+  int base = (lane & 16) ? 10 : 0, cnt;
+  bool up = lane & 8;                                     // 10 -> 5 | 5
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float a = w1[i], b = w1[i + 5];
+    w2[i] = (up ? b : a) + dppf<0x128>(up ? a : b);
+  }
+  base += up ? 5 : 0;
+  up = lane & 4;                                          // 5 -> 3 | 2
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float a = w2[i], b = i + 3 < 5 ? w2[i + 3] : 0.f;
+    w3[i] = (up ? b : a) + dppf<0x141>(up ? a : b);
+  }
+  base += up ? 3 : 0;
+  cnt = up ? 2 : 3;
+  up = lane & 2;                                          // 3 -> 2 | 1  (2 -> 2 | 0)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float a = w3[i], b = i + 2 < 3 ? w3[i + 2] : 0.f;
+    w4[i] = (up ? b : a) + dppf<0x4E>(up ? a : b);
+  }
+  base += up ? 2 : 0;
+  cnt = up ? cnt - 2 : (cnt < 2 ? cnt : 2);
+  up = lane & 1;                                          // 2 -> 1 | 1
+  const float w5 = (up ? w4[1] : w4[0]) + dppf<0xB1>(up ? w4[0] : w4[1]);
+  base += up ? 1 : 0;
+  cnt = up ? cnt - 1 : (cnt < 1 ? cnt : 1);
+  if (cnt >= 1) store(lane >> 5, base, w5);
 }
 
 __device__ __forceinline__ unsigned long long qfix(float v) {
@@ -744,22 +796,32 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ee_fwd  grid (te, B), dynamic LDS u64 bins[Nc][2]
+// kw_ee_fwd  grid (ceil(Ne / TF), B), 8 waves
 //   model_4: e'_ij = softmax(U2'^T relu(P1'^T [1-a, a, eff_ij] + p1) + p2) replaces the
 //   one-hot E_edge in B_2 (model_4.py:95-97), and marshalling_B2 bins B_2 by the index
 //   file's hunk maps: n_c[2+m] += e'_r[m] for c in {hid[i'], hid[j']} of every relation
 //   r < n(n-1) on the n-grid (utils2.py:121-137).  Relations outside that range feed
-//   nothing, so only they are evaluated.  Lanes walk index rows i' (one per lane), each
-//   wave a quarter of the j' range; relation r -> entity pair (i, j) on the Ne-grid is
-//   advanced incrementally.  Source bins: per-lane sums; target bins: wave sums, both
-//   added to the block's LDS bins in 2^-32 fixed point (integer adds: order-free), which
-//   go out as one partial row per tile.
+//   nothing, so only they are evaluated.  The two-class softmax is a sigmoid of the logit
+//   difference: e = exp(-delta) = 2^delta' (prescaled D_EECQ / D_EEBQ), p1 = 1 / (1 + e),
+//   p0 = e p1; the weight constants are wave-uniform scalar loads.
+//   A block takes TF = 32 index rows i'; each half of a wave holds all 32 (one per lane) and
+//   walks its own sixteenth of the j' range, so a 200-row commit fills 7 blocks (224 lane
+//   rows) instead of 4 x 64.  Relation r -> entity pair (i, j) on the Ne-grid is advanced
+//   incrementally.  kappa = rho_i + (gam_j + a d): rho, gam and gam + d are LDS tables
+//   (Ne <= EE_TAB_LDS_MAX; else read from HBM, the same sums).  Source bins: per-lane sums;
+//   target bins: one 32-lane sum per half-wave and step into tsum[j'], binned after the
+//   loop.  Both go to the block's LDS bins in 2^-32 fixed point (integer adds: order-free),
+//   which leave as one partial row per tile.
 // ---------------------------------------------------------------------------------
-constexpr int EE_GAM_LDS_MAX = 800;   // Ne up to which the commit's gam table sits in LDS
-#ifndef EE_ABL          // diagnostic ablation builds only (tools/gpu_eeabl.sh); 0 in the engine
-#define EE_ABL 0
-#endif
+constexpr int TF = 32;                // index rows per kw_ee_fwd block
+constexpr int EE_TAB_LDS_MAX = 400;   // Ne up to which rho, gam, gam + d sit in LDS
+__host__ __device__ inline int ee_fwd_tiles(int Ne) { return (Ne + TF - 1) / TF; }
+__host__ __device__ inline size_t ee_fwd_lds(int Ne, int Nc) {
+  const size_t head = (size_t)((2 * Nc + 1) & ~1) * 8 + (size_t)((2 * Ne + 3) & ~3) * 4;
+  return head + (Ne <= EE_TAB_LDS_MAX ? (size_t)3 * Ne * H * 4 : 0);
+}
 
+template <bool LDS>
 __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                  const int32_t* __restrict__ hidg,
                                                  const int32_t* __restrict__ nleng,
@@ -769,42 +831,52 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
                                                  const float* __restrict__ gmm,
                                                  unsigned long long* __restrict__ ncpart) {
 #pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) unsigned long long bins[];   // [Nc][2] | gam
-  const int b = blockIdx.y, t0 = blockIdx.x * TN;
-  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  (void)W;
+  (void)o;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long bins[];   // [Nc][2] | ...
+  float* tsum = reinterpret_cast<float*>(bins + ((2 * Nc + 1) & ~1));         // [Ne][2]
+  float* rl = tsum + ((2 * Ne + 3) & ~3);                                     // rho [Ne][H]
+  float* gl = rl + Ne * H;                                                    // gam
+  float* gdl = gl + Ne * H;                                                   // gam + d
+  const int b = blockIdx.y, t0 = blockIdx.x * TF;
+  const int t = threadIdx.x, lane = t & 63, wv = uni(t >> 6), half = lane >> 5;
   unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  for (int c = threadIdx.x; c < 2 * Nc; c += NTP) bins[c] = 0ull;
+  for (int c = t; c < 2 * Nc; c += NTP) bins[c] = 0ull;
   if (n < 2 || t0 >= n) {         // block-uniform: this tile holds no index row
-    for (int c = threadIdx.x; c < 2 * Nc; c += NTP) outp[c] = 0ull;
+    for (int c = t; c < 2 * Nc; c += NTP) outp[c] = 0ull;
     return;
   }
+  const float* rb = rho + (size_t)b * Ne * H;
   const float* gb = gmm + (size_t)b * Ne * H;
-  const bool gl = Ne <= EE_GAM_LDS_MAX;
-  float* gs = reinterpret_cast<float*>(bins + ((2 * Nc + 1) & ~1));
-  if (gl) stage_rows(gs, gb, 0, Ne);
-  const float* gt = gl ? gs : gb;
+  for (int e = t; e < 2 * n; e += NTP) tsum[e] = 0.f;
+  if constexpr (LDS) {
+    stage_rows(rl, rb, 0, Ne);
+    for (int e = t; e < Ne * H; e += NTP) {
+      const float g = gb[e];
+      gl[e] = g;
+      gdl[e] = g + D[D_EED + e % H];
+    }
+  }
   __syncthreads();
   const int WE = (Ne + 31) >> 5;
-  const int32_t* hid = hidg + (size_t)b * Ne;
-  const int ip = t0 + lane;
+  const int ip = t0 + (lane & 31);
   const bool live = ip < n;
   const int ipc = live ? ip : 0;
-  const int jlo = (n * wv) / NWP, jhi = (n * (wv + 1)) / NWP;
+  const int part = 2 * wv + half, NPART = 2 * NWP;
+  const int jlo = (n * part) / NPART, jhi = (n * (part + 1)) / NPART;
+  const int trips = (n + NPART - 1) / NPART;   // >= every part's length: both halves step
   const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
   int ei = r0 / (Ne - 1), ejj = r0 - ei * (Ne - 1);
-  const float* rb = rho + (size_t)b * Ne * H;
-  f2 rh[H2], dl[H2], u2[H];
+  f2 rh[H2];
+  int cur = -1;
+  if constexpr (!LDS) {
 #pragma unroll
-  for (int kk = 0; kk < H2; ++kk) {
-    rh[kk] = ld2(rb + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
-    dl[kk] = ld2(D + D_EED + 2 * kk);
+    for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
+    cur = ei;
   }
-#pragma unroll
-  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.EC_W2 + 2 * k);
-  int cur = ei;
-  const f2 bb = ld2(W + o.EC_B2);
+  const float bq = D[D_EEBQ];
   float s0 = 0.f, s1 = 0.f;
   // class-bit words: the lane's relations walk the a-bit rows in order, so the word index
   // ei * WE + (j >> 5) grows by at most one per relation; the next word is prefetched
@@ -814,15 +886,18 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   int widx = (ei < Ne ? ei : Ne - 1) * WE + ((ejj + (ejj >= ei ? 1 : 0)) >> 5);
   widx = widx < wlast ? widx : wlast;
   uint32_t wcur = ab[widx], wnxt = ab[widx + 1 < wlast ? widx + 1 : wlast];
-  for (int jp = jlo; jp < jhi; ++jp) {
-    const bool valid = live && jp != ip;
+  for (int it = 0; it < trips; ++it) {
+    const int jp = jlo + it;
+    const bool valid = live && jp < jhi && jp != ip;
     float p0 = 0.f, p1 = 0.f;
     if (valid) {
       const int ej = ejj + (ejj >= ei ? 1 : 0);
-      if (ei != cur && !(EE_ABL & 16)) {
+      if constexpr (!LDS) {
+        if (ei != cur) {
 #pragma unroll
-        for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + ei * H + 2 * kk);
-        cur = ei;
+          for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + ei * H + 2 * kk);
+          cur = ei;
+        }
       }
       const int nidx = ei * WE + (ej >> 5);
       if (nidx != widx) {
@@ -830,45 +905,63 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
         widx = nidx;
         wnxt = ab[nidx + 1 < wlast ? nidx + 1 : wlast];
       }
-      const float af = (EE_ABL & 8) ? 0.f : (((wcur >> (ej & 31)) & 1u) ? 1.f : 0.f);
-      const f2 a2 = {af, af};
-      const float4* g4 = reinterpret_cast<const float4*>(gt + (size_t)ej * H);
-      f2 zz = bb;
+      const bool a1 = (wcur >> (ej & 31)) & 1u;
+      f2 dz = {bq, 0.f}, dzb = {0.f, 0.f};   // two chains: the fma latency overlaps
+      if constexpr (LDS) {
+        const float4* r4 = reinterpret_cast<const float4*>(rl + ei * H);
+        const float4* g4 = reinterpret_cast<const float4*>((a1 ? gdl : gl) + ej * H);
 #pragma unroll
-      for (int v = 0; v < H / 4; ++v) {   // rho_i + gam_j (kw_ee_clsb forms the same sum)
-        const float4 q = g4[v];
-        const f2 ka = relu2(fma2(a2, dl[2 * v], rh[2 * v] + (f2){q.x, q.y}));
-        const f2 kb = relu2(fma2(a2, dl[2 * v + 1], rh[2 * v + 1] + (f2){q.z, q.w}));
-        zz = fma2((f2){ka.x, ka.x}, u2[4 * v], zz);
-        zz = fma2((f2){ka.y, ka.y}, u2[4 * v + 1], zz);
-        zz = fma2((f2){kb.x, kb.x}, u2[4 * v + 2], zz);
-        zz = fma2((f2){kb.y, kb.y}, u2[4 * v + 3], zz);
+        for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + (gam_j + a d), as kw_ee_clsb
+          const float4 q = r4[v], g = g4[v];
+          const f2 ka = relu2((f2){q.x, q.y} + (f2){g.x, g.y});
+          const f2 kb = relu2((f2){q.z, q.w} + (f2){g.z, g.w});
+          dz = fma2(ka, ld2(D + D_EECQ + 4 * v), dz);
+          dzb = fma2(kb, ld2(D + D_EECQ + 4 * v + 2), dzb);
+        }
+      } else {
+        const float af = a1 ? 1.f : 0.f;
+        const f2 a2 = {af, af};
+        const float4* g4 = reinterpret_cast<const float4*>(gb + (size_t)ej * H);
+#pragma unroll
+        for (int v = 0; v < H / 4; ++v) {
+          const float4 g = g4[v];
+          const f2 ka = relu2(rh[2 * v] + fma2(a2, ld2(D + D_EED + 4 * v), (f2){g.x, g.y}));
+          const f2 kb = relu2(rh[2 * v + 1] + fma2(a2, ld2(D + D_EED + 4 * v + 2), (f2){g.z, g.w}));
+          dz = fma2(ka, ld2(D + D_EECQ + 4 * v), dz);
+          dzb = fma2(kb, ld2(D + D_EECQ + 4 * v + 2), dzb);
+        }
       }
-      const float mx = fmaxf(zz.x, zz.y);
-      const float e0 = __expf(zz.x - mx), e1 = __expf(zz.y - mx);
-      const float inv = __builtin_amdgcn_rcpf(e0 + e1);   // e0 + e1 in [1, 2]: 1-ulp rcp
-      p0 = e0 * inv;
-      p1 = e1 * inv;
+      dz += dzb;
+      const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
+      p1 = __builtin_amdgcn_rcpf(1.f + e);
+      p0 = e * p1;
       if (++ejj == Ne - 1) { ejj = 0; ++ei; }
     }
     s0 += p0;
     s1 += p1;
-    const float w01 = wsum2(p0, p1);                 // lane 0: sum p0, lane 32: sum p1
-    const int ht = hid[jp];
-    if (!(EE_ABL & 32) && (lane & 31) == 0 && ht >= 0 && ht < Nc)
-      atomicAdd(&bins[2 * ht + (lane >> 5)], qfix(w01));
+    // 32-lane sums of (p0, p1) per half: one permlane16 swap, then a 16-lane DPP reduction;
+    // DPP row q of the wave ends with half q >> 1's sum of p_(q & 1)
+    float x = p0, y = p1;
+    swap16(x, y);
+    const float v = row_total16(x + y);
+    if ((lane & 15) == 0 && jp < jhi) tsum[2 * jp + ((lane >> 4) & 1)] = v;
   }
-  if (live) {
-    const int hs = hid[ip];
+  if (live) {                          // source bins: the lane's row i'
+    const int hs = hidg[(size_t)b * Ne + ip];
     if (hs >= 0 && hs < Nc) {
       atomicAdd(&bins[2 * hs], qfix(s0));
       atomicAdd(&bins[2 * hs + 1], qfix(s1));
     }
   }
   __syncthreads();
-  // per-tile partial bins, summed in tile order by kw_cross_fwd (no global atomics: the
-  // L2s of the 8 XCDs are not coherent for device-scope atomics on coarse-grained memory)
-  for (int c = threadIdx.x; c < 2 * Nc; c += NTP) outp[c] = bins[c];
+  for (int e = t; e < 2 * n; e += NTP) {   // target bins: column j' of the tile's rows
+    const int ht = hidg[(size_t)b * Ne + (e >> 1)];
+    if (ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (e & 1)], qfix(tsum[e]));
+  }
+  __syncthreads();
+  // per-tile partial bins, summed in tile order by kw_cross_fwd / kw_ee_bins (no global
+  // atomics: the L2s of the 8 XCDs are not coherent for device-scope atomics)
+  for (int c = t; c < 2 * Nc; c += NTP) outp[c] = bins[c];
 }
 
 // ---------------------------------------------------------------------------------
@@ -1791,22 +1884,30 @@ __device__ __forceinline__ void divmod_sel(int r, int d, float inv, int& q, int&
   rem = lo ? r0 + d : (hi ? r0 - d : r0);
 }
 
+constexpr int TB = 32;   // kw_ee_clsb: columns per block (a wave's two halves take two rows)
+__host__ __device__ inline int ee_bwd_tiles(int Ne) { return (Ne + TB - 1) / TB; }
+
 __device__ __forceinline__ void ee_clsb_rows(
     const int lo, const int hi, const int c0, const float* os_, const uint32_t* abl,
     const int Ne, const int jn, const bool live, const int nrel, const int dn1, const float inv,
-    const bool aligned, const float* Eq, const float Ej, const float4* gl,
+    const bool aligned, const float* Eq, const float Ej, const float4* gl, const float4* gdl,
     const float* __restrict__ D, float* rowp, f2 (&acc)[H2], f2 (&ag)[H2], float& sdl,
     float& zr, int& kst) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
   const float bq = D[D_EEBQ];
+  const int trips = (hi - lo + 1) >> 1;
   int wi = -1;
   uint32_t word = 0;
-  for (int m = lo; m < hi; ++m) {
-    if ((m >> 5) != wi) { wi = m >> 5; word = abl[wi * TN]; }
-    const float af = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
+  for (int it = 0; it < trips; ++it) {
+    const int mr = lo + 2 * it + half;           // the half's row
+    const bool inr = mr < hi;
+    const int m = inr ? mr : lo;                 // past the share: a staged row, d1 = 0
+    if ((m >> 5) != wi) { wi = m >> 5; word = abl[wi * TB]; }
+    const bool a1 = (word >> (m & 31)) & 1u;
+    const float af = a1 ? 1.f : 0.f;
     const f2 a2 = {af, af};
     const int r = m * (Ne - 1) + jn - (jn > m ? 1 : 0);
-    const bool valid = live && m != jn && r < nrel;
+    const bool valid = live && inr && m != jn && r < nrel;
     float dp;
     if (aligned) {                     // n = Ne: (i', j') = (i, j)   (block-uniform branch)
       dp = Eq[m] + Ej;
@@ -1817,19 +1918,24 @@ __device__ __forceinline__ void ee_clsb_rows(
     }
     const float* orow = os_ + (m - c0) * H;
     const float4* o4 = reinterpret_cast<const float4*>(orow);
+    const float4* g4 = a1 ? gdl : gl;            // gam_j + a d: the LDS table by address
     f2 pre[H2], st[H2];
 #pragma unroll
-    for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + gam_j + a d: the sum kw_ee_fwd forms
-      const float4 q = o4[v], g = gl[v * TN];
-      pre[2 * v] = fma2(a2, ld2(D + D_EED + 4 * v), (f2){g.x, g.y} + (f2){q.x, q.y});
-      pre[2 * v + 1] = fma2(a2, ld2(D + D_EED + 4 * v + 2), (f2){g.z, g.w} + (f2){q.z, q.w});
+    for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + (gam_j + a d), as kw_ee_fwd
+      const float4 q = o4[v], g = g4[v * TB];
+      pre[2 * v] = (f2){q.x, q.y} + (f2){g.x, g.y};
+      pre[2 * v + 1] = (f2){q.z, q.w} + (f2){g.z, g.w};
     }
-    f2 dz = {bq, 0.f};
+    f2 dz = {bq, 0.f}, dzb = {0.f, 0.f};   // two chains: the fma latency overlaps
 #pragma unroll
     for (int kk = 0; kk < H2; ++kk) {  // relu(kappa) = kappa [kappa > 0]
       st[kk] = step2(pre[kk]);
-      dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
+      if (kk & 1)
+        dzb = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dzb);
+      else
+        dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
     }
+    dz += dzb;
     const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
     const float p1 = __builtin_amdgcn_rcpf(1.f + e);
     const float d1 = valid ? (e * p1) * (p1 * dp) : 0.f;
@@ -1844,12 +1950,12 @@ __device__ __forceinline__ void ee_clsb_rows(
       sv[2 * kk] = sd.x;
       sv[2 * kk + 1] = sd.y;
     }
-    // the row's sums over the tile: this tile's drho partial (without c: kw_ee_nodeb scales
-    // the summed partials) and, for the classifier's second layer,
-    // sum_j relu(kappa) dz1 = sum_j kappa s dz1: its rho part rho_i . (row sum) here, the gam
-    // and a d parts from the column sums after the loop
-    wave_sums20(sv, lane, [&](int k, float x) {
-      rowp[(size_t)m * H + k] = x;
+    // the half's row sums over the tile's 32 columns: this tile's drho partial (without c:
+    // kw_ee_nodeb scales the summed partials) and, for the classifier's second layer,
+    // sum_j relu(kappa) dz1 = sum_j kappa s dz1: its rho part rho_i . (row sum) here, the
+    // gam + a d part from the column sums after the loop
+    half_sums20(sv, lane, [&](int, int k, float x) {
+      if (inr) rowp[(size_t)m * H + k] = x;
       zr = fmaf(orow[k], x, zr);
       kst = k;
     });
@@ -1865,16 +1971,18 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma clang fp contract(off)
   (void)abits;
   (void)W;
-  extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][64]
+  (void)o;
+  extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][TB]
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
-  __shared__ float buf[NWP * TN * HP];
-  __shared__ float res[TN * HP];
+  __shared__ float buf[NWP * 2 * TB * HP];
+  __shared__ float res[TB * HP];
   __shared__ float red[NWP * 21];
   __shared__ float tot[21];
   __shared__ float cl[H];
-  __shared__ float zred[NWP * H];
-  __shared__ float4 gl4[(H / 4) * TN];            // the lane columns' gam rows, [v][lane]
-  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x;
+  __shared__ float zred[NWP * 2 * H];
+  __shared__ float4 gl4[(H / 4) * TB];            // the columns' gam rows, [v][column]
+  __shared__ float4 gdl4[(H / 4) * TB];           // gam + d
+  const int b = blockIdx.y, t0 = blockIdx.x * TB, te = gridDim.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
@@ -1888,16 +1996,20 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     const float* d = dn + ((size_t)b * Nc + (h >= 0 && h < Nc ? h : 0)) * 4;
     Eq[e] = (h >= 0 && h < Nc) ? d[3] - d[2] : 0.f;
   }
-  for (int e = t; e < WE * TN; e += NTP) {        // a^T rows of the tile's columns: bit m = a[m][j]
-    const int w = e / TN, l = e - w * TN, node = t0 + l < Ne ? t0 + l : Ne - 1;
+  for (int e = t; e < WE * TB; e += NTP) {        // a^T rows of the tile's columns: bit m = a[m][j]
+    const int w = e / TB, l = e - w * TB, node = t0 + l < Ne ? t0 + l : Ne - 1;
     abl[e] = aT[((size_t)b * Ne + node) * WE + w];
   }
   if (t < H) cl[t] = D[D_EEC + t];
-  for (int e = t; e < (H / 4) * TN; e += NTP) {   // [v][lane]: conflict-free 16-B reads
-    const int v = e / TN, l = e - v * TN, node = t0 + l < Ne ? t0 + l : Ne - 1;
-    gl4[e] = reinterpret_cast<const float4*>(gmm + ((size_t)b * Ne + node) * H)[v];
+  for (int e = t; e < (H / 4) * TB; e += NTP) {   // [v][column]: conflict-free 16-B reads
+    const int v = e / TB, l = e - v * TB, node = t0 + l < Ne ? t0 + l : Ne - 1;
+    const float4 g = reinterpret_cast<const float4*>(gmm + ((size_t)b * Ne + node) * H)[v];
+    const float4 d = reinterpret_cast<const float4*>(D + D_EED)[v];
+    gl4[e] = g;
+    gdl4[e] = make_float4(g.x + d.x, g.y + d.y, g.z + d.z, g.w + d.w);
   }
-  const int jn = t0 + lane, jc = jn < Ne ? jn : Ne - 1;
+  const int col = lane & (TB - 1);
+  const int jn = t0 + col, jc = jn < Ne ? jn : Ne - 1;
   const bool live = jn < Ne;
   f2 acc[H2], ag[H2];
 #pragma unroll
@@ -1914,7 +2026,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   const float* rb = rho + (size_t)b * Ne * H;
   const float inv = 1.f / (float)dn1;
   const bool aligned = n == Ne;
-  __syncthreads();                                 // Eq, abl, cl, gl4
+  __syncthreads();                                 // Eq, abl, cl, gl4, gdl4
   const float Ej = Eq[jc];
   for (int c0 = 0; c0 < rows; c0 += CHM) {
     const int c1 = c0 + CHM < rows ? c0 + CHM : rows;
@@ -1923,15 +2035,29 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     int lo, hi;
     wave_share(c0, c1, lo, hi);
-    ee_clsb_rows(lo, hi, c0, os_, abl + lane, Ne, jn, live, nrel, dn1, inv, aligned, Eq, Ej,
-                 gl4 + lane, D, rowp, acc, ag, sdl, zr, kst);
+    ee_clsb_rows(lo, hi, c0, os_, abl + col, Ne, jn, live, nrel, dn1, inv, aligned, Eq, Ej,
+                 gl4 + col, gdl4 + col, D, rowp, acc, ag, sdl, zr, kst);
   }
-  if (lane < H) zred[wv * H + lane] = 0.f;
+  if (lane < 2 * H) zred[wv * 2 * H + lane] = 0.f;
   __syncthreads();
-  if (kst >= 0) zred[wv * H + kst] = zr;           // one storing lane per (wave, unit)
-  combine8(acc, buf, res);                         // sum over the waves' row shares (barriers)
+  if (kst >= 0) zred[(wv * 2 + (lane >> 5)) * H + kst] = zr;   // one storing lane per (half, unit)
+  // column sums over the waves and the two halves (fixed order) -> res[TB][HP]
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    buf[(wv * 2 * TB + lane) * HP + 2 * kk] = acc[kk].x;
+    buf[(wv * 2 * TB + lane) * HP + 2 * kk + 1] = acc[kk].y;
+  }
+  __syncthreads();
+  for (int e = t; e < TB * H; e += NTP) {
+    const int nn = e / H, k = e - nn * H;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * NWP; ++q) sum += buf[(q * TB + nn) * HP + k];   // row q*TB+nn: wave q/2, half q&1
+    res[nn * HP + k] = sum;
+  }
+  __syncthreads();
   float* dout = dgam + (size_t)b * Ne * H;
-  for (int e = t; e < TN * H; e += NTP) {
+  for (int e = t; e < TB * H; e += NTP) {
     const int nn = e / H, k = e - nn * H;
     if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = res[nn * HP + k] * cl[k];
   }
@@ -1949,14 +2075,14 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     // (kappa = rho + gam + a d; R, C the row / column sums of s dz1)
     float sc = 0.f, zg = 0.f;
     const float* glf = reinterpret_cast<const float*>(gl4);
-    for (int nn = 0; nn < TN; ++nn) {
+    for (int nn = 0; nn < TB; ++nn) {
       if (t0 + nn >= Ne) break;
       const float cs = res[nn * HP + t];
       sc += cs;
-      zg = fmaf(glf[((t >> 2) * TN + nn) * 4 + (t & 3)], cs, zg);
+      zg = fmaf(glf[((t >> 2) * TB + nn) * 4 + (t & 3)], cs, zg);
     }
     float zw = 0.f;
-    for (int w = 0; w < NWP; ++w) zw += zred[w * H + t];
+    for (int q = 0; q < 2 * NWP; ++q) zw += zred[q * H + t];
     const float zk = (zw + zg) + D[D_EED + t] * tot[t];
     const float sg_ = sc * cl[t];                    // sum of g over the tile
     const float a1 = tot[t] * cl[t];
@@ -1981,7 +2107,8 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
 // dQ2 = sum R1 (x) dR + C1 (x) dC, dq2 = (Ne-1) sum (dR + dC)
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void kw_ee_nodeb(
-    const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, const float* __restrict__ R1,
+    const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int np,
+    const float* __restrict__ R1,
     const float* __restrict__ C1, const float* __restrict__ Rn, const float* __restrict__ Cn,
     const float* __restrict__ drho, const float* __restrict__ dgam, float* __restrict__ phi,
     float* __restrict__ psi, float* __restrict__ part, Segs sg) {
@@ -1996,7 +2123,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
   stage_w(Wl + 400, W + o.EE_W2, 400);
   // staging: every element's loads issued before the first use (NE_IT elements per thread;
-  // the te row partials of drho four tiles at a time, summed in tile order)
+  // the np row partials of drho (kw_ee_clsb's column tiles) eight at a time, in tile order)
   constexpr int NE_IT = TN * H / NT;
   static_assert(TN * H % NT == 0, "kw_ee_nodeb staging");
   float dr[NE_IT];
@@ -2012,26 +2139,21 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     Ct[n * HP + k] = in ? Cn[base + e] : 0.f;
   }
   {
-    const float* src = drho + ((size_t)b * te * Ne + t0) * H + t;
+    const float* src = drho + ((size_t)b * np * Ne + t0) * H + t;
     const size_t sq = (size_t)Ne * H;
     const int nin = (Ne - t0) * H;                    // elements e < nin are in range
-    int q = 0;
-    for (; q + 4 <= te; q += 4) {
-      float v[NE_IT][4];
+    for (int q = 0; q < np; q += 8) {                 // 8 tiles' loads in flight, summed in order
+      float v[NE_IT][8];
 #pragma unroll
       for (int it = 0; it < NE_IT; ++it)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          v[it][u] = (t + it * NT < nin) ? src[(q + u) * sq + it * NT] : 0.f;
+        for (int u = 0; u < 8; ++u)
+          v[it][u] = (q + u < np && t + it * NT < nin) ? src[(q + u) * sq + it * NT] : 0.f;
 #pragma unroll
       for (int it = 0; it < NE_IT; ++it)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dr[it] += v[it][u];
+        for (int u = 0; u < 8; ++u) dr[it] += v[it][u];
     }
-    for (; q < te; ++q)
-#pragma unroll
-      for (int it = 0; it < NE_IT; ++it)
-        if (t + it * NT < nin) dr[it] += src[q * sq + it * NT];
   }
 #pragma unroll
   for (int it = 0; it < NE_IT; ++it) {
@@ -2215,7 +2337,7 @@ __global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
 struct WideWork {
   size_t xp, ov, P, Eb, hE, rhoE;                 // entity stage   [B][Ne](*H)
   size_t R1, C1, Rn, Cn, rho, gmm, drho, dgam, phi, psi;   // EE     [B][Ne][H]
-  size_t ncpart;                                  // u64 [B][te][Nc][2] EE partial bins
+  size_t ncpart;                                  // u64 [B][tef][Nc][2] EE partial bins
   size_t nvec, alpha, beta, G, Hh, sig, tau, Dsig, Dtau, dG, dH, Dal, Dbe, dn;   // hunk
   size_t gam;                                     // [B][Nc][Nc]
   size_t D;                                       // derived weights
@@ -2244,9 +2366,9 @@ WideWork wide_layout(const hdg_shape* s) {
   if (has_ee(v)) {
     w.R1 = take(NEH); w.C1 = take(NEH); w.Rn = take(NEH); w.Cn = take(NEH);
     w.rho = take(NEH); w.gmm = take(NEH); w.dgam = take(NEH);
-    w.drho = take(NEH * (size_t)((Ne + TN - 1) / TN));    // one partial per column tile
+    w.drho = take(NEH * (size_t)ee_bwd_tiles((int)Ne));    // one partial per kw_ee_clsb tile
     w.phi = take(NEH); w.psi = take(NEH);
-    w.ncpart = take(B * ((Ne + TN - 1) / TN) * Nc * 4);
+    w.ncpart = take(B * ee_fwd_tiles((int)Ne) * Nc * 4);
   }
   w.nvec = take(B * Nc * 4);
   w.alpha = take(NCH); w.beta = take(NCH); w.G = take(NCH); w.Hh = take(NCH);
@@ -2275,8 +2397,9 @@ WideWork wide_layout(const hdg_shape* s) {
     seg(SG_E1W1, o.E1_W1, 100, re);
   }
   if (has_ee(v)) {
-    seg(SG_ECW1A, o.EC_W1, 40, re);
-    seg(SG_ECB1, o.EC_B1, 62, re);
+    const int rb = (int)B * ee_bwd_tiles((int)Ne);      // kw_ee_clsb blocks
+    seg(SG_ECW1A, o.EC_W1, 40, rb);
+    seg(SG_ECB1, o.EC_B1, 62, rb);
     seg(SG_ECW1E, o.EC_W1 + 40, 400, re);
     seg(SG_EEW2, o.EE_W2, 420, re);
     seg(SG_EEW11, o.EE_W11, 80, re);
@@ -2302,10 +2425,28 @@ int set_wide_attrs() {
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<false>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     attr_set = true;
   }
+  return 0;
+}
+
+// kw_ee_fwd over the batch: LDS tables up to EE_TAB_LDS_MAX nodes, HBM reads beyond
+int launch_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, const float* D,
+                  const float* rho, const float* gmm, unsigned long long* ncpart, hipStream_t st) {
+  const int B = s->batch, Ne = s->ne, Nc = s->nc;
+  const Off o = param_offsets(s->variant);
+  const dim3 grid(ee_fwd_tiles(Ne), B);
+  if (Ne <= EE_TAB_LDS_MAX)
+    hipLaunchKernelGGL(kw_ee_fwd<true>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+  else
+    hipLaunchKernelGGL(kw_ee_fwd<false>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+  WTRY(hipGetLastError());
   return 0;
 }
 
@@ -2340,13 +2481,9 @@ int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
                      F(w.Cn), F(w.rho), F(w.gmm));
   WTRY(hipGetLastError());
   unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
-  const size_t elds = (size_t)((2 * Nc + 1) & ~1) * 8 +
-                      (Ne <= EE_GAM_LDS_MAX ? (size_t)Ne * H * 4 : 0);
-  hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NTP), elds, st, bt->abits, bt->hid, bt->nlen,
-                     params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), ncpart);
-  WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_ee_bins, dim3((2 * Nc + NT - 1) / NT, B), dim3(NT), 0, st, ncpart, te, Nc,
-                     ncls);
+  if (int rc = launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st)) return rc;
+  hipLaunchKernelGGL(kw_ee_bins, dim3((2 * Nc + NT - 1) / NT, B), dim3(NT), 0, st, ncpart,
+                     ee_fwd_tiles(Ne), Nc, ncls);
   WTRY(hipGetLastError());
   return 0;
 }
@@ -2362,12 +2499,13 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const int te = (Ne + TN - 1) / TN;
   float* part = ws;
-  const size_t lds = (size_t)(Ne + TN * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-  hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
+  const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
+  hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
                      bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                      F(w.dgam), part, w.segs);
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne, F(w.R1), F(w.C1),
+  hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
+                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1),
                      F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
@@ -2447,15 +2585,11 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
   if (ee) {
-    const size_t elds = (size_t)((2 * Nc + 1) & ~1) * 8 +
-                        (Ne <= EE_GAM_LDS_MAX ? (size_t)Ne * H * 4 : 0);
-    hipLaunchKernelGGL(kw_ee_fwd, dim3(te, B), dim3(NTP), elds, st, bt->abits, bt->hid,
-                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), ncpart);
-    WTRY(hipGetLastError());
+    if (int rc = launch_ee_fwd(s, bt, params, D, F(w.rho), F(w.gmm), ncpart, st)) return rc;
   }
   // ---- hunk side ----
   hipLaunchKernelGGL(kw_cross_fwd, dim3((Nc + NW - 1) / NW, B), dim3(NT), 0, st, prep,
-                     ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncpart, te, F(w.nvec), F(w.alpha),
+                     ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncpart, ee_fwd_tiles(Ne), F(w.nvec), F(w.alpha),
                      F(w.beta));
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
@@ -2503,12 +2637,13 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     WTRY(hipGetLastError());
   }
   if (ee) {
-    const size_t lds = (size_t)(Ne + TN * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-    hipLaunchKernelGGL(kw_ee_clsb, dim3(te, B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
+    const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
                        bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                        F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne, F(w.R1), F(w.C1),
+    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
+                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1),
                        F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
