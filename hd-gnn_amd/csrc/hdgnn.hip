@@ -1445,12 +1445,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     unsigned long long* __restrict__ stamps, float* __restrict__ aux,
     const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch,
     uint32_t* __restrict__ status, const uint32_t xfault, const int ee_ins,
-    const float* __restrict__ ncls, float* __restrict__ dnout) {
+    const unsigned long long* __restrict__ ncpart, const int ncpt, float* __restrict__ dnout) {
   // model_4 on this kernel (hdg hybrid path): ee_ins = the entity-edge parameter block's
   // length in the flat vector (the model_2-shaped parameters after it are staged at their
-  // model_2 offsets); ncls [B][Nc][2] = the entity-edge aggregate n_c[2:4] replacing the
-  // static class counts (model_4.py:95-97); dnout [B][Nc][4] receives dn for the
-  // entity-edge backward.  model_2: 0, nullptr, nullptr.
+  // model_2 offsets); ncpart [B][ncpt][Nc][2] = kw_ee_fwd's per-tile partial bins of the
+  // entity-edge aggregate n_c[2:4] (2^-32 fixed point), summed here in tile order, replacing
+  // the static class counts (model_4.py:95-97); dnout [B][Nc][4] receives dn for the
+  // entity-edge backward.  model_2: 0, nullptr, 0, nullptr.
   using namespace m2;
   constexpr int NC16 = 16 * SMAXC;
   constexpr int CRED = tile_cred_words<SMAXC, KK_MID>();
@@ -1785,10 +1786,18 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         }
       });
     }
-    const float* ncl = ncls ? ncls + (size_t)b * 2 * Nc : ncst;   // model_4: the EE aggregate
-    for (int c = t; c < Nc; c += NT_MID) {
-      nb[4 * c + 2] = ncl[2 * c];
-      nb[4 * c + 3] = ncl[2 * c + 1];
+    if (ncpart) {   // model_4: the EE aggregate, tile partials in tile order (as kw_cross_fwd)
+      const unsigned long long* pr = ncpart + (size_t)b * ncpt * 2 * Nc;
+      for (int e = t; e < 2 * Nc; e += NT_MID) {
+        unsigned long long a = 0ull;
+        for (int tl = 0; tl < ncpt; ++tl) a += pr[(size_t)tl * 2 * Nc + e];
+        nb[4 * (e >> 1) + 2 + (e & 1)] = (float)((double)a * (1.0 / 4294967296.0));
+      }
+    } else {
+      for (int c = t; c < Nc; c += NT_MID) {
+        nb[4 * c + 2] = ncst[2 * c];
+        nb[4 * c + 3] = ncst[2 * c + 1];
+      }
     }
     if constexpr (SPLIT) {
       for (int i = t; i < NE4; i += NT_MID) xsc[2 * Nc + i] = (i >= nlo && i < nhi) ? os[i] : 0.f;
@@ -2620,16 +2629,19 @@ __device__ __forceinline__ void put_count(float* __restrict__ out, const uint32_
   out[2] = 0.f;
 }
 
+// slots [p_begin, p_end) -> out[p - p_begin], those >= shift_at moved by shift (model_4 on
+// the fused path: the model_2-layout slots past the entity-edge block)
 __global__ __launch_bounds__(1024) void k_grad_reduce(const float* __restrict__ part, int B,
-                                                      int p_begin, int p_end,
-                                                      float* __restrict__ out) {
+                                                      int p_begin, int p_end, int shift_at,
+                                                      int shift, float* __restrict__ out) {
   __shared__ RedShared sh;
   const int p = p_begin + blockIdx.x * RED_P + (threadIdx.x & (RED_P - 1));
   uint32_t cnt;
   const float g = reduce_commits(part, B, p, p < p_end, sh, cnt);
   if (threadIdx.x >= RED_P || p >= p_end) return;
-  if (p == CNT_SLOT && p + 2 < p_end) put_count(out + (p - p_begin), cnt);
-  else if (p < CNT_SLOT || p > CNT_SLOT + 2) out[p - p_begin] = g;
+  float* o = out + (p - p_begin) + (p >= shift_at ? shift : 0);
+  if (p == CNT_SLOT && p + 2 < p_end) put_count(o, cnt);
+  else if (p < CNT_SLOT || p > CNT_SLOT + 2) o[0] = g;
 }
 
 // Single-process training step tail: the reduction above fused with TF1 Adam for the
@@ -3203,10 +3215,12 @@ StepOut step_out(const hdg_outputs* out) {
   return out ? StepOut{out->probs, out->logits, out->status} : StepOut{nullptr, nullptr, nullptr};
 }
 
-// model_4 hooks of the step kernel (k_commit_step's ee_ins / ncls / dnout); all zero for model_2
+// model_4 hooks of the step kernel (k_commit_step's ee_ins / ncpart / dnout); all zero for
+// model_2
 struct Hyb {
   int ins;
-  const float* ncls;
+  const unsigned long long* ncpart;
+  int ncpt;
   float* dnout;
 };
 
@@ -3224,7 +3238,7 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
                      ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, o.probs,
                      o.logits, s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow,
                      s->batch, (unsigned long long*)(ws + w.xch), o.status,
-                     SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncls, hy.dnout);
+                     SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncpart, hy.ncpt, hy.dnout);
   return hipGetLastError();
 }
 
@@ -3232,7 +3246,7 @@ template <bool TRAIN, bool STAMPS = false>
 hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* params, float* ws,
                          const Work& w, const StepOut& o, float ce_scale,
                          unsigned long long* stamps, hipStream_t st, bool split,
-                         const float* bpow = nullptr, const Hyb& hy = Hyb{0, nullptr, nullptr}) {
+                         const float* bpow = nullptr, const Hyb& hy = Hyb{0, nullptr, 0, nullptr}) {
 #define HDG_STEP(SM)                                                                              \
   return split ? launch_step<SM, TRAIN, STAMPS, true>(s, bt, params, ws, w, o, ce_scale, stamps, \
                                                       bpow, st, hy)                               \
@@ -3257,7 +3271,7 @@ float pair_count(const hdg_shape* s) {
 // classifier, their backward) with model_4's parameters, the entity-edge aggregate as
 // the class part of n_c and dn exported for the entity-edge backward.  model_4 is model_2
 // plus that stage (model_4.py:92-97): the two meet only at n_c[2:4] and dn_c[2:4].
-// prep = [fused prep | general prep]; workspace = [fused | general | ncls [B][Nc][2]].
+// prep = [fused prep | general prep]; workspace = [fused | general].
 bool is_hybrid(const hdg_shape* s, int path) { return path == HDG_PATH_FUSED && s->variant == 4; }
 
 size_t fused_prep_bytes(const hdg_shape* s) {
@@ -3265,14 +3279,13 @@ size_t fused_prep_bytes(const hdg_shape* s) {
 }
 
 struct HybWork {
-  size_t wide, ncls, total;   // float offsets
+  size_t wide, total;   // float offsets
 };
 HybWork hyb_layout(const hdg_shape* s) {
   HybWork h;
   auto up = [](size_t n) { return (n + 63) & ~(size_t)63; };
   h.wide = up(work_layout(s).total);
-  h.ncls = h.wide + up(hdg::wide_workspace_bytes(s) / 4);
-  h.total = h.ncls + up((size_t)s->batch * s->nc * 2);
+  h.total = h.wide + up(hdg::wide_workspace_bytes(s) / 4);
   return h;
 }
 
@@ -3287,28 +3300,30 @@ hdg_batch wide_half(const hdg_batch* bt, const hdg_shape* s) {
 // !train: forward only, CE sum -> *ce_sum.  events[0..2] as hdg_fwd_bwd_events.
 int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
                hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st,
-               void* const* events) {
+               void* const* events, const hdg::WideAdam* adam = nullptr) {
   const HybWork hw = hyb_layout(s);
   float* ws = (float*)workspace;
   float* wws = ws + hw.wide;
-  float* ncls = ws + hw.ncls;
   const hdg_batch bw = wide_half(bt, s);
   const int ins = hdg::param_offsets(4).H1_W1 - m2::H1_W1;   // the entity-edge block (1002)
   auto mark = [&](int k) -> hipError_t {
     return events ? hipEventRecord((hipEvent_t)events[k], st) : hipSuccess;
   };
   HIP_TRY(mark(0));
-  if (int rc = hdg::wide_ee_fwd(s, &bw, params, wws, ncls, st)) return rc;
+  if (int rc = hdg::wide_ee_fwd(s, &bw, params, wws, st,
+                                adam && train ? adam->state->beta_pow : nullptr))
+    return rc;
   const Work w = work_layout(s);
   const bool split = use_split(s);
   const float pairs = pair_count(s);
-  const Hyb hy{ins, ncls, train ? hdg::wide_dn(s, wws) : nullptr};
+  const Hyb hy{ins, hdg::wide_ncpart(s, wws), hdg::wide_ncpart_tiles(s),
+               train ? hdg::wide_dn(s, wws) : nullptr};
   if (!train) {
     HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, step_out(out), 0.f, nullptr, st, split,
                                  nullptr, hy));
     if (ce_sum) {
       hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part,
-                         part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);
+                         part_rows(s, split), m2::NP, m2::NP + 1, GRAD_LEN, 0, ce_sum);
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(mark(1));
@@ -3318,14 +3333,17 @@ int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, flo
   HIP_TRY(dispatch_step<true>(s, bt, params, ws, w, step_out(out), 10.f / pairs, nullptr, st,
                               split, nullptr, hy));
   const int R = part_rows(s, split);
-  // the fused rows: [0, H1_W1) in place, [H1_W1, GRAD_LEN) past the entity-edge block
-  hipLaunchKernelGGL(k_grad_reduce, dim3((m2::H1_W1 + RED_P - 1) / RED_P), dim3(1024), 0, st,
-                     ws + w.part, R, 0, m2::H1_W1, grad);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN - m2::H1_W1 + RED_P - 1) / RED_P), dim3(1024),
-                     0, st, ws + w.part, R, m2::H1_W1, GRAD_LEN, grad + m2::H1_W1 + ins);
-  HIP_TRY(hipGetLastError());
-  if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st)) return rc;
+  if (adam) {   // the fused rows are reduced inside the final reduce + Adam kernel
+    hdg::WideAdam ad = *adam;
+    ad.fused = hdg::FusedRows{ws + w.part, R, NPART, m2::H1_W1, ins, m2::NP};
+    if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st, &ad)) return rc;
+  } else {
+    // the fused rows: [0, H1_W1) in place, [H1_W1, GRAD_LEN) past the entity-edge block
+    hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
+                       ws + w.part, R, 0, GRAD_LEN, m2::H1_W1, ins, grad);
+    HIP_TRY(hipGetLastError());
+    if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st)) return rc;
+  }
   HIP_TRY(mark(1));
   HIP_TRY(mark(2));
   return 0;
@@ -3419,7 +3437,7 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
                               st, split));
   HIP_TRY(mark(1));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
-                     ws + w.part, part_rows(s, split), 0, GRAD_LEN, grad);
+                     ws + w.part, part_rows(s, split), 0, GRAD_LEN, GRAD_LEN, 0, grad);
   HIP_TRY(hipGetLastError());
   HIP_TRY(mark(2));
   return 0;
@@ -3469,11 +3487,12 @@ int hdg_train_step(const hdg_shape* s, const hdg_batch* bt, hdg_state* state, fl
   if (!grad || !workspace) return fail(HDG_EINVAL, "NULL grad/workspace");
   hipStream_t st = (hipStream_t)stream;
   if (path == HDG_PATH_GENERAL || is_hybrid(s, path)) {
-    const int rc = path == HDG_PATH_GENERAL
-        ? hdg::wide_run(s, bt, state->params, grad, out, nullptr, workspace, true, st)
-        : hybrid_run(s, bt, state->params, grad, out, nullptr, workspace, true, st, nullptr);
-    if (rc) return rc;
-    return hdg_adam_tf(s, state, grad, lr, out ? out->stats : nullptr, stream);
+    // TF Adam inside the final reduction (kw_reduce_adam): no separate k_adam_tf launch
+    const hdg::WideAdam adam{state, lr, 1.f / pair_count(s), out ? out->stats : nullptr, {}};
+    return path == HDG_PATH_GENERAL
+        ? hdg::wide_run(s, bt, state->params, grad, out, nullptr, workspace, true, st, &adam)
+        : hybrid_run(s, bt, state->params, grad, out, nullptr, workspace, true, st, nullptr,
+                     &adam);
   }
   // single process, fused path: k_commit_step (+ loss stats / Adam factor from block 0),
   // then the fused deterministic reduction + TF Adam; no all-reduce point in between
@@ -3507,7 +3526,7 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
   HIP_TRY(dispatch_step<false>(s, bt, params, ws, w, step_out(out), 0.f, nullptr, st, split));
   if (ce_sum) {
     hipLaunchKernelGGL(k_grad_reduce, dim3(1), dim3(1024), 0, st, ws + w.part,
-                       part_rows(s, split), m2::NP, m2::NP + 1, ce_sum);
+                       part_rows(s, split), m2::NP, m2::NP + 1, GRAD_LEN, 0, ce_sum);
     HIP_TRY(hipGetLastError());
   }
   return 0;

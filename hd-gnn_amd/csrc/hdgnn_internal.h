@@ -79,6 +79,21 @@ struct Off {
 Off param_offsets(int variant);   // NP = -1 for an unknown variant
 
 // general path (wide.hip)
+// A single-process training step's TF-Adam tail run inside the general path's final
+// reduction (kw_reduce_adam) instead of a separate k_adam_tf launch; state updated in place.
+// The fused step kernel's per-block gradient rows (model_4 on the fused path): frows rows of
+// fstride floats in the model_2 layout; slot p of the model_4 vector is row slot p, or
+// p - f_shift from f_at on (past the entity-edge block); f_np = model_2's parameter count.
+struct FusedRows {
+  const float* fp;
+  int frows, fstride, f_at, f_shift, f_np;
+};
+struct WideAdam {
+  hdg_state* state;
+  float lr, inv_pairs;
+  float* stats;      // may be NULL
+  FusedRows fused;   // fp = NULL: every gradient slot from the general path's rows
+};
 size_t wide_workspace_bytes(const hdg_shape* s);
 size_t wide_prep_bytes(const hdg_shape* s);
 void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int64_t* kt,
@@ -86,19 +101,28 @@ void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, i
 int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st);
 // train: forward + backward -> grad[NP + 4] (slot NP = CE sum); !train: forward only,
 // CE sum -> *ce_sum (may be NULL).  Outputs as in hdg_fwd_bwd.
+// adam (train only, may be NULL): apply TF Adam to adam->state in the final reduction
 int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
-             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st);
+             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st,
+             const WideAdam* adam = nullptr);
 // model_4 on the fused path: the entity-edge stage on the general path's kernels around
 // the fused step kernel.  wide_ee_fwd: EE first layer, node products, classifier over the
-// mapped relations -> ncls [B][Nc][2] (n_c[2:4] of marshalling_B2, model_4.py:95-97);
+// mapped relations -> per-tile partial bins (wide_ncpart: u64 [B][wide_ncpart_tiles][Nc][2],
+// 2^-32 fixed point) of n_c[2:4] of marshalling_B2 (model_4.py:95-97), which the step kernel
+// sums;
 // wide_ee_bwd: from dn (wide_dn, [B][Nc][4], written by the step kernel) the EE backward
 // and the reduction of the EE parameters' gradient rows into grad[EE_W11 .. EC_B2 + 2).
 // bt->prep, workspace: this path's layouts (wide_prep_bytes / wide_workspace_bytes).
 float* wide_dn(const hdg_shape* s, void* workspace);
+// bpow (a step ending in wide_ee_bwd with adam): the Adam factors' beta powers.
+// wide_ee_bwd with adam: every parameter's TF-Adam update in its final reduction, the
+// non-entity-edge gradients read from grad (the fused kernel's reduction wrote them).
 int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
-                float* ncls, hipStream_t st);
+                hipStream_t st, const float* bpow = nullptr);
+const unsigned long long* wide_ncpart(const hdg_shape* s, void* workspace);
+int wide_ncpart_tiles(const hdg_shape* s);
 int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
-                float* grad, hipStream_t st);
+                float* grad, hipStream_t st, const WideAdam* adam = nullptr);
 
 // fused path pieces the general path reuses (hdgnn.hip)
 hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,

@@ -224,6 +224,8 @@ enum : int {
   D_EEC = 520,             // EE classifier U2'[:,1] - U2'[:,0]
   D_EECQ = 544,            // -log2(e) (U2'[:,1] - U2'[:,0])    (kw_ee_clsb: e = 2^delta')
   D_EEBQ = 564,            // -log2(e) (b2'[1] - b2'[0])
+  D_AUX = 568,             // [7] train steps: lpara, lmap, |theta1|, |theta2|,
+                           //     sqrt(1-b2^t)/(1-b1^t), b1^(t+1), b2^(t+1)  (kw_reduce_adam)
   D_WORDS = 576
 };
 
@@ -293,38 +295,6 @@ __device__ __forceinline__ void stage_w(float* dst, const float* src, int n) {
 }
 
 // ---------------------------------------------------------------------------------
-// kw_derive: weight products every phase reads (1 block)
-// ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void kw_derive(const float* __restrict__ W, Off o, int Nc,
-                                                float* __restrict__ D) {
-  const int t = threadIdx.x;
-  const float Nc1 = (float)(Nc - 1);
-  for (int e = t; e < H * H; e += NT) {           // M[l][k] = sum_m V2[l][m] U1e[m][k]
-    const int l = e / H, k = e - l * H;
-    float acc = 0.f;
-    for (int m = 0; m < H; ++m)
-      acc = fmaf(W[o.H1_W2 + l * H + m], W[o.H2_W1 + (2 + m) * H + k], acc);
-    D[D_M + e] = acc;
-  }
-  if (t < H) {
-    float cu = 0.f;
-    for (int m = 0; m < H; ++m) cu = fmaf(W[o.H1_B2 + m], W[o.H2_W1 + (2 + m) * H + t], cu);
-    cu *= Nc1;
-    D[D_T0 + t] = cu;
-    D[D_S0 + t] = cu + (W[o.H2_W1 + t] + W[o.H2_B1 + t]);
-    D[D_EPS + t] = W[o.H2_W1 + H + t] - W[o.H2_W1 + t];
-    D[D_CV + t] = W[o.H2_W2 + 2 * t + 1] - W[o.H2_W2 + 2 * t];
-    D[D_DLT + t] = W[o.H1_W1 + 9 * H + t] - W[o.H1_W1 + 8 * H + t];
-    if (o.EC_W1 >= 0) {
-      D[D_EED + t] = W[o.EC_W1 + H + t] - W[o.EC_W1 + t];
-      D[D_EEC + t] = W[o.EC_W2 + 2 * t + 1] - W[o.EC_W2 + 2 * t];
-      D[D_EECQ + t] = -1.4426950408889634f * D[D_EEC + t];
-      if (t == 0) D[D_EEBQ] = -1.4426950408889634f * (W[o.EC_B2 + 1] - W[o.EC_B2]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // block helpers
 // ---------------------------------------------------------------------------------
 // Combine per-wave accumulators acc[H] of the 64 lane-nodes over the 4 waves (fixed order)
@@ -356,6 +326,72 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red, float* out
   for (int q = threadIdx.x; q < NV; q += NT)
     out[q] = ((red[q] + red[NV + q]) + red[2 * NV + q]) + red[3 * NV + q];
   __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------
+// kw_derive: weight products every phase reads (1 block)
+// ---------------------------------------------------------------------------------
+// With bpow (a training step that ends in kw_reduce_adam) also the step's loss terms and
+// Adam factors from the pre-update parameters (D_AUX; k_adam_tf's formulas), so that no
+// block of the final reduce + Adam kernel depends on another.
+__device__ __forceinline__ void derive_body(const float* __restrict__ W, const Off& o, int Nc,
+                                            float* __restrict__ D,
+                                            const float* __restrict__ bpow) {
+  const int t = threadIdx.x;
+  if (bpow) {
+    __shared__ float red[NW * 3];
+    __shared__ float tot[3];
+    const int np = o.NP, TH1 = np - 4, TH2 = np - 2;
+    float v[3] = {0.f, 0.f, 0.f};
+    for (int p = t; p < np; p += NT) {
+      const float w = W[p];
+      v[0] = fmaf(w, w, v[0]);
+      if (p >= TH1 && p < TH1 + 2) v[1] = fmaf(w, w, v[1]);
+      if (p >= TH2 && p < TH2 + 2) v[2] = fmaf(w, w, v[2]);
+    }
+    block_sum<3>(v, red, tot);
+    if (t == 0) {
+      const float n1 = sqrtf(tot[1]), n2 = sqrtf(tot[2]);
+      const float b1p = bpow[0], b2p = bpow[1];
+      D[D_AUX + 0] = 0.0005f * tot[0];
+      D[D_AUX + 1] = 0.01f * (n2 + n1);
+      D[D_AUX + 2] = n1;
+      D[D_AUX + 3] = n2;
+      D[D_AUX + 4] = sqrtf(1.f - b2p) / (1.f - b1p);
+      D[D_AUX + 5] = b1p * 0.9f;
+      D[D_AUX + 6] = b2p * 0.999f;
+    }
+  }
+  const float Nc1 = (float)(Nc - 1);
+  for (int e = t; e < H * H; e += NT) {           // M[l][k] = sum_m V2[l][m] U1e[m][k]
+    const int l = e / H, k = e - l * H;
+    float acc = 0.f;
+    for (int m = 0; m < H; ++m)
+      acc = fmaf(W[o.H1_W2 + l * H + m], W[o.H2_W1 + (2 + m) * H + k], acc);
+    D[D_M + e] = acc;
+  }
+  if (t < H) {
+    float cu = 0.f;
+    for (int m = 0; m < H; ++m) cu = fmaf(W[o.H1_B2 + m], W[o.H2_W1 + (2 + m) * H + t], cu);
+    cu *= Nc1;
+    D[D_T0 + t] = cu;
+    D[D_S0 + t] = cu + (W[o.H2_W1 + t] + W[o.H2_B1 + t]);
+    D[D_EPS + t] = W[o.H2_W1 + H + t] - W[o.H2_W1 + t];
+    D[D_CV + t] = W[o.H2_W2 + 2 * t + 1] - W[o.H2_W2 + 2 * t];
+    D[D_DLT + t] = W[o.H1_W1 + 9 * H + t] - W[o.H1_W1 + 8 * H + t];
+    if (o.EC_W1 >= 0) {
+      D[D_EED + t] = W[o.EC_W1 + H + t] - W[o.EC_W1 + t];
+      D[D_EEC + t] = W[o.EC_W2 + 2 * t + 1] - W[o.EC_W2 + 2 * t];
+      D[D_EECQ + t] = -1.4426950408889634f * D[D_EEC + t];
+      if (t == 0) D[D_EEBQ] = -1.4426950408889634f * (W[o.EC_B2 + 1] - W[o.EC_B2]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void kw_derive(const float* __restrict__ W, Off o, int Nc,
+                                                float* __restrict__ D,
+                                                const float* __restrict__ bpow) {
+  derive_body(W, o, Nc, D, bpow);
 }
 
 // The m-range of the other index a wave sweeps, split around this tile's own nodes
@@ -685,14 +721,22 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   }
 }
 
-// grid (te, B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage
+// grid (te (+1), B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage.
+// D != NULL: one more x column whose block (te, 0, 0) runs kw_derive's work (no kernel of
+// its own; nothing here reads D)
 __global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
                                                  const uint32_t* __restrict__ abits,
                                                  const uint32_t* __restrict__ aT,
                                                  const uint32_t* __restrict__ prep,
                                                  const float* __restrict__ W, Off o, int Ne,
                                                  int Nc, int ent, float* __restrict__ P,
-                                                 float* __restrict__ R1, float* __restrict__ C1) {
+                                                 float* __restrict__ R1, float* __restrict__ C1,
+                                                 float* __restrict__ D,
+                                                 const float* __restrict__ bpow) {
+  if (D && blockIdx.x == gridDim.x - 1) {       // block-uniform
+    if (blockIdx.y == 0 && blockIdx.z == 0) derive_body(W, o, Nc, D, bpow);
+    return;
+  }
   if (blockIdx.z == 0 && ent)
     ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
   else
@@ -959,7 +1003,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     if (ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (e & 1)], qfix(tsum[e]));
   }
   __syncthreads();
-  // per-tile partial bins, summed in tile order by kw_cross_fwd / kw_ee_bins (no global
+  // per-tile partial bins, summed in tile order by kw_cross_fwd / k_commit_step (no global
   // atomics: the L2s of the 8 XCDs are not coherent for device-scope atomics)
   for (int c = t; c < 2 * Nc; c += NTP) outp[c] = bins[c];
 }
@@ -1018,18 +1062,6 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
     alpha[((size_t)b * Nc + c) * H + k] = al;
     beta[((size_t)b * Nc + c) * H + k] = be;
   }
-}
-
-// kw_ee_bins  grid (ceil(2 Nc / NT), B): the EE aggregate n_c[2:4] as floats, summed over
-// the kw_ee_fwd tile partials exactly as kw_cross_fwd does (the fused step kernel's class
-// part for model_4, hdgnn.hip hybrid path)
-__global__ __launch_bounds__(NT) void kw_ee_bins(const unsigned long long* __restrict__ ncpart,
-                                                 int nt, int Nc, float* __restrict__ ncls) {
-  const int b = blockIdx.y, e = blockIdx.x * NT + threadIdx.x;
-  if (e >= 2 * Nc) return;
-  unsigned long long a = 0ull;
-  for (int tl = 0; tl < nt; ++tl) a += ncpart[((size_t)b * nt + tl) * 2 * Nc + e];
-  ncls[(size_t)b * 2 * Nc + e] = (float)((double)a * (1.0 / FIX));
 }
 
 // ---------------------------------------------------------------------------------
@@ -2268,6 +2300,103 @@ __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ p
   if (lane == 0) out[blockIdx.x] = a;
 }
 
+// kw_reduce_adam  grid (np + HDG_TRAILER), one wave per slot: kw_grad_reduce fused with
+// k_adam_tf for a single-process training step (hdg_train_step on the general path and on
+// the model_4 fused path).  Slots in [seg_lo, seg_hi) are reduced from the partial rows as
+// in kw_grad_reduce; the others (model_4 on the fused path) from the step kernel's
+// per-block rows fp (frows rows of fstride floats, model_2 layout: slot p of the model_4
+// vector is p2 = p, or p - f_shift from f_at on), as k_grad_reduce does.  Then TF1
+// ApplyAdam for a parameter slot, with the loss terms and the Adam factor kw_derive put in
+// D_AUX from the pre-update parameters, so no block depends on another; the CE slot's wave
+// writes the loss stats, block 0 the new beta powers.  A fault in the step kernel's rows
+// (a block-pair exchange timed out) skips every update, as in k_adam_tf.
+__device__ __forceinline__ float wave_reduce_rows(const float* src, int rows, int stride,
+                                                  bool count, unsigned long long& c) {
+  const int lane = threadIdx.x;
+  float a = 0.f;
+  c = 0ull;
+  for (int r = lane; r < rows; r += 64) {
+    const float v = src[(size_t)r * stride];
+    if (count) c += (unsigned long long)v;
+    else a += v;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  return wsum(a);
+}
+
+__global__ __launch_bounds__(64) void kw_reduce_adam(
+    const float* __restrict__ part, Segs sg, int np, int seg_lo, int seg_hi, FusedRows fr,
+    float* __restrict__ grad, float* __restrict__ params, float* __restrict__ mm,
+    float* __restrict__ vv, float* __restrict__ bpow, const float* __restrict__ D, float lr,
+    float inv_pairs, float* __restrict__ stats) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const int pc = np + HDG_TR_COUNT;
+  if (p > pc && p <= pc + 2) return;              // written by the count slot's wave
+  const bool seg = p >= seg_lo && p < seg_hi;
+  // the update's operands first: their latency overlaps the reduction
+  const bool isp = p < np;
+  const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
+  unsigned long long c = 0ull;
+  float fault = 0.f;
+  if (fr.fp) {
+    unsigned long long cf;
+    fault = wave_reduce_rows(fr.fp + fr.f_np + HDG_TR_FAULT, fr.frows, fr.fstride, false, cf);
+  }
+  float g;
+  if (seg) {
+    float a = 0.f;
+    for (int q = 0; q < sg.count; ++q) {
+      const Seg& sgq = sg.s[q];
+      if (sgq.n > 0 && p >= sgq.p0 && p < sgq.p0 + sgq.n) {
+        const float* src = part + sgq.off + (long long)(p - sgq.p0) * sgq.rows;
+        if (p == pc)
+          for (int r = lane; r < sgq.rows; r += 64) c += (unsigned long long)src[r];
+        else
+          for (int r = lane; r < sgq.rows; r += 64) a += src[r];
+        break;
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+    g = wsum(a);
+  } else {
+    const int p2 = p < fr.f_at ? p : p - fr.f_shift;
+    g = wave_reduce_rows(fr.fp + p2, fr.frows, fr.fstride, p == pc, c);
+  }
+  if (lane != 0) return;
+  if (p == pc) {
+    grad[p] = (float)(c & 0xFFFFull);
+    grad[p + 1] = (float)((c >> 16) & 0xFFFFull);
+    grad[p + 2] = (float)(c >> 32);
+    return;
+  }
+  grad[p] = g;
+  if (p == np + HDG_TR_CE && stats) {
+    const float ce = g * inv_pairs;
+    stats[0] = ce;
+    stats[1] = D[D_AUX + 1];
+    stats[2] = D[D_AUX + 0];
+    stats[3] = 10.f * ce + 0.1f * D[D_AUX + 1] + D[D_AUX + 0];
+  }
+  if (!isp || fault != 0.f) return;
+  const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
+  const int TH1 = np - 4, TH2 = np - 2;
+  float gg = g + 0.001f * w;
+  if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / D[D_AUX + 2];
+  if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / D[D_AUX + 3];
+  float m = m0, v = v0;
+  m += (gg - m) * (1.f - b1);
+  v += (gg * gg - v) * (1.f - b2);
+  mm[p] = m;
+  vv[p] = v;
+  params[p] = w - (lr * D[D_AUX + 4]) * m / (sqrtf(v) + ep);
+  if (p == 0) {
+    bpow[0] = D[D_AUX + 5];
+    bpow[1] = D[D_AUX + 6];
+  }
+}
+
 // kw_prep_sort  grid (B), 1024 threads, dynamic LDS 2 Ne floats: stable rank sort of x,
 // distinct values, counts below each distinct value and f64 prefix sums (any Ne)
 __global__ __launch_bounds__(1024) void kw_prep_sort(const float* __restrict__ x,
@@ -2460,8 +2589,13 @@ float* wide_dn(const hdg_shape* s, void* workspace) {
   return (float*)workspace + wide_layout(s).dn;
 }
 
+const unsigned long long* wide_ncpart(const hdg_shape* s, void* workspace) {
+  return (const unsigned long long*)((float*)workspace + wide_layout(s).ncpart);
+}
+int wide_ncpart_tiles(const hdg_shape* s) { return ee_fwd_tiles(s->ne); }
+
 int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
-                float* ncls, hipStream_t st) {
+                hipStream_t st, const float* bpow) {
   const int B = s->batch, Ne = s->ne, Nc = s->nc;
   const Off o = param_offsets(s->variant);
   const WideWork w = wide_layout(s);
@@ -2471,25 +2605,20 @@ int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const int te = (Ne + TN - 1) / TN;
   if (int rc = set_wide_attrs()) return rc;
-  hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, ws + w.D);
-  WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
-                     bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1));
+  hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+                     bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1),
+                     ws + w.D, bpow);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, 1), dim3(NT), 0, st, bt->x, params, o, Ne, 0,
                      F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.R1), F(w.C1), F(w.Rn),
                      F(w.Cn), F(w.rho), F(w.gmm));
   WTRY(hipGetLastError());
   unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
-  if (int rc = launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st)) return rc;
-  hipLaunchKernelGGL(kw_ee_bins, dim3((2 * Nc + NT - 1) / NT, B), dim3(NT), 0, st, ncpart,
-                     ee_fwd_tiles(Ne), Nc, ncls);
-  WTRY(hipGetLastError());
-  return 0;
+  return launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st);
 }
 
 int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
-                float* grad, hipStream_t st) {
+                float* grad, hipStream_t st, const WideAdam* adam) {
   const int B = s->batch, Ne = s->ne, Nc = s->nc;
   const Off o = param_offsets(s->variant);
   const WideWork w = wide_layout(s);
@@ -2505,8 +2634,8 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
                      F(w.dgam), part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
-                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1),
-                     F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
+                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam),
+                     F(w.phi), F(w.psi), part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
                      F(w.psi), (double*)F(w.tab));
@@ -2517,7 +2646,15 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   WTRY(hipGetLastError());
   // the entity-edge parameters [EE_W11, EC_B2 + 2): one contiguous block of the flat vector
   const int p0 = o.EE_W11, n = o.EC_B2 + 2 - o.EE_W11;
-  hipLaunchKernelGGL(kw_grad_reduce, dim3(n), dim3(64), 0, st, part, w.segs, p0, o.NP, grad + p0);
+  if (adam) {
+    hdg_state* S = adam->state;
+    hipLaunchKernelGGL(kw_reduce_adam, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
+                       o.NP, p0, p0 + n, adam->fused, grad, S->params, S->adam_m, S->adam_v,
+                       S->beta_pow, ws + w.D, adam->lr, adam->inv_pairs, adam->stats);
+  } else {
+    hipLaunchKernelGGL(kw_grad_reduce, dim3(n), dim3(64), 0, st, part, w.segs, p0, o.NP,
+                       grad + p0);
+  }
   WTRY(hipGetLastError());
   return 0;
 }
@@ -2552,7 +2689,8 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
 }
 
 int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
-             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st) {
+             hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st,
+             const WideAdam* adam) {
   const int B = s->batch, Ne = s->ne, Nc = s->nc, v = s->variant;
   const Off o = param_offsets(v);
   const WideWork w = wide_layout(s);
@@ -2570,13 +2708,16 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
 
   const size_t tlds = sort_lds_bytes(Ne);
   if (int rc = set_wide_attrs()) return rc;
-  hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D);
-  WTRY(hipGetLastError());
+  const float* bpow = train && adam ? adam->state->beta_pow : nullptr;
+  if (!(ent || ee)) {
+    hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D, bpow);
+    WTRY(hipGetLastError());
+  }
   // ---- entity side ----
-  if (ent || ee) {
-    hipLaunchKernelGGL(kw_ent_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st, bt->x,
-                       bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P), F(w.R1),
-                       F(w.C1));
+  if (ent || ee) {   // + kw_derive's work in one more block column
+    hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st,
+                       bt->x, bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P),
+                       F(w.R1), F(w.C1), D, bpow);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
                        params, o, Ne, ent ? 1 : 0, F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp),
@@ -2642,9 +2783,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
                        F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
-                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1),
-                       F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
+    hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, D, Ne,
+                       ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
+                       F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
                        nullptr, F(w.psi), (double*)F(w.tab));
@@ -2654,8 +2795,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        w.segs);
     WTRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs, 0,
-                     o.NP, grad);
+  if (adam) {
+    hdg_state* S = adam->state;
+    hipLaunchKernelGGL(kw_reduce_adam, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
+                       o.NP, 0, o.NP + HDG_TRAILER, FusedRows{}, grad, S->params, S->adam_m,
+                       S->adam_v, S->beta_pow, D, adam->lr, adam->inv_pairs, adam->stats);
+  } else {
+    hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
+                       0, o.NP, grad);
+  }
   WTRY(hipGetLastError());
   return 0;
 }
