@@ -1977,8 +1977,10 @@ __device__ __forceinline__ void ee_clsb_rows(
 #pragma unroll
     for (int kk = 0; kk < H2; ++kk) {
       const f2 sd = st[kk] * d2;
-      acc[kk] += sd;
-      ag[kk] = fma2(a2, sd, ag[kk]);
+      // as asm: kept ahead of half_sums20's swaps (volatile order), so the swaps work on
+      // the sd registers in place instead of on copies
+      asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc[kk]) : "v"(sd));
+      asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(ag[kk]) : "v"(a2), "v"(sd));
       sv[2 * kk] = sd.x;
       sv[2 * kk + 1] = sd.y;
     }
