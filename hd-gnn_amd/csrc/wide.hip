@@ -1891,7 +1891,7 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------
-// kw_ee_clsb  grid (te, B), 8 waves: entity-edge classifier backward (model_4.py:286-304)
+// kw_ee_clsb  grid (ceil(Ne/32), B), 4 waves: entity-edge classifier backward (model_4.py:286-304)
 //   dz1 = p0 p1 (dp1 - dp0) = -dz0, dp_r[m] = dn[hid i'(r)][2+m] + dn[hid j'(r)][2+m]
 //   (relation r -> index pair (i', j') on the n-grid, the stride quirk of utils2.py:121-137);
 //   the two-class softmax as a sigmoid of the logit difference: with
@@ -1996,7 +1996,7 @@ __device__ __forceinline__ void ee_clsb_rows(
   }
 }
 
-__global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void kw_ee_clsb(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw_ee_clsb(
     const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
     const int32_t* __restrict__ hidg, const int32_t* __restrict__ nleng,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
@@ -2008,12 +2008,12 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   (void)o;
   extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][TB]
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
-  __shared__ float buf[NWP * 2 * TB * HP];
+  __shared__ float buf[NW * 2 * TB * HP];
   __shared__ float res[TB * HP];
-  __shared__ float red[NWP * 21];
+  __shared__ float red[NW * 21];
   __shared__ float tot[21];
   __shared__ float cl[H];
-  __shared__ float zred[NWP * 2 * H];
+  __shared__ float zred[NW * 2 * H];
   __shared__ float4 gl4[(H / 4) * TB];            // the columns' gam rows, [v][column]
   __shared__ float4 gdl4[(H / 4) * TB];           // gam + d
   const int b = blockIdx.y, t0 = blockIdx.x * TB, te = gridDim.x;
@@ -2025,17 +2025,17 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int WE = (Ne + 31) >> 5;
   float* Eq = dyn;
   uint32_t* abl = reinterpret_cast<uint32_t*>(dyn + Ne);
-  for (int e = t; e < Ne; e += NTP) {
+  for (int e = t; e < Ne; e += NT) {
     const int h = hidg[(size_t)b * Ne + e];
     const float* d = dn + ((size_t)b * Nc + (h >= 0 && h < Nc ? h : 0)) * 4;
     Eq[e] = (h >= 0 && h < Nc) ? d[3] - d[2] : 0.f;
   }
-  for (int e = t; e < WE * TB; e += NTP) {        // a^T rows of the tile's columns: bit m = a[m][j]
+  for (int e = t; e < WE * TB; e += NT) {        // a^T rows of the tile's columns: bit m = a[m][j]
     const int w = e / TB, l = e - w * TB, node = t0 + l < Ne ? t0 + l : Ne - 1;
     abl[e] = aT[((size_t)b * Ne + node) * WE + w];
   }
   if (t < H) cl[t] = D[D_EEC + t];
-  for (int e = t; e < (H / 4) * TB; e += NTP) {   // [v][column]: conflict-free 16-B reads
+  for (int e = t; e < (H / 4) * TB; e += NT) {   // [v][column]: conflict-free 16-B reads
     const int v = e / TB, l = e - v * TB, node = t0 + l < Ne ? t0 + l : Ne - 1;
     const float4 g = reinterpret_cast<const float4*>(gmm + ((size_t)b * Ne + node) * H)[v];
     const float4 d = reinterpret_cast<const float4*>(D + D_EED)[v];
@@ -2056,7 +2056,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   // rows holding relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
   float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // this tile's partial rows
-  for (int e = rows * H + t; e < Ne * H; e += NTP) rowp[e] = 0.f;   // rows past the relations
+  for (int e = rows * H + t; e < Ne * H; e += NT) rowp[e] = 0.f;   // rows past the relations
   const float* rb = rho + (size_t)b * Ne * H;
   const float inv = 1.f / (float)dn1;
   const bool aligned = n == Ne;
@@ -2067,8 +2067,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     stage_rows(os_, rb, c0, c1);
     __syncthreads();
-    int lo, hi;
-    wave_share(c0, c1, lo, hi);
+    const int lo = c0 + ((c1 - c0) * uni(wv)) / NW, hi = c0 + ((c1 - c0) * (uni(wv) + 1)) / NW;
     ee_clsb_rows(lo, hi, c0, os_, abl + col, Ne, jn, live, nrel, dn1, inv, aligned, Eq, Ej,
                  gl4 + col, gdl4 + col, D, rowp, acc, ag, sdl, zr, kst);
   }
@@ -2082,16 +2081,16 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     buf[(wv * 2 * TB + lane) * HP + 2 * kk + 1] = acc[kk].y;
   }
   __syncthreads();
-  for (int e = t; e < TB * H; e += NTP) {
+  for (int e = t; e < TB * H; e += NT) {
     const int nn = e / H, k = e - nn * H;
     float sum = 0.f;
 #pragma unroll
-    for (int q = 0; q < 2 * NWP; ++q) sum += buf[(q * TB + nn) * HP + k];   // row q*TB+nn: wave q/2, half q&1
+    for (int q = 0; q < 2 * NW; ++q) sum += buf[(q * TB + nn) * HP + k];   // row q*TB+nn: wave q/2, half q&1
     res[nn * HP + k] = sum;
   }
   __syncthreads();
   float* dout = dgam + (size_t)b * Ne * H;
-  for (int e = t; e < TB * H; e += NTP) {
+  for (int e = t; e < TB * H; e += NT) {
     const int nn = e / H, k = e - nn * H;
     if (t0 + nn < Ne) dout[(size_t)(t0 + nn) * H + k] = res[nn * HP + k] * cl[k];
   }
@@ -2102,7 +2101,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     v[2 * kk + 1] = ag[kk].y;
   }
   v[20] = sdl;
-  block_sum8<21>(v, red, tot);
+  block_sum<21>(v, red, tot);
   const int row = b * te + blockIdx.x;
   if (t < H) {
     // sum_pairs relu(kappa_k) dz1 = sum_i rho_ik R_ik + sum_j gam_jk C_jk + d_k sum_{a=1} s_k dz1
@@ -2116,7 +2115,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
       zg = fmaf(glf[((t >> 2) * TB + nn) * 4 + (t & 3)], cs, zg);
     }
     float zw = 0.f;
-    for (int q = 0; q < 2 * NWP; ++q) zw += zred[q * H + t];
+    for (int q = 0; q < 2 * NW; ++q) zw += zred[q * H + t];
     const float zk = (zw + zg) + D[D_EED + t] * tot[t];
     const float sg_ = sc * cl[t];                    // sum of g over the tile
     const float a1 = tot[t] * cl[t];
@@ -2631,9 +2630,9 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const int te = (Ne + TN - 1) / TN;
   float* part = ws;
   const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-  hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
-                     bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
-                     F(w.dgam), part, w.segs);
+  hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
+                     aT, bt->hid, bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm),
+                     F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
                      ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam),
@@ -2781,9 +2780,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   if (ee) {
     const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-    hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NTP), lds, st, bt->abits, aT, bt->hid,
-                       bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn), F(w.drho),
-                       F(w.dgam), part, w.segs);
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
+                       aT, bt->hid, bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn),
+                       F(w.drho), F(w.dgam), part, w.segs);
     WTRY(hipGetLastError());
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, D, Ne,
                        ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
