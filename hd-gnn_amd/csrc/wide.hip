@@ -10,7 +10,8 @@
 //   kw_derive       derived weight products (M = V2 U1e, offsets, differences)
 //   kw_ent_fwd      ENT: P_i  = sum_j relu(z_ij) + relu(z_ji)     (mlp_entity_B1 + agg)
 //                   EE : R1_i = sum_j relu(z'_ij), C1_i = sum_j relu(z'_ji)
-//   kw_node_fwd     ENT: E_bar, h, o, x'          EE: R, C, rho, gam (classifier operands)
+//   node_fwd_tile   ENT: E_bar, h, o, x'          EE: R, C, rho, gam (classifier operands),
+//                   in kw_ent_fwd's blocks after their tile's pair sums
 //   kw_ee_fwd       EE : entity-edge classifier + softmax on every relation the index file
 //                   maps, aggregated into n_c[2:4] (marshalling_B2 of B_2's edge part)
 //   kw_cross_fwd    n_c = [K_s x', K_t x', n_c[2:4]]; hunk first-layer alpha, beta
@@ -721,30 +722,9 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   }
 }
 
-// grid (te (+1), B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage.
-// D != NULL: one more x column whose block (te, 0, 0) runs kw_derive's work (no kernel of
-// its own; nothing here reads D)
-__global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
-                                                 const uint32_t* __restrict__ abits,
-                                                 const uint32_t* __restrict__ aT,
-                                                 const uint32_t* __restrict__ prep,
-                                                 const float* __restrict__ W, Off o, int Ne,
-                                                 int Nc, int ent, float* __restrict__ P,
-                                                 float* __restrict__ R1, float* __restrict__ C1,
-                                                 float* __restrict__ D,
-                                                 const float* __restrict__ bpow) {
-  if (D && blockIdx.x == gridDim.x - 1) {       // block-uniform
-    if (blockIdx.y == 0 && blockIdx.z == 0) derive_body(W, o, Nc, D, bpow);
-    return;
-  }
-  if (blockIdx.z == 0 && ent)
-    ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
-  else
-    ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
-}
 
 // ---------------------------------------------------------------------------------
-// kw_node_fwd  grid (te, B, 1 + EE)
+// node_fwd_tile (kw_ent_fwd's tail, one 64-node tile)
 //   ENT (model_2.py:181-205): E_bar = P W5 + 2(Ne-1) b5; h = relu([x, E_bar] W1' + b1');
 //        o = h w2' + b2'; x' = relu(o)
 //   EE  (model_4.py:232-243, 282-304): R = R1 Q2 + (Ne-1) q2, C = C1 Q2 + (Ne-1) q2;
@@ -770,12 +750,18 @@ __device__ __forceinline__ void rows_x_w(const float* As, const float* Wm, const
   }
 }
 
-__global__ __launch_bounds__(NT) void kw_node_fwd(
-    const float* __restrict__ x, const float* __restrict__ W, Off o, int Ne, int ent,
-    const float* __restrict__ P, float* __restrict__ Eb, float* __restrict__ hE,
-    float* __restrict__ ov, float* __restrict__ xp, const float* __restrict__ R1,
-    const float* __restrict__ C1, float* __restrict__ Rn, float* __restrict__ Cn,
-    float* __restrict__ rho, float* __restrict__ gmm) {
+struct NodeFwdOut {
+  float *Eb, *hE, *ov, *xp, *Rn, *Cn, *rho, *gmm;
+};
+
+// the tile's 64 nodes (t0 = blockIdx.x * TN, commit blockIdx.y): ENT (ent_part) or EE
+__device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
+                                              const float* __restrict__ W, const Off& o, int Ne,
+                                              bool ent_part, const float* __restrict__ P,
+                                              const float* __restrict__ R1,
+                                              const float* __restrict__ C1, const NodeFwdOut& no) {
+  float *Eb = no.Eb, *hE = no.hE, *ov = no.ov, *xp = no.xp;
+  float *Rn = no.Rn, *Cn = no.Cn, *rho = no.rho, *gmm = no.gmm;
   __shared__ float A[TN * HP], Bs[TN * HP], Cs[TN * HP], Ds[TN * HP];
   __shared__ float Wl[896];                       // the block's weights, staged once
   __shared__ float kz[1];                         // 0.f: stride-0 operand of padding tiles
@@ -785,7 +771,7 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
   const float Ne1 = (float)(Ne - 1);
   if (t == 0) kz[0] = 0.f;
   // rows n >= nn of the LDS tiles are never stored (MFMA rows are independent)
-  if (blockIdx.z == 0 && ent) {
+  if (ent_part) {
     const float *W5 = Wl, *B5 = Wl + 400, *W1e = Wl + 420, *B1e = Wl + 840, *W2e = Wl + 860;
     stage_w(Wl, W + o.E1_W5, 420);                // W5 | b5
     stage_w(Wl + 420, W + o.E3_W1, 461);          // W1' | b1' | w2' | b2'
@@ -837,6 +823,34 @@ __global__ __launch_bounds__(NT) void kw_node_fwd(
   rows_x_w(Ds, P1 + 2 * H, kz, [&](int n, int k, float c) {   // gam = C U1'[2:]
     if (n < nn) gmm[base + n * H + k] = c;
   });
+}
+
+
+// grid (te (+1), B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage.
+// D != NULL: one more x column whose block (te, 0, 0) runs kw_derive's work (no kernel of
+// its own; nothing here reads D)
+__global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
+                                                 const uint32_t* __restrict__ abits,
+                                                 const uint32_t* __restrict__ aT,
+                                                 const uint32_t* __restrict__ prep,
+                                                 const float* __restrict__ W, Off o, int Ne,
+                                                 int Nc, int ent, float* __restrict__ P,
+                                                 float* __restrict__ R1, float* __restrict__ C1,
+                                                 float* __restrict__ D,
+                                                 const float* __restrict__ bpow, NodeFwdOut no) {
+  if (D && blockIdx.x == gridDim.x - 1) {       // block-uniform
+    if (blockIdx.y == 0 && blockIdx.z == 0) derive_body(W, o, Nc, D, bpow);
+    return;
+  }
+  const bool ent_part = blockIdx.z == 0 && ent;
+  if (ent_part)
+    ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
+  else
+    ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
+  // the per-node products on the tile (node_fwd_tile): its inputs are this block's outputs
+  // (global writes made visible to the block by the barrier)
+  __syncthreads();
+  node_fwd_tile(x, W, o, Ne, ent_part, P, R1, C1, no);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2606,13 +2620,10 @@ int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const int te = (Ne + TN - 1) / TN;
   if (int rc = set_wide_attrs()) return rc;
+  const NodeFwdOut no{F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.Rn), F(w.Cn), F(w.rho), F(w.gmm)};
   hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
                      bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1),
-                     ws + w.D, bpow);
-  WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, 1), dim3(NT), 0, st, bt->x, params, o, Ne, 0,
-                     F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.R1), F(w.C1), F(w.Rn),
-                     F(w.Cn), F(w.rho), F(w.gmm));
+                     ws + w.D, bpow, no);
   WTRY(hipGetLastError());
   unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
   return launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st);
@@ -2715,14 +2726,12 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     WTRY(hipGetLastError());
   }
   // ---- entity side ----
-  if (ent || ee) {   // + kw_derive's work in one more block column
+  if (ent || ee) {   // + kw_derive's work in one more block column, node_fwd_tile per tile
+    const NodeFwdOut no{F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.Rn), F(w.Cn), F(w.rho),
+                        F(w.gmm)};
     hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st,
                        bt->x, bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P),
-                       F(w.R1), F(w.C1), D, bpow);
-    WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_node_fwd, dim3(te, B, (ent && ee) ? 2 : 1), dim3(NT), 0, st, bt->x,
-                       params, o, Ne, ent ? 1 : 0, F(w.P), F(w.Eb), F(w.hE), F(w.ov), F(w.xp),
-                       F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.rho), F(w.gmm));
+                       F(w.R1), F(w.C1), D, bpow, no);
     WTRY(hipGetLastError());
   }
   unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
