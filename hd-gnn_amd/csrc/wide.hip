@@ -1758,14 +1758,14 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
 }
 
 template <int MODE>
-__global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
-                                                   const uint32_t* __restrict__ abits,
-                                                   const uint32_t* __restrict__ prep,
-                                                   const float* __restrict__ W, Off o, int Ne,
-                                                   int Nc, const float* __restrict__ ra,
-                                                   const float* __restrict__ rb,
-                                                   const double* __restrict__ tab,
-                                                   float* __restrict__ part, Segs sg) {
+__device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
+                                               const uint32_t* __restrict__ abits,
+                                               const uint32_t* __restrict__ prep,
+                                               const float* __restrict__ W, const Off& o, int Ne,
+                                               int Nc, const float* __restrict__ ra,
+                                               const float* __restrict__ rb,
+                                               const double* __restrict__ tab,
+                                               float* __restrict__ part, const Segs& sg) {
 #pragma clang fp contract(off)
   const GenPrep GP = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x, B = gridDim.y;
@@ -1902,6 +1902,23 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
       }
     }
   }
+}
+
+// grid (te, B, stages): stage mode0 + z -- 0: E1 (ra = rb = rho_E), 1: EE (phi, psi); both
+// stages of model_4's general path in one launch
+__global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
+                                                   const uint32_t* __restrict__ abits,
+                                                   const uint32_t* __restrict__ prep,
+                                                   const float* __restrict__ W, Off o, int Ne,
+                                                   int Nc, int mode0, const float* __restrict__ r0,
+                                                   const float* __restrict__ phi,
+                                                   const float* __restrict__ psi,
+                                                   const double* __restrict__ tab,
+                                                   float* __restrict__ part, Segs sg) {
+  if (mode0 + (int)blockIdx.z == 0)
+    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg);
+  else
+    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2565,9 +2582,7 @@ int set_wide_attrs() {
   if (!attr_set) {
     WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
                              96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<0>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -2652,8 +2667,8 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
                      F(w.psi), (double*)F(w.tab));
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
-                     bt->abits, prep, params, o, Ne, Nc, F(w.phi), F(w.psi),
+  hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+                     bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
                      (const double*)F(w.tab), part, w.segs);
   WTRY(hipGetLastError());
   // the entity-edge parameters [EE_W11, EC_B2 + 2): one contiguous block of the flat vector
@@ -2779,13 +2794,6 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_node_bwd, dim3(te, B), dim3(NT), 0, st, prep, bt->x, params, o, Ne, Nc,
                        F(w.dn), F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 0,
-                       F(w.rhoE), nullptr, (double*)F(w.tab));
-    WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<0>, dim3(te, B), dim3(NT), tlds, st, bt->x, bt->abits, prep,
-                       params, o, Ne, Nc, F(w.rhoE), F(w.rhoE), (const double*)F(w.tab), part,
-                       w.segs);
-    WTRY(hipGetLastError());
   }
   if (ee) {
     const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
@@ -2797,12 +2805,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
                        F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
-                       nullptr, F(w.psi), (double*)F(w.tab));
+  }
+  if (ent || ee) {   // the first-layer backward of both stages: one scan, one launch
+    const int mode0 = ent ? 0 : 1, stages = (ent && ee) ? 2 : 1;
+    hipLaunchKernelGGL(kw_scan, dim3(H, B, stages), dim3(NT), 0, st, prep, params, o, Ne, Nc,
+                       mode0, F(w.rhoE), F(w.psi), (double*)F(w.tab));
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), tlds, st, bt->x, bt->abits, prep,
-                       params, o, Ne, Nc, F(w.phi), F(w.psi), (const double*)F(w.tab), part,
-                       w.segs);
+    hipLaunchKernelGGL(kw_first_bwd, dim3(te, B, stages), dim3(NT), tlds, st, bt->x, bt->abits,
+                       prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi), F(w.psi),
+                       (const double*)F(w.tab), part, w.segs);
     WTRY(hipGetLastError());
   }
   if (adam) {
