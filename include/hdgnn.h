@@ -51,7 +51,9 @@ typedef struct hdg_shape {
 } hdg_shape;
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
- * with ne <= 256, nc <= 160 (the benchmark shape).  GENERAL: one launch per phase, many
+ * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge
+ * stage runs on the GENERAL path's kernels around the fused step kernel, so its prepared
+ * tables and workspace hold both paths' parts).  GENERAL: one launch per phase, many
  * blocks per commit, state in HBM; every variant and shape.  AUTO picks FUSED when it
  * applies.  hdg_prep_bytes / hdg_workspace_bytes depend on the path. */
 #define HDG_PATH_AUTO 0
