@@ -1790,7 +1790,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       const unsigned long long* pr = ncpart + (size_t)b * ncpt * 2 * Nc;
       for (int e = t; e < 2 * Nc; e += NT_MID) {
         unsigned long long a = 0ull;
-        for (int tl = 0; tl < ncpt; ++tl) a += pr[(size_t)tl * 2 * Nc + e];
+        for (int tl = 0; tl < ncpt; tl += 8) {   // 8 tiles' loads in flight (integer sum:
+          unsigned long long v[8];               // any order gives the same bits)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = tl + u < ncpt ? pr[(size_t)(tl + u) * 2 * Nc + e] : 0ull;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) a += v[u];
+        }
         nb[4 * (e >> 1) + 2 + (e & 1)] = (float)((double)a * (1.0 / 4294967296.0));
       }
     } else {
