@@ -1946,8 +1946,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     divmod_bf(t, Nc1i, invNc1, r, qq);
     const int dr = NT_MID / Nc1i, dqq = NT_MID - dr * Nc1i;
     const int npad = NC16 - Nc;
-    if (TRAIN && GAML && npad > 0) {   // gamma's padding columns [Nc, NC16) of the own rows:
-                                       // pass B reads LDS gamma rows unmasked
+    if (TRAIN && npad > 0) {   // gamma's padding columns [Nc, NC16) of the own rows:
+                               // pass B reads the gamma rows unmasked (GFULL)
       for (int e = t; e < ((Nc - radd + rmul - 1) / rmul) * npad; e += NT_MID) {
         const int r2 = e / npad;
         gam[(rmul * r2 + radd) * GLD + Nc + (e - r2 * npad)] = 0.f;
@@ -2071,7 +2071,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
-  pair_pass<KK_MID, SMAXC, 2, HS, GAML>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
+  pair_pass<KK_MID, SMAXC, 2, HS, true>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
                                            nullptr, gam, GLD, Dsig, Dtau, ysumv, credg, rmul,
                                            radd);
   for (int e = t; e < Nc * HS; e += NT_MID) {
