@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
-    ap.add_argument("--graph-steps", type=int, default=10,
+    ap.add_argument("--graph-steps", type=int, default=50,
                     help="training steps captured per HIP graph (a divisor of --steps)")
     ap.add_argument("--variant", type=int, default=2, choices=(1, 2, 3, 4),
                     help="model_<variant>.py (the BASELINE metric is model_2)")
