@@ -2332,7 +2332,7 @@ __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ p
   if (lane == 0) out[blockIdx.x] = a;
 }
 
-// kw_reduce_adam  grid (np + HDG_TRAILER), one wave per slot: kw_grad_reduce fused with
+// kw_reduce_adam  (grid below): kw_grad_reduce fused with
 // k_adam_tf for a single-process training step (hdg_train_step on the general path and on
 // the model_4 fused path).  Slots in [seg_lo, seg_hi) are reduced from the partial rows as
 // in kw_grad_reduce; the others (model_4 on the fused path) from the step kernel's
@@ -2342,62 +2342,18 @@ __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ p
 // D_AUX from the pre-update parameters, so no block depends on another; the CE slot's wave
 // writes the loss stats, block 0 the new beta powers.  A fault in the step kernel's rows
 // (a block-pair exchange timed out) skips every update, as in k_adam_tf.
-__device__ __forceinline__ float wave_reduce_rows(const float* src, int rows, int stride,
-                                                  bool count, unsigned long long& c) {
-  const int lane = threadIdx.x;
-  float a = 0.f;
-  c = 0ull;
-  for (int r = lane; r < rows; r += 64) {
-    const float v = src[(size_t)r * stride];
-    if (count) c += (unsigned long long)v;
-    else a += v;
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
-  return wsum(a);
-}
 
-__global__ __launch_bounds__(64) void kw_reduce_adam(
-    const float* __restrict__ part, Segs sg, int np, int seg_lo, int seg_hi, FusedRows fr,
-    float* __restrict__ grad, float* __restrict__ params, float* __restrict__ mm,
-    float* __restrict__ vv, float* __restrict__ bpow, const float* __restrict__ D, float lr,
-    float inv_pairs, float* __restrict__ stats) {
-  const int p = blockIdx.x, lane = threadIdx.x;
-  const int pc = np + HDG_TR_COUNT;
-  if (p > pc && p <= pc + 2) return;              // written by the count slot's wave
-  const bool seg = p >= seg_lo && p < seg_hi;
-  // the update's operands first: their latency overlaps the reduction
-  const bool isp = p < np;
-  const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
-  unsigned long long c = 0ull;
-  float fault = 0.f;
-  if (fr.fp) {
-    unsigned long long cf;
-    fault = wave_reduce_rows(fr.fp + fr.f_np + HDG_TR_FAULT, fr.frows, fr.fstride, false, cf);
-  }
-  float g;
-  if (seg) {
-    float a = 0.f;
-    for (int q = 0; q < sg.count; ++q) {
-      const Seg& sgq = sg.s[q];
-      if (sgq.n > 0 && p >= sgq.p0 && p < sgq.p0 + sgq.n) {
-        const float* src = part + sgq.off + (long long)(p - sgq.p0) * sgq.rows;
-        if (p == pc)
-          for (int r = lane; r < sgq.rows; r += 64) c += (unsigned long long)src[r];
-        else
-          for (int r = lane; r < sgq.rows; r += 64) a += src[r];
-        break;
-      }
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
-    g = wsum(a);
-  } else {
-    const int p2 = p < fr.f_at ? p : p - fr.f_shift;
-    g = wave_reduce_rows(fr.fp + p2, fr.frows, fr.fstride, p == pc, c);
-  }
-  if (lane != 0) return;
-  if (p == pc) {
+// one slot's reduced value: the gradient out (the count slot as three 16-bit parts), the
+// stats on the CE slot, and TF1 ApplyAdam on a parameter slot
+__device__ __forceinline__ void reduce_adam_slot(int p, int np, float g, unsigned long long c,
+                                                 float w, float m0, float v0, bool fault,
+                                                 float* __restrict__ grad,
+                                                 float* __restrict__ params,
+                                                 float* __restrict__ mm, float* __restrict__ vv,
+                                                 float* __restrict__ bpow,
+                                                 const float* __restrict__ D, float lr,
+                                                 float inv_pairs, float* __restrict__ stats) {
+  if (p == np + HDG_TR_COUNT) {
     grad[p] = (float)(c & 0xFFFFull);
     grad[p + 1] = (float)((c >> 16) & 0xFFFFull);
     grad[p + 2] = (float)(c >> 32);
@@ -2411,7 +2367,7 @@ __global__ __launch_bounds__(64) void kw_reduce_adam(
     stats[2] = D[D_AUX + 0];
     stats[3] = 10.f * ce + 0.1f * D[D_AUX + 1] + D[D_AUX + 0];
   }
-  if (!isp || fault != 0.f) return;
+  if (p >= np || fault) return;
   const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
   const int TH1 = np - 4, TH2 = np - 2;
   float gg = g + 0.001f * w;
@@ -2427,6 +2383,89 @@ __global__ __launch_bounds__(64) void kw_reduce_adam(
     bpow[0] = D[D_AUX + 5];
     bpow[1] = D[D_AUX + 6];
   }
+}
+
+// grid (nfb + nsb), 256 threads.  Blocks [0, nfb): 16 consecutive slots of the step
+// kernel's rows (fr, model_2 layout p2, mapped to the model_4 slot p) x 16 row phases, so
+// each row's 16 slots are one 64-byte read; blocks [nfb, nfb + nsb): one wave per slot of
+// [seg_lo, seg_hi) over its segment rows (contiguous per slot).
+__global__ __launch_bounds__(NT) void kw_reduce_adam(
+    const float* __restrict__ part, Segs sg, int np, int seg_lo, int seg_hi, int nfb,
+    FusedRows fr, float* __restrict__ grad, float* __restrict__ params, float* __restrict__ mm,
+    float* __restrict__ vv, float* __restrict__ bpow, const float* __restrict__ D, float lr,
+    float inv_pairs, float* __restrict__ stats) {
+  __shared__ float rs[16][17];
+  __shared__ unsigned long long rc[16];
+  __shared__ int fl[1];
+  const int t = threadIdx.x, lane = t & 63;
+  const int pc = np + HDG_TR_COUNT;
+  bool fault = false;
+  if (fr.fp) {   // the step kernel's fault slot: any block-pair exchange timed out
+    if (t == 0) fl[0] = 0;
+    __syncthreads();
+    bool bad = false;
+    for (int r = t; r < fr.frows; r += NT)
+      bad |= fr.fp[(size_t)r * fr.fstride + fr.f_np + HDG_TR_FAULT] != 0.f;
+    if (bad) fl[0] = 1;
+    __syncthreads();
+    fault = fl[0] != 0;
+  }
+  if ((int)blockIdx.x < nfb) {
+    const int sl = t & 15, ph = t >> 4;
+    const int p2 = blockIdx.x * 16 + sl;
+    const int GL = fr.f_np + HDG_TRAILER;
+    const int p = p2 < fr.f_at ? p2 : p2 + fr.f_shift;
+    const bool ok = p2 < GL;
+    const bool isc = p == pc;
+    const bool isp = ok && ph == 0 && p < np;
+    const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
+    float a = 0.f;
+    unsigned long long c = 0ull;
+    if (ok)
+      for (int r = ph; r < fr.frows; r += 16) {
+        const float v = fr.fp[(size_t)r * fr.fstride + p2];
+        if (isc) c += (unsigned long long)v;
+        else a += v;
+      }
+    rs[ph][sl] = a;
+    if (isc) rc[ph] = c;
+    __syncthreads();
+    if (ph == 0 && ok && !(p > pc && p <= pc + 2)) {   // count parts: the count slot's thread
+      float g = 0.f;
+      unsigned long long cc = 0ull;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) g += rs[q][sl];     // fixed order
+      if (isc)
+        for (int q = 0; q < 16; ++q) cc += rc[q];
+      reduce_adam_slot(p, np, g, cc, w, m0, v0, fault, grad, params, mm, vv, bpow, D, lr,
+                       inv_pairs, stats);
+    }
+    return;
+  }
+  const int wv = t >> 6;
+  const int p = seg_lo + ((int)blockIdx.x - nfb) * NW + wv;
+  if (p >= seg_hi || (p > pc && p <= pc + 2)) return;   // count parts: the count slot's wave
+  const bool isp = lane == 0 && p < np;
+  const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
+  float a = 0.f;
+  unsigned long long c = 0ull;
+  for (int q = 0; q < sg.count; ++q) {
+    const Seg& sgq = sg.s[q];
+    if (sgq.n > 0 && p >= sgq.p0 && p < sgq.p0 + sgq.n) {
+      const float* src = part + sgq.off + (long long)(p - sgq.p0) * sgq.rows;
+      if (p == pc)
+        for (int r = lane; r < sgq.rows; r += 64) c += (unsigned long long)src[r];
+      else
+        for (int r = lane; r < sgq.rows; r += 64) a += src[r];
+      break;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  const float g = wsum(a);
+  if (lane == 0)
+    reduce_adam_slot(p, np, g, c, w, m0, v0, fault, grad, params, mm, vv, bpow, D, lr, inv_pairs,
+                     stats);
 }
 
 // kw_prep_sort  grid (B), 1024 threads, dynamic LDS 2 Ne floats: stable rank sort of x,
@@ -2675,9 +2714,11 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const int p0 = o.EE_W11, n = o.EC_B2 + 2 - o.EE_W11;
   if (adam) {
     hdg_state* S = adam->state;
-    hipLaunchKernelGGL(kw_reduce_adam, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
-                       o.NP, p0, p0 + n, adam->fused, grad, S->params, S->adam_m, S->adam_v,
-                       S->beta_pow, ws + w.D, adam->lr, adam->inv_pairs, adam->stats);
+    const FusedRows& fr = adam->fused;   // the step kernel's rows: every other slot
+    const int nfb = (fr.f_np + HDG_TRAILER + 15) / 16, nsb = (n + NW - 1) / NW;
+    hipLaunchKernelGGL(kw_reduce_adam, dim3(nfb + nsb), dim3(NT), 0, st, part, w.segs, o.NP,
+                       p0, p0 + n, nfb, fr, grad, S->params, S->adam_m, S->adam_v, S->beta_pow,
+                       ws + w.D, adam->lr, adam->inv_pairs, adam->stats);
   } else {
     hipLaunchKernelGGL(kw_grad_reduce, dim3(n), dim3(64), 0, st, part, w.segs, p0, o.NP,
                        grad + p0);
@@ -2818,8 +2859,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   if (adam) {
     hdg_state* S = adam->state;
-    hipLaunchKernelGGL(kw_reduce_adam, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
-                       o.NP, 0, o.NP + HDG_TRAILER, FusedRows{}, grad, S->params, S->adam_m,
+    const int nsb = (o.NP + HDG_TRAILER + NW - 1) / NW;
+    hipLaunchKernelGGL(kw_reduce_adam, dim3(nsb), dim3(NT), 0, st, part, w.segs, o.NP, 0,
+                       o.NP + HDG_TRAILER, 0, FusedRows{}, grad, S->params, S->adam_m,
                        S->adam_v, S->beta_pow, D, adam->lr, adam->inv_pairs, adam->stats);
   } else {
     hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
