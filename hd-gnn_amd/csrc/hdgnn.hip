@@ -194,6 +194,10 @@ __device__ __forceinline__ void wave_sums(const float (&v)[N], const int lane, F
 
 __device__ __forceinline__ float reluf(float v) { return fmaxf(v, 0.f); }
 
+// padding / masked-row value of the pair-tile operands: far below any real pre-activation
+// but finite, so that z [z > 0] (MODE 0) and [z > 0] w (MODE 1, 2) are 0, never inf * 0
+constexpr float PADNEG = -1e30f;
+
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_* ops)
 
 // [z > 0] for two lanes of a packed pair in ONE VALU op: clamp(z * 2^126, 0, 1) on
@@ -234,7 +238,8 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 //   callers subtract it; MODE 2 masks it)
 // Rows swept: i = rmul * r + radd, r = 0, 1, ... while i < N (a block pair splits the rows
 // by parity: rmul = 2, radd = half); Cout then holds the partial column sums of those rows.
-// A, B, wr, wc, Rout, Cout: LDS [node][LD] (rows/cols >= N padded with -inf in A/B).
+// A, B, wr, wc, Rout, Cout: LDS [node][LD] (rows/cols >= N padded with PADNEG or -inf in
+// A/B; MODE 0 needs the finite PADNEG).
 // Rout may alias A and Cout may alias B (rows are consumed before they are written,
 // columns are written after the closing barrier).  cred: 4*16*SMAX*KK + 8*KK words.
 // Every thread of the BLOCK must call this the same number of times (barriers).
@@ -285,14 +290,14 @@ __device__ __forceinline__ void pair_tile(
     const int i = rmul * r + radd;
     const bool iv = r < nown;
     p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
-    // rows past the sweep read the first swept row and are masked to A = -inf, w = 0
+    // rows past the sweep read the first swept row and are masked to A = PADNEG, w = 0
     // (e = 0): the sweep may run past the padded buffer when the rows are split by parity
     const int ib = iv ? i : radd;       // past the sweep: the first swept row (own, finite)
     const float* Ai = A + ib * LD;
     // masks applied arithmetically (that row's values are finite): every load of the sweep's
     // row operands is unconditional, so none of them is sunk into an exec-masked branch
     // with its own LDS round trip
-    const float addm = iv ? 0.f : -INFINITY, mulm = iv ? 1.f : 0.f;
+    const float addm = iv ? 0.f : PADNEG, mulm = iv ? 1.f : 0.f;
     const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
@@ -329,9 +334,12 @@ __device__ __forceinline__ void pair_tile(
       for (int p = 0; p < KP; ++p) {
         const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
-        p2 e;
         if constexpr (MODE == 0) {
-          e = __builtin_elementwise_max(z, z2);
+          // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
+          // max on gfx950: relu was two scalar v_max plus two packed adds)
+          const p2 sz = step2(z);
+          racc2[p] = __builtin_elementwise_fma(z, sz, racc2[p]);
+          cacc2[c][p] = __builtin_elementwise_fma(z, sz, cacc2[c][p]);
         } else {
           p2 w;
           if constexpr (MODE == 1) {
@@ -339,11 +347,11 @@ __device__ __forceinline__ void pair_tile(
           } else {
             w = (p2){g, g};
           }
-          e = step2(z) * w;
+          const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
+          racc2[p] += e;
+          cacc2[c][p] += e;
         }
-        racc2[p] += e;
-        cacc2[c][p] += e;
       }
       if constexpr (KT) {
         const float z = at + fmaf(af, dkt, Bj[ktl]);
@@ -470,7 +478,7 @@ __device__ __forceinline__ void pair_tile32(
     p2 a2[KP > 0 ? KP : 1], rw2[KP > 0 ? KP : 1], racc2[KP > 0 ? KP : 1];
     const int ib = iv ? i : radd;       // past the sweep: the first swept row (own, finite)
     const float* Ai = A + ib * LD;
-    const float addm = iv ? 0.f : -INFINITY, mulm = iv ? 1.f : 0.f;
+    const float addm = iv ? 0.f : PADNEG, mulm = iv ? 1.f : 0.f;
     const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
@@ -507,9 +515,12 @@ __device__ __forceinline__ void pair_tile32(
       for (int p = 0; p < KP; ++p) {
         const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
-        p2 e;
         if constexpr (MODE == 0) {
-          e = __builtin_elementwise_max(z, z2);
+          // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
+          // max on gfx950: relu was two scalar v_max plus two packed adds)
+          const p2 sz = step2(z);
+          racc2[p] = __builtin_elementwise_fma(z, sz, racc2[p]);
+          cacc2[c][p] = __builtin_elementwise_fma(z, sz, cacc2[c][p]);
         } else {
           p2 w;
           if constexpr (MODE == 1) {
@@ -517,11 +528,11 @@ __device__ __forceinline__ void pair_tile32(
           } else {
             w = (p2){g, g};
           }
-          e = step2(z) * w;
+          const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
+          racc2[p] += e;
+          cacc2[c][p] += e;
         }
-        racc2[p] += e;
-        cacc2[c][p] += e;
       }
       if constexpr (KT) {
         const float z = at + fmaf(af, dkt, Bj[ktl]);
@@ -1860,7 +1871,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
     const float a0 = Ws[H1_W1 + 8 * HS + mk] + Ws[H1_B1 + mk];
     for (int p = msl; p < NC16; p += NSL) {
-      float al = -INFINITY, be = -INFINITY;
+      float al = PADNEG, be = PADNEG;   // finite: MODE 0 accumulates z [z > 0]
       if (p < Nc) {
         const float4 nv = reinterpret_cast<const float4*>(nb)[p];
         al = fmaf(nv.w, wa[3], fmaf(nv.z, wa[2], fmaf(nv.y, wa[1], fmaf(nv.x, wa[0], a0))));
