@@ -1133,10 +1133,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
       const f2 y2 = {yf, yf};
       const float4* o4 = reinterpret_cast<const float4*>(os_ + (m - c0) * H);
 #pragma unroll
-      for (int v = 0; v < H / 4; ++v) {
-        const float4 q = o4[v];
-        acc[2 * v] += relu2(fma2(y2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y}));
-        acc[2 * v + 1] += relu2(fma2(y2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w}));
+      for (int v = 0; v < H / 4; ++v) {   // relu(z) summed as z [z > 0]: step + packed fma
+        const float4 q = o4[v];          // (no packed max on gfx950)
+        const f2 za = fma2(y2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y});
+        const f2 zb = fma2(y2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
+        acc[2 * v] = fma2(za, step2(za), acc[2 * v]);
+        acc[2 * v + 1] = fma2(zb, step2(zb), acc[2 * v + 1]);
       }
     }
   }
@@ -1144,8 +1146,10 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
     const float yf = bitf(brow, ncl);
     const f2 y2 = {yf, yf};
 #pragma unroll
-    for (int kk = 0; kk < H2; ++kk)
-      acc[kk] -= relu2(fma2(y2, dl[kk], ow[kk] + ld2(oth + ncl * H + 2 * kk)));
+    for (int kk = 0; kk < H2; ++kk) {
+      const f2 zs = fma2(y2, dl[kk], ow[kk] + ld2(oth + ncl * H + 2 * kk));
+      acc[kk] -= zs * step2(zs);      // the loop's form: the same value leaves
+    }
   }
   combine8(acc, buf, res);
   float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
@@ -1348,8 +1352,8 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
         const float4 q = o4[v];
         const f2 pa = fma2(y2, ep[2 * v], ow[2 * v] + (f2){q.x, q.y});
         const f2 pb = fma2(y2, ep[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
-        const f2 ea = {pa.x > 0.f ? g : 0.f, pa.y > 0.f ? g : 0.f};
-        const f2 eb = {pb.x > 0.f ? g : 0.f, pb.y > 0.f ? g : 0.f};
+        const f2 ea = step2(pa) * (f2){g, g};   // [p > 0] g (gamma finite, 0 on the diagonal)
+        const f2 eb = step2(pb) * (f2){g, g};
         acc[2 * v] += ea;
         acc[2 * v + 1] += eb;
         ya[2 * v] = fma2(y2, ea, ya[2 * v]);
@@ -1496,8 +1500,8 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
         const f2 pa = fma2(y2, dl[2 * v], ow[2 * v] + (f2){q.x, q.y});
         const f2 pb = fma2(y2, dl[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
         const f2 ga = wo[2 * v] + (f2){r.x, r.y}, gb2 = wo[2 * v + 1] + (f2){r.z, r.w};
-        const f2 da = {pa.x > 0.f ? ga.x : 0.f, pa.y > 0.f ? ga.y : 0.f};
-        const f2 db = {pb.x > 0.f ? gb2.x : 0.f, pb.y > 0.f ? gb2.y : 0.f};
+        const f2 da = step2(pa) * ga;   // [p > 0] g: one packed step + multiply (g finite)
+        const f2 db = step2(pb) * gb2;
         acc[2 * v] += da;
         acc[2 * v + 1] += db;
         ya[2 * v] = fma2(y2, da, ya[2 * v]);
@@ -1512,7 +1516,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
     for (int kk = 0; kk < H2; ++kk) {
       const f2 pr = fma2(y2, dl[kk], ow[kk] + ld2(oth + ncl * H + 2 * kk));
       const f2 gg = wo[kk] + ld2(woth + ncl * H + 2 * kk);
-      const f2 dz = {pr.x > 0.f ? gg.x : 0.f, pr.y > 0.f ? gg.y : 0.f};
+      const f2 dz = step2(pr) * gg;   // the loop's form: the same value leaves
       acc[kk] -= dz;
       ya[kk] -= y2 * dz;
     }
