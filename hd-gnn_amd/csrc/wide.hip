@@ -829,7 +829,7 @@ __device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
 // grid (te (+1), B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage.
 // D != NULL: one more x column whose block (te, 0, 0) runs kw_derive's work (no kernel of
 // its own; nothing here reads D)
-__global__ __launch_bounds__(NT) void kw_ent_fwd(const float* __restrict__ x,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw_ent_fwd(const float* __restrict__ x,
                                                  const uint32_t* __restrict__ abits,
                                                  const uint32_t* __restrict__ aT,
                                                  const uint32_t* __restrict__ prep,
