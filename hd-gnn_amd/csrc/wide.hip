@@ -1180,6 +1180,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float ss[CHM * H];
+  __shared__ __attribute__((aligned(16))) float se[CHM * H];   // sigma + eps (y = 1 rows)
   __shared__ float red[NWP * 23];
   __shared__ float tot[23];
   const int b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
@@ -1190,14 +1191,11 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   const int WC = (Nc + 31) >> 5;
   const int Pc = Nc * (Nc - 1);
   const float* sgb = sig + (size_t)b * Nc * H;
-  f2 tq[H2], ep[H2], u2[H];   // u2[k] = (U2[k][0], U2[k][1])
+  // kappa = (sigma_p + y eps) + tau_q: the y = 1 rows from a second staged table (picked
+  // by address, no per-pair fma); U2 and b2 are wave-uniform scalar loads in the loop
+  f2 tq[H2];
 #pragma unroll
-  for (int kk = 0; kk < H2; ++kk) {
-    tq[kk] = ld2(tau + ((size_t)b * Nc + qc) * H + 2 * kk);
-    ep[kk] = ld2(D + D_EPS + 2 * kk);
-  }
-#pragma unroll
-  for (int k = 0; k < H; ++k) u2[k] = ld2(W + o.H2_W2 + 2 * k);
+  for (int kk = 0; kk < H2; ++kk) tq[kk] = ld2(tau + ((size_t)b * Nc + qc) * H + 2 * kk);
   const f2 bb = ld2(W + o.H2_B2);
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
@@ -1209,25 +1207,26 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
     __syncthreads();
     stage_rows(ss, sgb, c0, c1);
+    for (int e = threadIdx.x; e < (c1 - c0) * H; e += NTP)
+      se[e] = sgb[(size_t)c0 * H + e] + D[D_EPS + e % H];
     __syncthreads();
     int lo, hi;
     wave_share(c0, c1, lo, hi);
     for (int p = lo; p < hi; ++p) {
       const float yf = bitf(ybits + ((size_t)b * Nc + p) * WC, qc);
-      const f2 y2 = {yf, yf};
-      const float4* s4 = reinterpret_cast<const float4*>(ss + (p - c0) * H);
+      const float4* s4 = reinterpret_cast<const float4*>((yf > 0.f ? se : ss) + (p - c0) * H);
       f2 kap[H2];
       f2 zz = bb;
 #pragma unroll
       for (int v = 0; v < H / 4; ++v) {
         const float4 sv = s4[v];
-        kap[2 * v] = relu2(fma2(y2, ep[2 * v], (f2){sv.x, sv.y} + tq[2 * v]));
-        kap[2 * v + 1] = relu2(fma2(y2, ep[2 * v + 1], (f2){sv.z, sv.w} + tq[2 * v + 1]));
+        kap[2 * v] = relu2((f2){sv.x, sv.y} + tq[2 * v]);
+        kap[2 * v + 1] = relu2((f2){sv.z, sv.w} + tq[2 * v + 1]);
       }
 #pragma unroll
       for (int kk = 0; kk < H2; ++kk) {
-        zz = fma2((f2){kap[kk].x, kap[kk].x}, u2[2 * kk], zz);
-        zz = fma2((f2){kap[kk].y, kap[kk].y}, u2[2 * kk + 1], zz);
+        zz = fma2((f2){kap[kk].x, kap[kk].x}, ld2(W + o.H2_W2 + 4 * kk), zz);
+        zz = fma2((f2){kap[kk].y, kap[kk].y}, ld2(W + o.H2_W2 + 4 * kk + 2), zz);
       }
       const float z0 = zz.x, z1 = zz.y;
       if (live && q != p) {
