@@ -6,7 +6,8 @@ A pair whose partner never arrives must fail loudly and leave the model untouche
   * forward-only launches poison the CE sum and the timed-out block's probs / logits rows;
   * training launches poison the CE, set the gradient trailer's fault slot and skip the
     Adam update (parameters, moments and beta powers bitwise unchanged), on the fused
-    single-process path (k_reduce_adam) and on the data-parallel split (k_adam_tf);
+    single-process path (k_reduce_adam; model_4: kw_reduce_adam) and on the
+    data-parallel split (k_adam_tf);
   * the next clean launch is correct again (exchange tags are per launch epoch).
 HDG_DEBUG_XCH_FAULT=1 makes block 1 of every pair send words its partner never accepts,
 so block 0 (the even hunk rows) waits out every exchange (~20 ms each).  GPU only.
@@ -23,12 +24,15 @@ pytestmark = pytest.mark.gpu
 B, NE, NC = 3, 40, 17
 
 
-@pytest.fixture
-def fused_split(monkeypatch):
+@pytest.fixture(params=[2, 4], ids=["model_2", "model_4"])
+def fused_split(monkeypatch, request):
+    """model_4 runs its model_2-shaped part in the same step kernel (the entity-edge stage
+    on general-path kernels around it, the reduction + Adam in kw_reduce_adam)."""
     monkeypatch.setenv("HDG_FUSED_SPLIT", "1")
     from hdgnn.engine import Engine
-    eng = Engine(NE, NC, B, path=_lib.PATH_FUSED)
-    eng.set_params(layout.init_flat(5))
+    v = request.param
+    eng = Engine(NE, NC, B, variant=v, path=_lib.PATH_FUSED)
+    eng.set_params(layout.init_flat(5, v))
     return eng, eng.upload(synth_commits(B, NE, NC, 7))
 
 
@@ -75,7 +79,7 @@ def test_train_timeout_skips_update(fused_split, monkeypatch):
     eng, db = fused_split
     before = _state(eng)
     monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
-    eng.train_step(db)                               # hdg_train_step: k_reduce_adam
+    eng.train_step(db)                      # hdg_train_step: k_reduce_adam / kw_reduce_adam
     torch.cuda.synchronize()
     for a, b in zip(before, _state(eng)):
         assert torch.equal(a, b)
@@ -102,8 +106,8 @@ def test_train_timeout_skips_update(fused_split, monkeypatch):
     torch.cuda.synchronize()
     eng.check_status()
     from hdgnn.engine import Engine
-    ref = Engine(NE, NC, B, path=_lib.PATH_FUSED)
-    ref.set_params(layout.init_flat(5))
+    ref = Engine(NE, NC, B, variant=eng.variant, path=_lib.PATH_FUSED)
+    ref.set_params(layout.init_flat(5, eng.variant))
     ref.train_step(ref.upload(synth_commits(B, NE, NC, 7)))
     torch.cuda.synchronize()
     assert torch.equal(eng.params, ref.params)
