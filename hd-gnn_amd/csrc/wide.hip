@@ -258,6 +258,24 @@ __host__ __device__ inline GenPrep gen_prep(int Ne, int Nc) {
   return G;
 }
 
+// neighbour id lists (kw_prep_lists), past the per-commit words, aT and yT: counts u32
+// [2][B][Ne] (side 0: row bits of a, 1: column bits), ids u16 [2][B][Ne][LS] -- the j != i
+// with a_ij = 1 (side 0) / a_ji = 1 (side 1) ascending, padded to a multiple of 4 with the
+// sentinel Ne.  Offsets in 4-byte words from the prep base.
+__host__ __device__ inline int list_stride(int Ne) { return (Ne + 3) & ~3; }
+struct ListLayout {
+  size_t cnt, ids, end;
+};
+__host__ __device__ inline ListLayout list_layout(int B, int Ne, int Nc) {
+  const size_t WE = (Ne + 31) / 32, WC = (Nc + 31) / 32;
+  ListLayout L;
+  L.cnt = ((size_t)B * gen_prep(Ne, Nc).words + (size_t)B * Ne * WE + (size_t)B * Nc * WC + 3) &
+          ~(size_t)3;
+  L.ids = L.cnt + ((2 * (size_t)B * Ne + 3) & ~(size_t)3);
+  L.end = L.ids + (size_t)B * Ne * list_stride(Ne);     // 2 sides x LS/2 words
+  return L;
+}
+
 // per-block partial gradient rows: segment s holds n consecutive parameters starting at
 // flat index p0, laid out [n][rows] at part + off
 constexpr int MAXSEG = 16;
@@ -528,8 +546,11 @@ __device__ __forceinline__ SortTabs stage_tabs(const uint32_t* prep, const GenPr
     cum[e] = G.cum[e];
     if (e < G.nd) xu[e] = G.xu[e];
   }
-  if (xg)   // the neighbour walks read x_j from LDS, not one dependent HBM load each
+  if (xg) {  // the neighbour walks read x_j from LDS, not one dependent HBM load each;
+             // xs[Ne] = NaN for the lists' sentinel (a clamped fma turns it into 0)
     for (int e = threadIdx.x; e < Ne; e += blockDim.x) xs[e] = xg[e];
+    if (threadIdx.x == 0) xs[Ne] = __builtin_nanf("");
+  }
   __syncthreads();
   SortTabs T;
   T.xu = xu;
@@ -542,7 +563,7 @@ __device__ __forceinline__ SortTabs stage_tabs(const uint32_t* prep, const GenPr
 
 __host__ __device__ inline size_t sort_lds_bytes(int Ne) {
   const size_t NE4 = (Ne + 3) & ~3;
-  return (NE4 + 4) * 8 + (NE4 + 4) * 4 + 2 * NE4 * 4;   // pxd, cum, xu, x
+  return (NE4 + 4) * 8 + (NE4 + 4) * 4 + (2 * NE4 + 4) * 4;   // pxd, cum, xu, x (+ sentinel)
 }
 
 __device__ __forceinline__ int top_pow2(int n) { return 1 << (31 - __builtin_clz((unsigned)n)); }
@@ -559,17 +580,25 @@ __device__ __forceinline__ int set_bound(const SortTabs& T, bool inc, P pred) {
   return q;
 }
 
-// walk the set bits j != i of a bit row: f(j)
+// walk node i's neighbour id list (list_layout; side 0: a_ij = 1, 1: a_ji = 1) four ids per
+// 8-byte load: f(j) for each id of a group, the sentinel Ne included (callers make it a
+// zero term).  One independent group of loads per trip instead of a bit walk whose trip
+// count is the set bits of every word.
 template <class F>
-__device__ __forceinline__ void for_bits(const uint32_t* row, int WE, int i, F f) {
-  for (int w = 0; w < WE; ++w) {
-    uint32_t m = row[w];
-    if ((i >> 5) == w) m &= ~(1u << (i & 31));
-    while (m) {
-      const int j = 32 * w + __builtin_ctz(m);
-      m &= m - 1u;
-      f(j);
-    }
+__device__ __forceinline__ void for_list(const uint32_t* prep, int side, int b, int i, int Ne,
+                                         int Nc, F f) {
+  const int B = gridDim.y, LS = list_stride(Ne);
+  const ListLayout L = list_layout(B, Ne, Nc);
+  const size_t r = ((size_t)side * B + b) * Ne + i;
+  const int n = (int)prep[L.cnt + r];
+  const uint2* ids = reinterpret_cast<const uint2*>(
+      reinterpret_cast<const uint16_t*>(prep + L.ids) + r * LS);
+  for (int k = 0; k < n; k += 4) {
+    const uint2 q = ids[k >> 2];
+    f((int)(q.x & 0xffffu));
+    f((int)(q.x >> 16));
+    f((int)(q.y & 0xffffu));
+    f((int)(q.y >> 16));
   }
 }
 
@@ -618,11 +647,8 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
   const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
   if (i >= Ne) return;   // no barriers below
-  const int WE = (Ne + 31) >> 5;
   const float* xb = T.xs;
   const float xi = xb[i];
-  const uint32_t* rowb = abits + ((size_t)b * Ne + i) * WE;
-  const uint32_t* colb = aT + ((size_t)b * Ne + i) * WE;
   float u[KPW], v[KPW], s1[KPW], s2[KPW], c0[KPW], wa[KPW], wb[KPW], dd[KPW];
   double dense[KPW], dense2[KPW];
 #pragma unroll
@@ -688,13 +714,13 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
     rat = q[4].ca; rbt = q[4].cb; cat = qc[4].ca; cbt = qc[4].cb;
     f2 sr[2] = {(f2){0.f, 0.f}, (f2){0.f, 0.f}}, sc[2] = {sr[0], sr[1]};
     float srt = 0.f, sct = 0.f;
-    for_bits(rowb, WE, i, [&](int j) {
+    for_list(prep, 0, b, i, Ne, Nc, [&](int j) {   // xb[Ne] = NaN: clamps to 0
       const float xj = xb[j];
       sr[0] += clamp_fma2(xj, ra[0], rb2[0]);
       sr[1] += clamp_fma2(xj, ra[1], rb2[1]);
       srt += clamp_fma1(xj, rat, rbt);
     });
-    for_bits(colb, WE, i, [&](int j) {
+    for_list(prep, 1, b, i, Ne, Nc, [&](int j) {
       const float xj = xb[j];
       sc[0] += clamp_fma2(xj, ca[0], cb[0]);
       sc[1] += clamp_fma2(xj, ca[1], cb[1]);
@@ -1776,7 +1802,6 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
   const int i = t0 + lane;
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
-  const int WE = (Ne + 31) >> 5;
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
   const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
   const float* xb = T.xs;
@@ -1840,7 +1865,11 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       s32[h] = (f2){0.f, 0.f};
     }
     float cst = 0.f, s1t = S1[4], s3t = 0.f;
-    for_bits(abits + ((size_t)b * Ne + i) * WE, WE, i, [&](int j) {
+    for_list(prep, 0, b, i, Ne, Nc, [&](int j0) {
+      // the sentinel Ne reads node 0's row with gg = 0: every term below vanishes
+      const bool ok = j0 < Ne;
+      const int j = ok ? j0 : 0;
+      const float vm = ok ? 1.f : 0.f;
       const float xj = xb[j];
       const float* qj = rbb + (size_t)j * H + g * KPW;
       const f2 xx = {xj, xj};
@@ -1848,7 +1877,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       for (int h = 0; h < 2; ++h) {
         const f2 z0 = MODE == 0 ? u2[h] + xx * wb2[h] : fma2(xx, wb2[h], u2[h]);
         const f2 z1 = z0 + dd2[h];
-        const f2 gg = ri2[h] + (f2){qj[2 * h], qj[2 * h + 1]};   // finite
+        const f2 gg = (ri2[h] + (f2){qj[2 * h], qj[2 * h + 1]}) * vm;   // finite
         const f2 m1 = step2(z1) * gg, m0 = step2(z0) * gg;
         const f2 dm = m1 - m0;
         cs2[h] += dm;
@@ -1857,7 +1886,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       }
       const float z0 = MODE == 0 ? u[4] + xj * wb[4] : fmaf(xj, wb[4], u[4]);
       const float z1 = z0 + dd[4];
-      const float gg = ri[4] + qj[4];
+      const float gg = ok ? ri[4] + qj[4] : 0.f;
       const float m1 = z1 > 0.f ? gg : 0.f, m0 = z0 > 0.f ? gg : 0.f;
       const float dm = m1 - m0;
       cst += dm;
@@ -2534,6 +2563,42 @@ __global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
   }
 }
 
+// kw_prep_lists  grid (ceil(Ne/4), B, 2), one wave per node and side: the set bits j != i of
+// the node's a row (side 0) / aT row (side 1) as ascending u16 ids (list_layout); the wave
+// scans the words' popcounts for each lane's write offset, then pads to 4 with Ne
+__global__ __launch_bounds__(NT) void kw_prep_lists(const uint32_t* __restrict__ abits,
+                                                    const uint32_t* __restrict__ aT,
+                                                    uint32_t* __restrict__ prep, int Ne, int Nc) {
+  const int lane = threadIdx.x & 63, i = blockIdx.x * NW + (threadIdx.x >> 6);
+  const int b = blockIdx.y, side = blockIdx.z, B = gridDim.y;
+  if (i >= Ne) return;
+  const int WE = (Ne + 31) >> 5, LS = list_stride(Ne);
+  const ListLayout L = list_layout(B, Ne, Nc);
+  const size_t r = ((size_t)side * B + b) * Ne + i;
+  const uint32_t* row = (side ? aT : abits) + ((size_t)b * Ne + i) * WE;
+  uint16_t* out = reinterpret_cast<uint16_t*>(prep + L.ids) + r * LS;
+  int base = 0;
+  for (int w0 = 0; w0 < WE; w0 += 64) {
+    const int w = w0 + lane;
+    uint32_t m = w < WE ? row[w] : 0u;
+    if (w == (i >> 5)) m &= ~(1u << (i & 31));
+    const int pc = __builtin_popcount(m);
+    int incl = pc;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    int pos = base + incl - pc;
+    while (m) {
+      out[pos++] = (uint16_t)(32 * w + __builtin_ctz(m));
+      m &= m - 1u;
+    }
+    base += __shfl(incl, 63);
+  }
+  for (int e = base + lane; e < ((base + 3) & ~3); e += 64) out[e] = (uint16_t)Ne;
+  if (lane == 0) prep[L.cnt + r] = (uint32_t)base;
+}
+
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
@@ -2741,6 +2806,7 @@ void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, i
 
 size_t wide_prep_bytes(const hdg_shape* s) {
   const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
+  if (has_ent(s->variant)) return list_layout(s->batch, s->ne, s->nc).end * 4;
   return (B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
 }
 
@@ -2756,6 +2822,11 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_prep_T, dim3(4, s->batch), dim3(NT), 0, st, bt->ybits, yT, s->nc);
   WTRY(hipGetLastError());
+  if (has_ent(s->variant)) {   // the entity walks' neighbour lists
+    hipLaunchKernelGGL(kw_prep_lists, dim3((s->ne + NW - 1) / NW, s->batch, 2), dim3(NT), 0, st,
+                       bt->abits, aT, (uint32_t*)bt->prep, s->ne, s->nc);
+    WTRY(hipGetLastError());
+  }
   return 0;
 }
 
