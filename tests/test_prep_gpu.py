@@ -64,3 +64,36 @@ def test_count_tables_bit_exact(B, ne, nc, variant, path):
     np.testing.assert_array_equal(ks, eks)
     np.testing.assert_array_equal(kt, ekt)
     np.testing.assert_array_equal(ncst, encst.astype(np.float32))
+
+
+@pytest.mark.parametrize("B,ne,nc,variant", [
+    (3, 24, 10, 2), (3, 37, 12, 4), (4, 200, 74, 4), (2, 1024, 512, 2), (3, 5, 3, 2)])
+def test_neighbour_lists_bit_exact(B, ne, nc, variant):
+    """The general path's per-node neighbour id lists (wide.hip kw_prep_lists: side 0 the
+    j != i with a_ij = 1, side 1 the j with a_ji = 1, ascending, padded to 4 with the
+    sentinel ne) against the adjacency, including a full and an empty commit."""
+    cb = synth_commits(B, ne, nc, 5 + ne)
+    cb.a[0] = 1                      # full adjacency, diagonal included (lists skip j == i)
+    cb.a[1] = 0
+    db = cb.to_device("cuda:0", variant, _lib.PATH_GENERAL)
+    lib = _lib.load()
+    sh = _lib.Shape(B, ne, nc, variant, B, _lib.PATH_GENERAL)
+    st, ks, kt, nco = (ctypes.c_int64() for _ in range(4))
+    _lib.check(lib.hdg_prep_counts_layout(ctypes.byref(sh), ctypes.byref(st), ctypes.byref(ks),
+                                          ctypes.byref(kt), ctypes.byref(nco)))
+    we, wc, ls = (ne + 31) // 32, (nc + 31) // 32, (ne + 3) & ~3
+    c0 = (B * st.value + B * ne * we + B * nc * wc + 3) & ~3
+    i0 = c0 + ((2 * B * ne + 3) & ~3)
+    words = db.prep.cpu().numpy().view(np.uint32)
+    assert words.size >= i0 + B * ne * ls
+    cnt = words[c0:c0 + 2 * B * ne].reshape(2, B, ne)
+    ids = words[i0:i0 + B * ne * ls].copy().view(np.uint16).reshape(2, B, ne, ls)
+    for side, adj in ((0, cb.a), (1, cb.a.transpose(0, 2, 1))):
+        for b in range(B):
+            for i in range(ne):
+                exp = np.flatnonzero(adj[b, i])
+                exp = exp[exp != i]
+                n = len(exp)
+                assert cnt[side, b, i] == n, (side, b, i)
+                np.testing.assert_array_equal(ids[side, b, i, :n], exp)
+                assert (ids[side, b, i, n:(n + 3) & ~3] == ne).all()
