@@ -2695,6 +2695,8 @@ int set_wide_attrs() {
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<false>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_clsb,      // 41 KiB static + 32 KiB at Ne 4096
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     attr_set = true;
   }
   return 0;

@@ -282,3 +282,10 @@ def test_on_device_correct_count(v, path):
     torch.cuda.synchronize()
     want = metrics.top_acc_count(onehot_relations(cb.y), eng.probs.cpu().numpy())
     assert eng.correct_count() == want
+
+
+@pytest.mark.parametrize("v", [2, 4])
+def test_max_shape_matches_oracle(v):
+    """The general path's upper limit Ne = 4096 (largest dynamic LDS of the entity and
+    entity-edge kernels, 13-word neighbour lists of 4096 ids, a^T tiles of 128 words)."""
+    _run_and_check(synth_commits(1, 4096, 40, 3), v, 3)
