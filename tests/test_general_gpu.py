@@ -289,3 +289,10 @@ def test_max_shape_matches_oracle(v):
     """The general path's upper limit Ne = 4096 (largest dynamic LDS of the entity and
     entity-edge kernels, 13-word neighbour lists of 4096 ids, a^T tiles of 128 words)."""
     _run_and_check(synth_commits(1, 4096, 40, 3), v, 3)
+
+
+@pytest.mark.parametrize("v", [1, 4])
+def test_max_classes_matches_oracle(v):
+    """The general path's class limit Nc = 2048 (hunk pair passes over 2048 x 2047
+    relations, 64-word y rows, u16 count tables)."""
+    _run_and_check(synth_commits(1, 40, 2048, 4), v, 4)
