@@ -71,7 +71,8 @@ typedef struct hdg_batch {
     const int32_t*  nlen;   /* [B] n = len(readlines()[:Ne]) of the commit's index file   */
     void*           prep;   /* hdg_prep_bytes(shape) of device scratch, filled once per
                                uploaded batch by hdg_prepare (sorted x, transposed bits,
-                               cross-graph count matrices); read by every step after    */
+                               cross-graph count matrices, per-node neighbour id lists);
+                               read by every step after                                 */
 } hdg_batch;
 
 /* Adam / parameter state (all device, fp32). */
