@@ -584,17 +584,19 @@ __device__ __forceinline__ int set_bound(const SortTabs& T, bool inc, P pred) {
 // 8-byte load: f(j) for each id of a group, the sentinel Ne included (callers make it a
 // zero term).  One independent group of loads per trip instead of a bit walk whose trip
 // count is the set bits of every word.
+// part / nparts: this caller's share of the list's 4-id groups (contiguous, in order).
 template <class F>
 __device__ __forceinline__ void for_list(const uint32_t* prep, int side, int b, int i, int Ne,
-                                         int Nc, F f) {
+                                         int Nc, F f, int part = 0, int nparts = 1) {
   const int B = gridDim.y, LS = list_stride(Ne);
   const ListLayout L = list_layout(B, Ne, Nc);
   const size_t r = ((size_t)side * B + b) * Ne + i;
-  const int n = (int)prep[L.cnt + r];
+  const int ng = ((int)prep[L.cnt + r] + 3) >> 2;
   const uint2* ids = reinterpret_cast<const uint2*>(
       reinterpret_cast<const uint16_t*>(prep + L.ids) + r * LS);
-  for (int k = 0; k < n; k += 4) {
-    const uint2 q = ids[k >> 2];
+  const int g1 = (ng * (part + 1)) / nparts;
+  for (int gq = (ng * part) / nparts; gq < g1; ++gq) {
+    const uint2 q = ids[gq];
     f((int)(q.x & 0xffffu));
     f((int)(q.x >> 16));
     f((int)(q.y & 0xffffu));
@@ -1794,11 +1796,14 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
                                                int Nc, const float* __restrict__ ra,
                                                const float* __restrict__ rb,
                                                const double* __restrict__ tab,
-                                               float* __restrict__ part, const Segs& sg) {
+                                               float* __restrict__ part, const Segs& sg,
+                                               float* hand) {
 #pragma clang fp contract(off)
   const GenPrep GP = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x, B = gridDim.y;
-  const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
+  // 8 waves: wave g + 4 hw takes hidden units g; the halves hw split each lane's neighbour
+  // list (hw 1 hands its partial sums over through LDS), hw 0 also does the dense part
+  const int lane = threadIdx.x & 63, g = uni((threadIdx.x >> 6) & 3), hw = uni(threadIdx.x >> 8);
   const int i = t0 + lane;
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
@@ -1825,6 +1830,11 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     }
     wb[kk] = slope;
     ri[kk] = ra[((size_t)b * Ne + ic) * H + k];
+    S0[kk] = 0.f;                                 // x_i-weighted corrections only
+    S1[kk] = 0.f;
+    S2[kk] = 0.f;
+    S3[kk] = 0.f;
+    if (hw) continue;                             // the dense part: hw 0
     const float uu = u[kk];
     const bool inc = slope >= 0.f;
     const int br = MODE == 0
@@ -1845,8 +1855,6 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     }
     S2[kk] = (float)gs;
     S1[kk] = (float)gx;
-    S0[kk] = 0.f;                                 // x_i-weighted corrections only
-    S3[kk] = 0.f;
   }
   float cs[KPW];                                  // sum of the corrections' dm
 #pragma unroll
@@ -1892,7 +1900,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       cst += dm;
       s1t = fmaf(xj, dm, s1t);
       s3t += m1;
-    });
+    }, hw, 2);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       cs[2 * h] = cs2[h].x; cs[2 * h + 1] = cs2[h].y;
@@ -1900,6 +1908,23 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       S3[2 * h] = s32[h].x; S3[2 * h + 1] = s32[h].y;
     }
     cs[4] = cst; S1[4] = s1t; S3[4] = s3t;
+  }
+  float* hd = hand + g * 3 * KPW * TN + lane;     // hw 1's sums, added in a fixed order
+  if (hw) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      hd[kk * TN] = cs[kk];
+      hd[(KPW + kk) * TN] = S1[kk];
+      hd[(2 * KPW + kk) * TN] = S3[kk];
+    }
+  }
+  __syncthreads();
+  if (hw) return;                                 // no barriers below
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    cs[kk] += hd[kk * TN];
+    S1[kk] += hd[(KPW + kk) * TN];
+    S3[kk] += hd[(2 * KPW + kk) * TN];
   }
   float v[4 * KPW];
 #pragma unroll
@@ -1938,7 +1963,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
 
 // grid (te, B, stages): stage mode0 + z -- 0: E1 (ra = rb = rho_E), 1: EE (phi, psi); both
 // stages of model_4's general path in one launch
-__global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
+__global__ __launch_bounds__(NTP) void kw_first_bwd(const float* __restrict__ x,
                                                    const uint32_t* __restrict__ abits,
                                                    const uint32_t* __restrict__ prep,
                                                    const float* __restrict__ W, Off o, int Ne,
@@ -1947,10 +1972,11 @@ __global__ __launch_bounds__(NT) void kw_first_bwd(const float* __restrict__ x,
                                                    const float* __restrict__ psi,
                                                    const double* __restrict__ tab,
                                                    float* __restrict__ part, Segs sg) {
+  __shared__ float hand[NW * 3 * KPW * TN];        // hw 1's walk sums [g][3 KPW][lane]
   if (mode0 + (int)blockIdx.z == 0)
-    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg);
+    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg, hand);
   else
-    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg);
+    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg, hand);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2689,8 +2715,8 @@ int set_wide_attrs() {
   if (!attr_set) {
     WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
                              96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,    // + 15 KiB static hand-over
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<true>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<false>,
@@ -2776,7 +2802,7 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
                      F(w.psi), (double*)F(w.tab));
   WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+  hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NTP), sort_lds_bytes(Ne), st, bt->x,
                      bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
                      (const double*)F(w.tab), part, w.segs);
   WTRY(hipGetLastError());
@@ -2928,7 +2954,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_scan, dim3(H, B, stages), dim3(NT), 0, st, prep, params, o, Ne, Nc,
                        mode0, F(w.rhoE), F(w.psi), (double*)F(w.tab));
     WTRY(hipGetLastError());
-    hipLaunchKernelGGL(kw_first_bwd, dim3(te, B, stages), dim3(NT), tlds, st, bt->x, bt->abits,
+    hipLaunchKernelGGL(kw_first_bwd, dim3(te, B, stages), dim3(NTP), tlds, st, bt->x, bt->abits,
                        prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi), F(w.psi),
                        (const double*)F(w.tab), part, w.segs);
     WTRY(hipGetLastError());
