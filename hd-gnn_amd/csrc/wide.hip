@@ -1202,7 +1202,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
 // ---------------------------------------------------------------------------------
 template <bool TRAIN>
 __global__ __launch_bounds__(NTP) void kw_hunk_cls(
-    const uint32_t* __restrict__ ybits, const float* __restrict__ W, Off o,
+    const uint32_t* __restrict__ yT, const float* __restrict__ W, Off o,
     const float* __restrict__ D, int Nc, const float* __restrict__ sig,
     const float* __restrict__ tau, float* __restrict__ probs, float* __restrict__ logits,
     float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
@@ -1219,6 +1219,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   const int WC = (Nc + 31) >> 5;
   const int Pc = Nc * (Nc - 1);
   const float* sgb = sig + (size_t)b * Nc * H;
+  const uint32_t* ycol = yT + ((size_t)b * Nc + qc) * WC;   // bit p: y_pq (p != q)
   // kappa = (sigma_p + y eps) + tau_q: the y = 1 rows from a second staged table (picked
   // by address, no per-pair fma); U2 and b2 are wave-uniform scalar loads in the loop
   f2 tq[H2];
@@ -1240,8 +1241,11 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     __syncthreads();
     int lo, hi;
     wave_share(c0, c1, lo, hi);
-    for (int p = lo; p < hi; ++p) {
-      const float yf = bitf(ybits + ((size_t)b * Nc + p) * WC, qc);
+    int wi = -1;
+    uint32_t word = 0;
+    for (int p = lo; p < hi; ++p) {   // y_pq from the lane's y^T row: one load per 32 rows
+      if ((p >> 5) != wi) { wi = p >> 5; word = ycol[wi]; }
+      const float yf = ((word >> (p & 31)) & 1u) ? 1.f : 0.f;
       const float4* s4 = reinterpret_cast<const float4*>((yf > 0.f ? se : ss) + (p - c0) * H);
       f2 kap[H2];
       f2 zz = bb;
@@ -2907,7 +2911,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   float* probs = out ? out->probs : nullptr;
   float* logits = out ? out->logits : nullptr;
   if (!train) {
-    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NTP), 0, st, bt->ybits, params, o, D,
+    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D,
                        Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
     WTRY(hipGetLastError());
     if (ce_sum) {
@@ -2917,7 +2921,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
     return 0;
   }
-  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, bt->ybits, params, o, D, Nc,
+  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D, Nc,
                      F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
   WTRY(hipGetLastError());
   hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o, D,
