@@ -955,13 +955,14 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   const int trips = (n + NPART - 1) / NPART;   // >= every part's length: both halves step
   const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
   int ei = r0 / (Ne - 1), ejj = r0 - ei * (Ne - 1);
+  // rho_i in registers, reloaded when the lane's entity row changes (every Ne - 1
+  // relations): per relation only the gam row is read (a broadcast across the half-wave's
+  // lanes, which share j), not the lanes' 32 distinct rho rows
   f2 rh[H2];
-  int cur = -1;
-  if constexpr (!LDS) {
+  const float* rsrc = LDS ? rl : rb;
 #pragma unroll
-    for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
-    cur = ei;
-  }
+  for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rsrc + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
+  int cur = ei;
   const float bq = D[D_EEBQ];
   float s0 = 0.f, s1 = 0.f;
   // class-bit words: the lane's relations walk the a-bit rows in order, so the word index
@@ -978,12 +979,10 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     float p0 = 0.f, p1 = 0.f;
     if (valid) {
       const int ej = ejj + (ejj >= ei ? 1 : 0);
-      if constexpr (!LDS) {
-        if (ei != cur) {
+      if (ei != cur) {
 #pragma unroll
-          for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rb + ei * H + 2 * kk);
-          cur = ei;
-        }
+        for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rsrc + ei * H + 2 * kk);
+        cur = ei;
       }
       const int nidx = ei * WE + (ej >> 5);
       if (nidx != widx) {
@@ -994,13 +993,12 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
       const bool a1 = (wcur >> (ej & 31)) & 1u;
       f2 dz = {bq, 0.f}, dzb = {0.f, 0.f};   // two chains: the fma latency overlaps
       if constexpr (LDS) {
-        const float4* r4 = reinterpret_cast<const float4*>(rl + ei * H);
         const float4* g4 = reinterpret_cast<const float4*>((a1 ? gdl : gl) + ej * H);
 #pragma unroll
         for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + (gam_j + a d), as kw_ee_clsb
-          const float4 q = r4[v], g = g4[v];
-          const f2 ka = relu2((f2){q.x, q.y} + (f2){g.x, g.y});
-          const f2 kb = relu2((f2){q.z, q.w} + (f2){g.z, g.w});
+          const float4 g = g4[v];
+          const f2 ka = relu2(rh[2 * v] + (f2){g.x, g.y});
+          const f2 kb = relu2(rh[2 * v + 1] + (f2){g.z, g.w});
           dz = fma2(ka, ld2(D + D_EECQ + 4 * v), dz);
           dzb = fma2(kb, ld2(D + D_EECQ + 4 * v + 2), dzb);
         }
