@@ -893,18 +893,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
 //   A block takes TF = 32 index rows i'; each half of a wave holds all 32 (one per lane) and
 //   walks its own sixteenth of the j' range, so a 200-row commit fills 7 blocks (224 lane
 //   rows) instead of 4 x 64.  Relation r -> entity pair (i, j) on the Ne-grid is advanced
-//   incrementally.  kappa = rho_i + (gam_j + a d): rho, gam and gam + d are LDS tables
-//   (Ne <= EE_TAB_LDS_MAX; else read from HBM, the same sums).  Source bins: per-lane sums;
+//   incrementally.  kappa = rho_i + (gam_j + a d): rho_i in registers (reloaded when the
+//   lane's row changes), gam and gam + d LDS tables (Ne <= EE_TAB_LDS_MAX; else read from
+//   HBM, the same sums).  Source bins: per-lane sums;
 //   target bins: one 32-lane sum per half-wave and step into tsum[j'], binned after the
 //   loop.  Both go to the block's LDS bins in 2^-32 fixed point (integer adds: order-free),
 //   which leave as one partial row per tile.
 // ---------------------------------------------------------------------------------
 constexpr int TF = 32;                // index rows per kw_ee_fwd block
-constexpr int EE_TAB_LDS_MAX = 400;   // Ne up to which rho, gam, gam + d sit in LDS
+constexpr int EE_TAB_LDS_MAX = 400;   // Ne up to which gam, gam + d sit in LDS
 __host__ __device__ inline int ee_fwd_tiles(int Ne) { return (Ne + TF - 1) / TF; }
 __host__ __device__ inline size_t ee_fwd_lds(int Ne, int Nc) {
   const size_t head = (size_t)((2 * Nc + 1) & ~1) * 8 + (size_t)((2 * Ne + 3) & ~3) * 4;
-  return head + (Ne <= EE_TAB_LDS_MAX ? (size_t)3 * Ne * H * 4 : 0);
+  return head + (Ne <= EE_TAB_LDS_MAX ? (size_t)2 * Ne * H * 4 : 0);
 }
 
 template <bool LDS>
@@ -921,8 +922,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   (void)o;
   extern __shared__ __attribute__((aligned(16))) unsigned long long bins[];   // [Nc][2] | ...
   float* tsum = reinterpret_cast<float*>(bins + ((2 * Nc + 1) & ~1));         // [Ne][2]
-  float* rl = tsum + ((2 * Ne + 3) & ~3);                                     // rho [Ne][H]
-  float* gl = rl + Ne * H;                                                    // gam
+  float* gl = tsum + ((2 * Ne + 3) & ~3);                                     // gam [Ne][H]
   float* gdl = gl + Ne * H;                                                   // gam + d
   const int b = blockIdx.y, t0 = blockIdx.x * TF;
   const int t = threadIdx.x, lane = t & 63, wv = uni(t >> 6), half = lane >> 5;
@@ -938,7 +938,6 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   const float* gb = gmm + (size_t)b * Ne * H;
   for (int e = t; e < 2 * n; e += NTP) tsum[e] = 0.f;
   if constexpr (LDS) {
-    stage_rows(rl, rb, 0, Ne);
     for (int e = t; e < Ne * H; e += NTP) {
       const float g = gb[e];
       gl[e] = g;
@@ -955,11 +954,11 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   const int trips = (n + NPART - 1) / NPART;   // >= every part's length: both halves step
   const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
   int ei = r0 / (Ne - 1), ejj = r0 - ei * (Ne - 1);
-  // rho_i in registers, reloaded when the lane's entity row changes (every Ne - 1
-  // relations): per relation only the gam row is read (a broadcast across the half-wave's
-  // lanes, which share j), not the lanes' 32 distinct rho rows
+  // rho_i in registers, loaded from HBM / L2 when the lane's entity row changes (every
+  // Ne - 1 relations, about once per lane at glide): per relation only the gam row is read
+  // from LDS, and rho is not staged at all
   f2 rh[H2];
-  const float* rsrc = LDS ? rl : rb;
+  const float* rsrc = rb;
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rsrc + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
   int cur = ei;
