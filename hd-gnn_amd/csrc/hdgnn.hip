@@ -247,18 +247,54 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 template <int SMAX, int KK>
 constexpr int tile_cred_words() { return 4 * 16 * SMAX * KK + 8 * KK; }
 
-template <int KK, int SMAX, int MODE, int LD, int ABL = 0, bool GFULL = false>
+// Column closing of a pair pass: element e = (node j, local unit k) of the group's
+// column sums is the fixed-order sum of the 4 waves' partials in cred.  Every partial
+// of the thread is loaded before the first add (one LDS round trip).  fix(j, unit, v)
+// stores it (NoFix: Cout[j][unit] = v); a caller's fix also finishes node j's row value
+// (diagonal pair removed, classifier c applied) -- rows are complete at this point.
+struct NoFix {};
+template <int NEL, int KK, class KOF, class FIX, class DFL>
+__device__ __forceinline__ void close_columns(const float* cred, const int N, const int t,
+                                              KOF kof, FIX fix, DFL dfl) {
+  constexpr int NU = (NEL + 255) / 256;
+  float c[NU][4];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int e = t + 256 * u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[u][q] = e < NEL ? cred[e + q * NEL] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int e = t + 256 * u;
+    const int j = e / KK, k = e - j * KK;
+    const float v = ((c[u][0] + c[u][1]) + c[u][2]) + c[u][3];
+    if (e < NEL && j < N) {
+      if constexpr (__is_same(FIX, NoFix)) dfl(j, kof(k), v);
+      else fix(j, kof(k), v);
+    }
+  }
+}
+
+template <int KK, int SMAX, int MODE, int LD, int ABL = 0, bool GFULL = false, class FIX = NoFix>
 __device__ __forceinline__ void pair_tile(
     const int N, const int t, const float* A, const float* Bv, const int k0,
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
-    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0) {
+    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0,
+    FIX fix = FIX{}) {
   typedef float p2 __attribute__((ext_vector_type(2)));
   constexpr int NP16 = 16 * SMAX;
   constexpr int NW = (SMAX + 1) / 2;
   constexpr int KP = KK / 2, KT = KK & 1;      // packed fp32 pairs (v_pk_*) + odd tail
-  const int tj = t & 15, ti = t >> 4, lane = t & 63, wv = t >> 6;
+  // SIMD balance: waves 4g + w of a block share one SIMD for every group g (workgroup waves
+  // are dealt to the 4 SIMDs cyclically), so group g's wave w takes the tile rows of
+  // ti-block (w + g) & 3, and a wave whose rows of a trip all lie past the sweep skips the
+  // trip: the partial last trip's work lands on different SIMDs in the 4 groups
+  const int grp = k0 / KK;
+  const int tj = t & 15, ti = ((t >> 4) + 4 * grp) & 15, lane = t & 63, wv = t >> 6;
+  const int wrow = __builtin_amdgcn_readfirstlane(4 * ((wv + grp) & 3));   // wave's first ti
   // hidden units of the chunk [k0, k0 + KK): the packed pairs start at the even unit kpb
   // (k0 or k0 + 1), so every pair is one 8-byte-aligned LDS read at an immediate offset
   // from a per-thread base; the unit left over is the tail ktl
@@ -286,6 +322,7 @@ __device__ __forceinline__ void pair_tile(
   }
 
   for (int s = 0; s < S; ++s) {
+    if (wrow + 16 * s >= nown) continue;    // wave-uniform: no row of this wave in the trip
     const int r = ti + 16 * s;
     const int i = rmul * r + radd;
     const bool iv = r < nown;
@@ -414,11 +451,8 @@ __device__ __forceinline__ void pair_tile(
     wave_sums(yacc, lane, [&](int k, float x) { credy[wv * KK + k] = x; });
   }
   __syncthreads();
-  for (int e = t; e < NP16 * KK; e += 256) {
-    const int j = e / KK, k = e - j * KK;
-    const float v = cred[e] + cred[e + NP16 * KK] + cred[e + 2 * NP16 * KK] + cred[e + 3 * NP16 * KK];
-    if (j < N) Cout[j * LD + kof(k)] = v;
-  }
+  close_columns<NP16 * KK, KK>(cred, N, t, kof, fix,
+                               [&](int j, int kk, float v) { Cout[j * LD + kk] = v; });
   if constexpr (MODE != 0) {
     if (t < KK) ysum[kof(t)] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
   }
@@ -435,19 +469,22 @@ __device__ __forceinline__ void pair_tile(
 // plus one permlane16 swap (the two DPP rows of a half-wave), column partials with one
 // permlane32 swap per pair of values, then the 4 waves through LDS as in pair_tile.
 // ------------------------------------------------------------------------------
-template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false>
+template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false, class FIX = NoFix>
 __device__ __forceinline__ void pair_tile32(
     const int N, const int t, const float* A, const float* Bv, const int k0,
     const float* __restrict__ dl, const uint32_t* __restrict__ bits, const int W,
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
-    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0) {
+    float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0,
+    FIX fix = FIX{}) {
   typedef float p2 __attribute__((ext_vector_type(2)));
   static_assert(SMAX16 % 2 == 0, "32-wide tiles cover an even count of 16-column tiles");
   constexpr int NP16 = 16 * SMAX16;
   constexpr int SMAX = SMAX16 / 2;
   constexpr int KP = KK / 2, KT = KK & 1;
-  const int tj = t & 31, ti = t >> 5, lane = t & 63, wv = t >> 6;
+  const int grp = k0 / KK;                     // SIMD-balanced rows, as in pair_tile
+  const int tj = t & 31, ti = ((t >> 5) + 2 * grp) & 7, lane = t & 63, wv = t >> 6;
+  const int wrow = __builtin_amdgcn_readfirstlane(2 * ((wv + grp) & 3));
   const int kpb = k0 + (k0 & 1);
   const int ktl = (k0 & 1) ? k0 : k0 + KK - 1;
   auto kof = [&](const int k) { return k < 2 * KP ? kpb + k : ktl; };
@@ -472,6 +509,7 @@ __device__ __forceinline__ void pair_tile32(
   }
 
   for (int s = 0; s < S; ++s) {
+    if (wrow + 8 * s >= nown) continue;     // wave-uniform skip
     const int r = ti + 8 * s;
     const int i = rmul * r + radd;
     const bool iv = r < nown;
@@ -603,11 +641,8 @@ __device__ __forceinline__ void pair_tile32(
     wave_sums(yacc, lane, [&](int k, float x) { credy[wv * KK + k] = x; });
   }
   __syncthreads();
-  for (int e = t; e < NP16 * KK; e += 256) {
-    const int j = e / KK, k = e - j * KK;
-    const float v = cred[e] + cred[e + NP16 * KK] + cred[e + 2 * NP16 * KK] + cred[e + 3 * NP16 * KK];
-    if (j < N) Cout[j * LD + kof(k)] = v;
-  }
+  close_columns<NP16 * KK, KK>(cred, N, t, kof, fix,
+                               [&](int j, int kk, float v) { Cout[j * LD + kk] = v; });
   if constexpr (MODE != 0) {
     if (t < KK) ysum[kof(t)] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
   }
@@ -615,12 +650,13 @@ __device__ __forceinline__ void pair_tile32(
 }
 
 // the hunk pair passes: 16 x 16 thread tiles up to NC16 = 80 (glide), 8 x 32 beyond
-template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false, class... Args>
+template <int KK, int SMAX16, int MODE, int LD, bool GFULL = false, class FIX = NoFix,
+          class... Args>
 __device__ __forceinline__ void pair_pass(Args... args) {
   if constexpr (SMAX16 > 5)
-    pair_tile32<KK, SMAX16, MODE, LD, GFULL>(args...);
+    pair_tile32<KK, SMAX16, MODE, LD, GFULL, FIX>(args...);
   else
-    pair_tile<KK, SMAX16, MODE, LD, 0, GFULL>(args...);
+    pair_tile<KK, SMAX16, MODE, LD, 0, GFULL, FIX>(args...);
 }
 
 // ------------------------------------------------------------------------------
@@ -1456,7 +1492,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     unsigned long long* __restrict__ stamps, float* __restrict__ aux,
     const float* __restrict__ bpow, const int B, unsigned long long* __restrict__ xch,
     uint32_t* __restrict__ status, const uint32_t xfault, const int ee_ins,
-    const unsigned long long* __restrict__ ncpart, const int ncpt, float* __restrict__ dnout) {
+    const unsigned long long* __restrict__ ncpart, const int ncpt, float* __restrict__ dnout,
+    const int ehr_park) {
   // model_4 on this kernel (hdg hybrid path): ee_ins = the entity-edge parameter block's
   // length in the flat vector (the model_2-shaped parameters after it are staged at their
   // model_2 offsets); ncpart [B][ncpt][Nc][2] = kw_ee_fwd's per-tile partial bins of the
@@ -1593,8 +1630,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     xsv = reinterpret_cast<const float*>(pp + PL.xsrt)[t];
     pmv = reinterpret_cast<const int*>(pp + PL.perm)[t];
   }
-  if (t <= nd) {
-    if (t < nd) xuv = reinterpret_cast<const float*>(pp + PL.xu)[t];
+  if (t <= Ne) {   // nd <= Ne: loaded without waiting for nd (stored below for t <= nd)
+    if (t < Ne) xuv = reinterpret_cast<const float*>(pp + PL.xu)[t];
     cmv = reinterpret_cast<const int*>(pp + PL.cum)[t];
     pxv = reinterpret_cast<const double*>(pp + PL.pxd)[t];
   }
@@ -1603,12 +1640,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     ocv = reinterpret_cast<const int*>(pp + PL.xoffc)[t];
   }
   if (t < Nc * WC) ybv = ybits[(size_t)b * Nc * WC + t];
+  // the first LQ x-list float4 per thread are loaded without waiting for xwords (reads
+  // bounded by the list region's static size, stored below only when they belong)
+  const int xlcap = 2 * Ne * (Ne - 1) + 6 * Ne + 8;      // prep_layout's x-list words
   float4 lv[LQ];
 #pragma unroll
   for (int u = 0; u < LQ; ++u) {
     const int w = 4 * (t + u * NT_MID);
-    lv[u] = (lfit && w < xwords) ? *reinterpret_cast<const float4*>(pp + PL.xl + w)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    lv[u] = w + 4 <= xlcap ? *reinterpret_cast<const float4*>(pp + PL.xl + w)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float l2 = 0.f;
 #pragma unroll
@@ -1887,15 +1927,22 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M5: hunk pair sums G_p = sum_q g1_pq, H_q = sum_p g1_pq (model_2.py:260-275) ---
   float* G = Bf[2];
   float* Hh = Bf[3];
-  pair_pass<KK_MID, SMAXC, 0, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr,
-                                  nullptr, 0, G, Hh, nullptr, credg, rmul, radd);
-  for (int e = t; e < Nc * HS; e += NT_MID) {
-    if (SPLIT && ((e / HS) & 1) != h) continue;       // the diagonal of the own rows
-    const float dg = reluf(alpha[e] + beta[e]);
-    G[e] -= dg;
-    Hh[e] -= dg;
+  {
+    // the pass includes the diagonal pair (p, p) of every swept row (y_pp = 0): removed from
+    // both sums of the own rows when the columns close
+    auto m5fix = [&](int j, int kk, float v) {
+      const int e = j * HS + kk;
+      if (!SPLIT || (j & 1) == h) {
+        const float dg = reluf(alpha[e] + beta[e]);
+        G[e] -= dg;
+        v -= dg;
+      }
+      Hh[e] = v;
+    };
+    pair_pass<KK_MID, SMAXC, 0, HS, false, decltype(m5fix)>(
+        Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, nullptr, nullptr, nullptr, 0, G, Hh,
+        nullptr, credg, rmul, radd, m5fix);
   }
-  __syncthreads();
   if constexpr (SPLIT) pair_send(Hh, Nc * HS, xout, xtag(epoch, 1) ^ xsend, t);   // received in M6
   MID_STAMP();
 
@@ -1936,6 +1983,15 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   m6_tiles(1);
   __syncthreads();
+  if constexpr (!TRAIN) {
+    if (ehr_park) {   // loss_E_HR (hdg_forward only): G's own rows and H (block 0) to gamma's
+                      // workspace slot, unused by a forward launch, for kw_ehr
+      for (int e = t; e < Nc * HS; e += NT_MID) {
+        if (!SPLIT || ((e / HS) & 1) == h) gamG[e] = G[e];
+        if (h == 0) gamG[Nc * HS + e] = Hh[e];
+      }
+    }
+  }
   MID_STAMP();
 
   // ---- M7: edge classifier + softmax CE per hunk pair (model_2.py:304-324, 115-118) ----
@@ -1974,9 +2030,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           reinterpret_cast<const float4*>((TAUE && yf > 0.f ? tauE : tau) + q * HS);
       const float4* ep4 = reinterpret_cast<const float4*>(eps);
       const float ey = TAUE ? 0.f : yf;       // without tau+eps: add y*eps here
-      typedef float p2 __attribute__((ext_vector_type(2)));
-      p2 zz = {b0, b1}, zy = {0.f, 0.f};      // (z0, z1) += kappa_k (U2[k][0], U2[k][1]):
-                                              // two chains (even / odd hidden-unit pairs)
+      // two classes: softmax / CE / gradient need only d = z1 - z0 = sum_k relu(kappa_k) c_k
+      // + (b1 - b0) (c = U2[:,1] - U2[:,0]): one fma per unit instead of two (the logits
+      // themselves only when requested); two accumulation chains
+      const float4* cv4 = reinterpret_cast<const float4*>(cvec);
+      float da = b1 - b0, dbb = 0.f;
       float kap[HS];
 #pragma unroll
       for (int v = 0; v < HS / 4; ++v) {
@@ -1989,32 +2047,45 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
           c.z = fmaf(ey, ee.z, c.z);
           c.w = fmaf(ey, ee.w, c.w);
         }
-        const p2 k01 = __builtin_elementwise_max((p2){a.x, a.y} + (p2){c.x, c.y}, (p2){0.f, 0.f});
-        const p2 k23 = __builtin_elementwise_max((p2){a.z, a.w} + (p2){c.z, c.w}, (p2){0.f, 0.f});
-        kap[4 * v] = k01.x;
-        kap[4 * v + 1] = k01.y;
-        kap[4 * v + 2] = k23.x;
-        kap[4 * v + 3] = k23.y;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float4 w = u2[2 * v + h];           // w0_k, w1_k, w0_k+1, w1_k+1
-          zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h], kap[4 * v + 2 * h]},
-                                         (p2){w.x, w.y}, zz);
-          zy = __builtin_elementwise_fma((p2){kap[4 * v + 2 * h + 1], kap[4 * v + 2 * h + 1]},
-                                         (p2){w.z, w.w}, zy);
-        }
+        kap[4 * v] = reluf(a.x + c.x);
+        kap[4 * v + 1] = reluf(a.y + c.y);
+        kap[4 * v + 2] = reluf(a.z + c.z);
+        kap[4 * v + 3] = reluf(a.w + c.w);
+        const float4 cw = cv4[v];
+        da = fmaf(kap[4 * v], cw.x, da);
+        dbb = fmaf(kap[4 * v + 1], cw.y, dbb);
+        da = fmaf(kap[4 * v + 2], cw.z, da);
+        dbb = fmaf(kap[4 * v + 3], cw.w, dbb);
       }
-      zz += zy;
-      const float z0 = zz.x, z1 = zz.y;
-      const float mx = fmaxf(z0, z1);
-      const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
-      const float ssum = e0 + e1;
-      const float inv = __builtin_amdgcn_rcpf(ssum);   // ssum in [1, 2]: 1-ulp rcp
-      const float p0 = e0 * inv, p1 = e1 * inv;
-      ce_acc += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+      float d = da + dbb;
+      if (lgb) {                              // C_edge_output2_logits (model_2.py:321-323)
+        typedef float p2 __attribute__((ext_vector_type(2)));
+        p2 zz = {b0, b1}, zy = {0.f, 0.f};
+#pragma unroll
+        for (int v = 0; v < HS / 4; ++v) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const float4 w = u2[2 * v + hh];      // w0_k, w1_k, w0_k+1, w1_k+1
+            zz = __builtin_elementwise_fma((p2){kap[4 * v + 2 * hh], kap[4 * v + 2 * hh]},
+                                           (p2){w.x, w.y}, zz);
+            zy = __builtin_elementwise_fma((p2){kap[4 * v + 2 * hh + 1], kap[4 * v + 2 * hh + 1]},
+                                           (p2){w.z, w.w}, zy);
+          }
+        }
+        zz += zy;
+        lgb[e] = zz.x;
+        lgb[Pc + e] = zz.y;
+        d = zz.y - zz.x;   // probs = softmax of the returned logits, as the graph defines them
+      }
+      // p1 = 1 / (1 + e^-d), p0 = e^-d p1, evaluated with e = e^-|d| in (0, 1] (no overflow);
+      // CE = softplus(d) (y = 0) or softplus(-d) (y = 1) = max(+-d, 0) + log(1 + e)
+      const float ex = __expf(-fabsf(d));
+      const float inv = __builtin_amdgcn_rcpf(1.f + ex);   // 1 + e in (1, 2]: 1-ulp rcp
+      const float pbig = inv, psmall = ex * inv;
+      const float p1 = d >= 0.f ? pbig : psmall, p0 = d >= 0.f ? psmall : pbig;
+      ce_acc += __logf(1.f + ex) + reluf(yf > 0.f ? -d : d);
       corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
       if (prb) { prb[e] = p0; prb[Pc + e] = p1; }
-      if (lgb) { lgb[e] = z0; lgb[Pc + e] = z1; }
       if constexpr (TRAIN) {
         if (qq == p || (p == Nc1i && qq == Nc1i - 1))   // defined diagonal, every row
           gam[p * GLD + p] = 0.f;
@@ -2082,15 +2153,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
-  pair_pass<KK_MID, SMAXC, 2, HS, true>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
-                                           nullptr, gam, GLD, Dsig, Dtau, ysumv, credg, rmul,
-                                           radd);
-  for (int e = t; e < Nc * HS; e += NT_MID) {
-    const int k = e % HS;
-    Dsig[e] *= cvec[k];
-    Dtau[e] *= cvec[k];
+  {
+    auto m8fix = [&](int j, int kk, float v) {     // dkappa = c (.) [kappa > 0] gamma
+      const float ck = cvec[kk];
+      Dsig[j * HS + kk] *= ck;
+      Dtau[j * HS + kk] = v * ck;
+    };
+    pair_pass<KK_MID, SMAXC, 2, HS, true, decltype(m8fix)>(
+        Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr, gam, GLD, Dsig, Dtau, ysumv,
+        credg, rmul, radd, m8fix);
   }
-  __syncthreads();
   if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, xtag(epoch, 2) ^ xsend, t);   // received in M9
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
@@ -2209,18 +2281,22 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // ---- M10: hunk pair backward: dgamma = [g1 > 0](dG_p + dH_q) -----------------------
   float* Dal = Bf[4];   // Dsig/Dtau dead after dG/dH
   float* Dbe = Bf[5];
-  pair_pass<KK_MID, SMAXC, 1, HS>(Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0,
-                                  Dal, Dbe, ysumv, credg, rmul, radd);
-  for (int e = t; e < Nc * HS; e += NT_MID) {
-    if (SPLIT && ((e / HS) & 1) != h) {             // partner's rows: no D_alpha here
-      Dal[e] = 0.f;
-      continue;
-    }
-    const float dz = (alpha[e] + beta[e] > 0.f) ? (dG[e] + dH[e]) : 0.f;
-    Dal[e] -= dz;
-    Dbe[e] -= dz;
+  {
+    auto m10fix = [&](int j, int kk, float v) {
+      const int e = j * HS + kk;
+      if (SPLIT && (j & 1) != h) {                  // partner's rows: no D_alpha here
+        Dal[e] = 0.f;
+      } else {                                      // minus the diagonal pair of an own row
+        const float dz = (alpha[e] + beta[e] > 0.f) ? (dG[e] + dH[e]) : 0.f;
+        Dal[e] -= dz;
+        v -= dz;
+      }
+      Dbe[e] = v;
+    };
+    pair_pass<KK_MID, SMAXC, 1, HS, false, decltype(m10fix)>(
+        Nc, tg, alpha, beta, g * KK_MID, dlt, yb, WC, dG, dH, nullptr, 0, Dal, Dbe, ysumv, credg,
+        rmul, radd, m10fix);
   }
-  __syncthreads();
   MID_STAMP();
   // dn_c[m] = Dalpha_c V1[m] + Dbeta_c V1[4+m]: m in {0,1} (x' parts) for M11, m in {2,3}
   // (class parts, [NC16][2] in the pair-tile scratch: dead after M10, below M11's dx'
@@ -3227,9 +3303,11 @@ struct StepOut {
   float* probs;
   float* logits;
   uint32_t* status;
+  float* ehr;
 };
 StepOut step_out(const hdg_outputs* out) {
-  return out ? StepOut{out->probs, out->logits, out->status} : StepOut{nullptr, nullptr, nullptr};
+  return out ? StepOut{out->probs, out->logits, out->status, out->ehr}
+             : StepOut{nullptr, nullptr, nullptr, nullptr};
 }
 
 // model_4 hooks of the step kernel (k_commit_step's ee_ins / ncpart / dnout); all zero for
@@ -3255,7 +3333,8 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
                      ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, o.probs,
                      o.logits, s->ne, s->nc, ce_scale, stamps, bpow ? ws + w.aux : nullptr, bpow,
                      s->batch, (unsigned long long*)(ws + w.xch), o.status,
-                     SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncpart, hy.ncpt, hy.dnout);
+                     SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncpart, hy.ncpt, hy.dnout,
+                     (!TRAIN && o.ehr) ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -3275,6 +3354,15 @@ hipError_t dispatch_step(const hdg_shape* s, const hdg_batch* bt, const float* p
     default: HDG_STEP(10);
   }
 #undef HDG_STEP
+}
+
+// loss_E_HR of a fused forward launch: the step kernel parked G / H in gamma's slot
+hipError_t fused_ehr(const hdg_shape* s, float* ws, const Work& w, const float* params,
+                     const hdg_outputs* out, hipStream_t st) {
+  if (!out || !out->ehr) return hipSuccess;
+  const size_t cs = (size_t)16 * smax_c(s->nc) * 16 * smax_c(s->nc);   // NC16^2 per commit
+  return hdg::launch_ehr(ws + w.gam, ws + w.gam + (size_t)s->nc * HS, cs, s->batch, s->nc,
+                         params, s->variant, out->ehr, st);
 }
 
 float pair_count(const hdg_shape* s) {
@@ -3343,6 +3431,7 @@ int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, flo
                          part_rows(s, split), m2::NP, m2::NP + 1, GRAD_LEN, 0, ce_sum);
       HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(fused_ehr(s, ws, w, params, out, st));
     HIP_TRY(mark(1));
     HIP_TRY(mark(2));
     return 0;
@@ -3546,6 +3635,7 @@ int hdg_forward(const hdg_shape* s, const hdg_batch* bt, const float* params, hd
                        part_rows(s, split), m2::NP, m2::NP + 1, GRAD_LEN, 0, ce_sum);
     HIP_TRY(hipGetLastError());
   }
+  HIP_TRY(fused_ehr(s, ws, w, params, out, st));
   return 0;
 }
 

@@ -124,6 +124,11 @@ int wide_ncpart_tiles(const hdg_shape* s);
 int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, void* workspace,
                 float* grad, hipStream_t st, const WideAdam* adam = nullptr);
 
+// loss_E_HR of a forward launch (model_2.py:122) from the complete hunk row / column sums
+// G, H ([Nc][20] per commit at stride cs floats): out[0] = 0.001 l2_loss(C_edge_output)
+hipError_t launch_ehr(const float* G, const float* Hh, size_t cs, int B, int Nc,
+                      const float* params, int variant, float* out, hipStream_t st);
+
 // fused path pieces the general path reuses (hdgnn.hip)
 hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,
                             int o_kt, int o_ncst, hipStream_t st);

@@ -2859,6 +2859,80 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// kw_ehr  grid (1): loss_E_HR = 0.001 * l2_loss(C_edge_output) (model_2.py:122), the
+// graph's unfetched regulariser of the hunk-pair effects (mlp_hunk_B2's output,
+// model_2.py:245-277): C_edge_output[b][k][pq] = S_pk + T_qk with S = G V2 + (Nc-1) c2 and
+// T = H V2 + (Nc-1) c2 (the second layer commutes with the row / column sums).
+// Per commit and unit k, over the pairs p != q:
+//   sum (S_p + T_q)^2 = (Nc-1)(sum S^2 + sum T^2) + 2 (sum S sum T - sum_p S_p T_p)
+// so five additive per-unit sums suffice.  Thread (k = t % 20, slice t / 20) walks its
+// nodes; f64 sums closed in a fixed order (deterministic).  G, H: [Nc][20] per commit at
+// stride `cs` floats (the rows of kw_hunk_fwd, or those the fused step kernel parks).
+// Forward-only diagnostic: one block, never on the training path.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void kw_ehr(const float* __restrict__ G,
+                                               const float* __restrict__ Hh, size_t cs, int B,
+                                               int Nc, const float* __restrict__ W, int oV2,
+                                               int oc2, float* __restrict__ out) {
+  constexpr int NSL = 1024 / H;                      // 51 node slices
+  __shared__ double red[NSL][5][H];
+  __shared__ double tot[H];
+  const int t = threadIdx.x, k = t % H, sl = t / H;
+  float v2[H];
+#pragma unroll
+  for (int l = 0; l < H; ++l) v2[l] = W[oV2 + l * H + k];
+  const float off = (float)(Nc - 1) * W[oc2 + k];
+  if (t < H) tot[t] = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double sS = 0.0, sT = 0.0, sS2 = 0.0, sT2 = 0.0, sST = 0.0;
+    if (sl < NSL) {
+      for (int p = sl; p < Nc; p += NSL) {
+        const float* g = G + (size_t)b * cs + (size_t)p * H;
+        const float* h = Hh + (size_t)b * cs + (size_t)p * H;
+        float S = 0.f, T = 0.f;
+#pragma unroll
+        for (int l = 0; l < H; ++l) {
+          S = fmaf(g[l], v2[l], S);
+          T = fmaf(h[l], v2[l], T);
+        }
+        const double Sd = (double)(S + off), Td = (double)(T + off);
+        sS += Sd;
+        sT += Td;
+        sS2 += Sd * Sd;
+        sT2 += Td * Td;
+        sST += Sd * Td;
+      }
+      red[sl][0][k] = sS;
+      red[sl][1][k] = sT;
+      red[sl][2][k] = sS2;
+      red[sl][3][k] = sT2;
+      red[sl][4][k] = sST;
+    }
+    __syncthreads();
+    if (t < H) {
+      double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int q = 0; q < NSL; ++q)
+        for (int c = 0; c < 5; ++c) a[c] += red[q][c][t];
+      tot[t] += (double)(Nc - 1) * (a[2] + a[3]) + 2.0 * (a[0] * a[1] - a[4]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    double s = 0.0;
+    for (int q = 0; q < H; ++q) s += tot[q];
+    out[0] = (float)(0.0005 * s);                    // 0.001 * l2_loss = 0.001 * sum / 2
+  }
+}
+
+hipError_t launch_ehr(const float* G, const float* Hh, size_t cs, int B, int Nc,
+                      const float* params, int variant, float* out, hipStream_t st) {
+  const Off o = param_offsets(variant);
+  hipLaunchKernelGGL(kw_ehr, dim3(1), dim3(1024), 0, st, G, Hh, cs, B, Nc, params, o.H1_W2,
+                     o.H1_B2, out);
+  return hipGetLastError();
+}
+
 int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
              hdg_outputs* out, float* ce_sum, void* workspace, bool train, hipStream_t st,
              const WideAdam* adam) {
@@ -2915,6 +2989,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
       hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, o.NP,
                          ce_sum);
       WTRY(hipGetLastError());
+    }
+    if (out && out->ehr) {
+      WTRY(launch_ehr(F(w.G), F(w.Hh), (size_t)Nc * H, B, Nc, params, v, out->ehr, st));
     }
     return 0;
   }

@@ -35,7 +35,8 @@ class State(ctypes.Structure):
 
 class Outputs(ctypes.Structure):
     _fields_ = [("probs", ctypes.c_void_p), ("logits", ctypes.c_void_p),
-                ("stats", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+                ("stats", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("ehr", ctypes.c_void_p)]
 
 
 class Dp(ctypes.Structure):
@@ -46,7 +47,7 @@ class Dp(ctypes.Structure):
 
 DP_MAX_WORLD, DP_HANDLE_BYTES, DP_MAX_LEN = 16, 64, 3152
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 # gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
 TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
 STATUS_XCH_TIMEOUT, STATUS_DP_TIMEOUT = 1, 2

@@ -54,6 +54,7 @@ class Engine:
         # sticky status word (HDG_STATUS_* bits); check_status() reads it
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ce_sum = torch.zeros(1, dtype=f32, device=dev)
+        self.ehr = torch.zeros(1, dtype=f32, device=dev)     # loss_E_HR of the last forward
         pc = nc * (nc - 1)
         self.probs = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
         self.logits = torch.zeros(batch, 2, pc, dtype=f32, device=dev)
@@ -61,10 +62,11 @@ class Engine:
                                  self.beta_pow.data_ptr())
         st = self.status.data_ptr()
         self._out = _lib.Outputs(self.probs.data_ptr(), self.logits.data_ptr(),
-                                 self.stats.data_ptr(), st)
+                                 self.stats.data_ptr(), st, self.ehr.data_ptr())
         # a training sess.run fetches C_edge_output2 (the probabilities), not the logits
-        self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr(), st)
-        self._out_none = _lib.Outputs(None, None, None, st)   # status only
+        self._out_train = _lib.Outputs(self.probs.data_ptr(), None, self.stats.data_ptr(), st,
+                                       None)
+        self._out_none = _lib.Outputs(None, None, None, st, None)   # status only
         # data parallelism: which all-reduce joins the ranks' gradients
         self.xgmi, self.allreduce_kind = None, None
         if self._distributed():
@@ -234,7 +236,8 @@ class Engine:
         self._graph.replay()
 
     def forward(self, dbatch):
-        """sess.run([loss_Hedge_mse, loss_map, C_edge_output2]) equivalent (test path)."""
+        """sess.run([loss_Hedge_mse, loss_map, C_edge_output2]) equivalent (test path);
+        also fills self.ehr with the batch's loss_E_HR (model_2.py:122)."""
         self._check(dbatch)
         b = dbatch.struct()
         _lib.check(self.lib.hdg_forward(ctypes.byref(self.shape), ctypes.byref(b),

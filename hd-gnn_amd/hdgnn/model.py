@@ -59,6 +59,61 @@ def _default_reader(model, step):
     return read_data(model, step)
 
 
+def _evaluation_funcs():
+    """The reference's metrics module, imported from the caller's path the way model_2.py
+    does (`from EvaluationFuncs import *`, model_2.py:12; the north star keeps it as-is);
+    hdgnn.metrics (the same functions restated, pinned by the reference's own outputs in
+    tests/golden/metrics_tiny.*) only when EvaluationFuncs is not importable."""
+    try:
+        import EvaluationFuncs
+        return EvaluationFuncs
+    except ImportError:
+        return metrics
+
+
+class Saver(object):
+    """tf.train.Saver() of build_model (model_2.py:139): every variable of the graph
+    (tf.global_variables() at that point: the model's weights) saved
+    as a TF V2 bundle under the TF variable names (hdgnn.tfckpt), plus this engine's TF1
+    Adam slots and beta powers so a restore resumes training.  save() keeps the newest
+    max_to_keep bundles (TF's default 5) and rewrites the 'checkpoint' state file, as
+    Saver.save does; restore() reads a TF-written bundle too (no Adam slots: the
+    optimizer state is then left as it is)."""
+
+    def __init__(self, model, max_to_keep=5):
+        self._model = model
+        self.max_to_keep = max_to_keep
+        self._last = []              # prefixes saved by this Saver, oldest first
+
+    def save(self, sess, save_path, global_step=None):
+        prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+        eng = self._model.engine
+        d = os.path.dirname(prefix) or "."
+        os.makedirs(d, exist_ok=True)
+        tfckpt.write(prefix, tfckpt.state_tensors(eng.get_params(), self._model.variant,
+                                                  eng.m.cpu().numpy(), eng.v.cpu().numpy(),
+                                                  eng.beta_pow.cpu().numpy()))
+        if prefix in self._last:
+            self._last.remove(prefix)
+        self._last.append(prefix)
+        while self.max_to_keep and len(self._last) > self.max_to_keep:
+            tfckpt.remove_bundle(self._last.pop(0))
+        tfckpt.write_state_file(d, os.path.basename(prefix),
+                                [os.path.basename(q) for q in self._last
+                                 if (os.path.dirname(q) or ".") == d])
+        return prefix
+
+    def restore(self, sess, save_path):
+        import torch
+        eng = self._model.engine
+        flat, m, v, bp = tfckpt.engine_state(tfckpt.read(save_path), self._model.variant)
+        eng.set_params(flat)
+        if m is not None:
+            eng.m.copy_(torch.from_numpy(np.asarray(m, np.float32)))
+            eng.v.copy_(torch.from_numpy(np.asarray(v, np.float32)))
+            eng.beta_pow.copy_(torch.from_numpy(np.asarray(bp, np.float32)))
+
+
 class graph2graph(object):
     variant = 2        # model_<variant>.py
 
@@ -108,6 +163,13 @@ class graph2graph(object):
         self.loss_Hedge_mse = None
         self.loss_map = None
         self.loss_para = None
+        # 0.001 * l2_loss(C_edge_output) (model_2.py:122): computed by the graph but fetched
+        # by neither train nor test; here filled by test()'s forward launches
+        self.loss_E_HR = None
+        # the training sess.run fetches C_edge_output2 only (model_2.py:369-371); set True
+        # to have train() also fill C_edge_output2_logits every step
+        self.fetch_logits = False
+        self.saver = Saver(self)
 
     def _initialize(self):
         """tf.global_variables_initializer(): truncated_normal(0.1) weights, zero biases,
@@ -178,7 +240,7 @@ class graph2graph(object):
             tr_loss_map = 0.0
             correct = 0
             for j, db in enumerate(batches):
-                eng.train_step(db)
+                eng.train_step(db, logits=self.fetch_logits)
                 # one small copy per step: pre-update losses (like sess.run), the
                 # on-device top_ACC numerator (gradient trailer count slots; already
                 # summed over ranks by the data-parallel all-reduce) and the status word
@@ -192,7 +254,7 @@ class graph2graph(object):
                                                                       float(host[1]),
                                                                       float(host[2]))
                 self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
-                self.C_edge_output2_logits = None          # not fetched in training
+                self.C_edge_output2_logits = eng.logits if self.fetch_logits else None
                 correct += _lib.trailer_count(host[4:4 + _lib.TRAILER])
             torch.cuda.synchronize(eng.device)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
@@ -226,14 +288,8 @@ class graph2graph(object):
         the 'checkpoint' state file tf.train.get_checkpoint_state reads."""
         if self.rank != 0:
             return
-        d = self._model_dir(checkpoint_dir)
-        os.makedirs(d, exist_ok=True)
-        eng = self.engine
-        name = "g2g.model-%d" % step
-        tfckpt.write(os.path.join(d, name),
-                     tfckpt.state_tensors(eng.get_params(), self.variant, eng.m.cpu().numpy(),
-                                          eng.v.cpu().numpy(), eng.beta_pow.cpu().numpy()))
-        tfckpt.write_state_file(d, name)
+        self.saver.save(self.sess, os.path.join(self._model_dir(checkpoint_dir), "g2g.model"),
+                        global_step=step)
 
     def load(self, checkpoint_dir):
         """get_checkpoint_state + saver.restore (model_2.py:439-451).  Reads TF V2 bundles
@@ -246,8 +302,9 @@ class graph2graph(object):
             return False
         path = os.path.join(d, name)
         if os.path.exists(path + ".index"):
-            flat, m, v, bp = tfckpt.engine_state(tfckpt.read(path), self.variant)
-        elif os.path.exists(path + ".npz"):
+            self.saver.restore(self.sess, path)
+            return True
+        if os.path.exists(path + ".npz"):
             z = np.load(path + ".npz", allow_pickle=False)
             flat = np.concatenate([np.asarray(z[n], np.float32).reshape(-1)
                                    for n, _ in layout.specs(self.variant)])
@@ -282,6 +339,8 @@ class graph2graph(object):
         for db in self._device_batches(test, maps):
             probs, logits, ce_sum = eng.forward(db)
             p = probs.cpu().numpy()
+            self.C_edge_output2_logits = logits
+            self.loss_E_HR = self._allsum(float(eng.ehr.item()))
             eng.check_status()
             ce = self._allsum(float(ce_sum.item())) / (self.mini_batch_num * self.Ncr)
             th1 = self.vars["map_conv/map_theta1:0"].reshape(-1).astype(np.float64)
@@ -302,11 +361,12 @@ class graph2graph(object):
         np.save(step_dir + 'C_edge_t' + str(self.Ne) + '.npy', C_edge_t1)
         np.save(step_dir + 'C_edge_y' + str(self.Ne) + '.npy',
                 C_edge_test.reshape(len(C_edge_test), self.Dr, self.Ncr))
-        C_edge_t2 = metrics.process_edge(C_edge_t1)
+        ev = _evaluation_funcs()
+        C_edge_t2 = ev.process_edge(C_edge_t1)
         C_edge_y = C_edge_test[:n_used]
-        print('topol_acc: ' + str(metrics.top_ACC(C_edge_y, C_edge_t2)))
-        print('prec: ' + str(metrics.prec(C_edge_y, C_edge_t2)))
-        print('recall: ' + str(metrics.recall(C_edge_y, C_edge_t2)))
-        print('F1-score: ' + str(metrics.f1(C_edge_y, C_edge_t2)))
-        print('AUC-score: ' + str(metrics.AUC(C_edge_y, C_edge_t2)))
+        print('topol_acc: ' + str(ev.top_ACC(C_edge_y, C_edge_t2)))
+        print('prec: ' + str(ev.prec(C_edge_y, C_edge_t2)))
+        print('recall: ' + str(ev.recall(C_edge_y, C_edge_t2)))
+        print('F1-score: ' + str(ev.f1(C_edge_y, C_edge_t2)))
+        print('AUC-score: ' + str(ev.AUC(C_edge_y, C_edge_t2)))
         print('test time:' + str(end_time - start_time))

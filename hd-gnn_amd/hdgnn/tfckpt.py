@@ -444,9 +444,22 @@ def latest(checkpoint_dir):
     return None
 
 
-def write_state_file(checkpoint_dir, name):
+def write_state_file(checkpoint_dir, name, all_names=None):
+    """The CheckpointState text proto tf.train.Saver.save writes next to the bundles:
+    the latest prefix and every prefix still kept (max_to_keep), oldest first."""
     with open(os.path.join(checkpoint_dir, "checkpoint"), "w") as f:
-        f.write('model_checkpoint_path: "%s"\nall_model_checkpoint_paths: "%s"\n' % (name, name))
+        f.write('model_checkpoint_path: "%s"\n' % name)
+        for n in (all_names or [name]):
+            f.write('all_model_checkpoint_paths: "%s"\n' % n)
+
+
+def remove_bundle(prefix):
+    """Delete the files of the bundle at prefix (index + data shards), as Saver does for
+    checkpoints that fall out of max_to_keep."""
+    d, base = os.path.split(prefix)
+    for f in os.listdir(d or "."):
+        if f == base + ".index" or f.startswith(base + ".data-"):
+            os.remove(os.path.join(d, f))
 
 
 # ------------------------------------------------------------------ engine state <-> TF names

@@ -39,40 +39,51 @@ def _variant(argv):
     return a.model, a.loader, rest
 
 
-def main(argv=None):
+# the reference's per-step tables (main.py:11-15): glide steps 2, 3, 5
+STEPS = [2, 3, 5]
+ENTITY_NODES = [200, 250, 250]
+HUNK_NODES = [74, 114, 150]
+ENTITY_EDGES = [39800, 62250, 62250]
+HUNK_EDGES = [5402, 12882, 22350]
+
+
+def build_parser(step, entity_node, hunk_node, entity_edge, hunk_edge):
+    """The reference's per-step parser (main.py:24-48): same flags, types, defaults, help."""
+    parser = argparse.ArgumentParser(description='')
+    parser.add_argument('--epoch', type=int, default=50, help='number of training epochs')
+    parser.add_argument('--Ds', type=int, default=1, help='The State Dimention')
+    parser.add_argument('--Ds_inter', type=int, default=1, help='The State Dimention of inter state')
+    parser.add_argument('--Dr', type=int, default=2, help='The Relationship Dimension')
+    parser.add_argument('--Dr_inter', type=int, default=2, help='The Relationship Dimension of inter state')
+    parser.add_argument('--De_e', type=int, default=20, help='The Effect Dimension on entity')
+    parser.add_argument('--De_er', type=int, default=20, help='The Effect Dimension on entity Relations')
+    parser.add_argument('--Mini_batch', type=int, default=50, help='The training mini_batch')
+    parser.add_argument('--checkpoint_dir', dest='checkpoint_dir', default='./checkpoint40/',
+                        help='models are saved here')
+    parser.add_argument('--Ne', type=int, default=entity_node, help='The Number of entities')
+    parser.add_argument('--Nc', type=int, default=hunk_node, help='The Number of code changes')
+    parser.add_argument('--Ner', type=int, default=entity_edge, help='The Number of entity Relations')
+    parser.add_argument('--Ncr', type=int, default=hunk_edge, help='The Number of code change Relations')
+    parser.add_argument('--Step', type=int, default=step, help='the number of commits/groups')
+    parser.add_argument('--Repo', type=str, default='glide', help='the name of repository')
+    parser.add_argument('--Type', dest='Type', default='train', help='train or test')
+    return parser
+
+
+def main(argv=None, model_cls=None):
+    """model_cls: the graph2graph class to run (tests inject a recorder); default
+    hdgnn.model[_N].graph2graph for --model N."""
     import importlib
     variant, loader, argv = _variant(sys.argv[1:] if argv is None else argv)
-    graph2graph = importlib.import_module("hdgnn.model" + ("" if variant == 2 else "_%d" % variant)).graph2graph
-    _init_distributed()
-    steps = [2, 3, 5]
-    entity_nodes = [200, 250, 250]
-    hunk_nodes = [74, 114, 150]
-    entity_edges = [39800, 62250, 62250]
-    hunk_edges = [5402, 12882, 22350]
+    graph2graph = model_cls or importlib.import_module(
+        "hdgnn.model" + ("" if variant == 2 else "_%d" % variant)).graph2graph
+    if model_cls is None:
+        _init_distributed()
 
     for step, entity_node, hunk_node, entity_edge, hunk_edge in zip(
-            steps, entity_nodes, hunk_nodes, entity_edges, hunk_edges):
+            STEPS, ENTITY_NODES, HUNK_NODES, ENTITY_EDGES, HUNK_EDGES):
         print(step, entity_node, hunk_node, entity_edge, hunk_edge)
-
-        parser = argparse.ArgumentParser(description='')
-        parser.add_argument('--epoch', type=int, default=50, help='number of training epochs')
-        parser.add_argument('--Ds', type=int, default=1, help='The State Dimention')
-        parser.add_argument('--Ds_inter', type=int, default=1, help='The State Dimention of inter state')
-        parser.add_argument('--Dr', type=int, default=2, help='The Relationship Dimension')
-        parser.add_argument('--Dr_inter', type=int, default=2, help='The Relationship Dimension of inter state')
-        parser.add_argument('--De_e', type=int, default=20, help='The Effect Dimension on entity')
-        parser.add_argument('--De_er', type=int, default=20, help='The Effect Dimension on entity Relations')
-        parser.add_argument('--Mini_batch', type=int, default=50, help='The training mini_batch')
-        parser.add_argument('--checkpoint_dir', dest='checkpoint_dir', default='./checkpoint40/',
-                            help='models are saved here')
-        parser.add_argument('--Ne', type=int, default=entity_node, help='The Number of entities')
-        parser.add_argument('--Nc', type=int, default=hunk_node, help='The Number of code changes')
-        parser.add_argument('--Ner', type=int, default=entity_edge, help='The Number of entity Relations')
-        parser.add_argument('--Ncr', type=int, default=hunk_edge, help='The Number of code change Relations')
-        parser.add_argument('--Step', type=int, default=step, help='the number of commits/groups')
-        parser.add_argument('--Repo', type=str, default='glide', help='the name of repository')
-        parser.add_argument('--Type', dest='Type', default='train', help='train or test')
-        args = parser.parse_args(argv)
+        args = build_parser(step, entity_node, hunk_node, entity_edge, hunk_edge).parse_args(argv)
 
         if not os.path.exists(args.checkpoint_dir):
             os.makedirs(args.checkpoint_dir)

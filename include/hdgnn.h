@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 5
+#define HDG_ABI_VERSION 6
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -92,6 +92,10 @@ typedef struct hdg_outputs {
     uint32_t* status;    /* [1] sticky device status word: the library ORs HDG_STATUS_*
                             bits into it (write-through store) and never clears it; the
                             caller zeroes it and reads it whenever it synchronises     */
+    float* ehr;          /* [1] loss_E_HR = 0.001 l2_loss(C_edge_output) of the call's
+                            commits (model_2.py:122; computed by the reference graph but
+                            fetched by neither of its sess.run calls): written by
+                            hdg_forward only, ignored by the training entry points      */
 } hdg_outputs;
 
 /* Status bits (hdg_outputs.status).  HDG_STATUS_XCH_TIMEOUT: in the fused path's split

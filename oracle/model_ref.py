@@ -222,8 +222,11 @@ def forward(P, x, a, y, hid, nlen, variant=2, dtype=torch.float64):
     for k, _, _ in layout.keyed_specs(variant):
         loss_para = loss_para + 0.001 * (0.5 * (P[k] * P[k]).sum())
     total = 10 * ce + 0.1 * loss_map + loss_para                           # model_2.py:336
+    # loss_E_HR = 0.001 * l2_loss(C_edge_output) (model_2.py:122): computed, never fetched
+    loss_E_HR = 0.001 * 0.5 * (eff_h * eff_h).sum()
     return dict(logits=logits, probs=probs, ce=ce, loss_map=loss_map,
-                loss_para=loss_para, total=total, theta=P["th2"], xp=xp, nbr=nbr)
+                loss_para=loss_para, total=total, theta=P["th2"], xp=xp, nbr=nbr,
+                loss_E_HR=loss_E_HR)
 
 
 def to_torch_params(params, dtype=torch.float64, requires_grad=True):

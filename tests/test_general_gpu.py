@@ -91,6 +91,7 @@ def _run_and_check(cb, v, seed, path=GEN):
     torch.cuda.synchronize()
     _check_outputs(logits.cpu().numpy(), probs.cpu().numpy(), out)
     np.testing.assert_allclose(ce_sum.item() / (B * nc * (nc - 1)), float(out["ce"]), rtol=1e-5)
+    np.testing.assert_allclose(eng.ehr.item(), float(out["loss_E_HR"]), rtol=1e-4)
     return eng
 
 

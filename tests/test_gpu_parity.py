@@ -106,6 +106,8 @@ def test_forward_matches_oracle(B, ne, nc, seed, split_mode):
     _check_outputs(logits.cpu().numpy(), probs.cpu().numpy(), out)
     ce = ce_sum.item() / (B * nc * (nc - 1))
     np.testing.assert_allclose(ce, float(out["ce"]), rtol=1e-5)
+    # loss_E_HR (model_2.py:122) of the forward launch; sums of squares in f64
+    np.testing.assert_allclose(eng.ehr.item(), float(out["loss_E_HR"]), rtol=1e-4)
 
 
 @pytest.mark.parametrize("B,ne,nc,seed", CASES)
