@@ -102,6 +102,46 @@ def cpu_baseline(cb, steps, threads):
                       "B=%d Ne=%d Nc=%d, %.1f s timed after 1 warm-up step" % (steps, B, ne, nc, dt)}
 
 
+def e2e_train(B, ne, nc, v, epochs, dev):
+    """The reference training loop as main.py --Type train runs it (model_2.py:335-424):
+    graph2graph.train for `epochs` epochs, one Mini_batch = B step per epoch (2B synthetic
+    commits split 50/50 as utils2 does), with its per-epoch result line, result file and
+    checkpoint save, in a scratch directory.  Includes the upload + prepare of the batch."""
+    import importlib
+    import tempfile
+    from hdgnn.synth import synth_commits
+    mod = importlib.import_module("hdgnn.model" + ("" if v == 2 else "_%d" % v))
+    cb = synth_commits(2 * B, ne, nc, 20250301 + 7)
+    train, test = cb.slice(0, B), cb.slice(B, 2 * B)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            class Args:
+                checkpoint_dir, Repo = os.path.join(d, "ck"), "glide"
+            m = mod.graph2graph(None, Ds=1, Ne=ne, Nc=nc, Ner=ne * (ne - 1), Ncr=nc * (nc - 1),
+                                Dr=2, De_e=20, De_er=20, Mini_batch=B, checkpoint_dir=Args.checkpoint_dir,
+                                epoch=epochs, Ds_inter=1, Dr_inter=2, Step=2, Repo="glide",
+                                device=dev, compact=(train, test, train))
+            import contextlib
+            import io
+            with contextlib.redirect_stdout(io.StringIO()):
+                m.train(Args)                      # warm: allocations, first checkpoint
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                m.train(Args)
+                torch.cuda.synchronize(dev)
+            wall = time.perf_counter() - t0
+        finally:
+            os.chdir(cwd)
+    return {"epochs": epochs, "commits_per_epoch": B, "wall_s": round(wall, 4),
+            "commits_per_s": round(epochs * B / wall, 1),
+            "ms_per_epoch": round(1e3 * wall / epochs, 3),
+            "note": "graph2graph.train as main.py runs it: upload + hdg_prepare of the batch, "
+                    "then per epoch one training step, one device->host read of the epoch's "
+                    "losses / count, the result line + file and a TF-bundle checkpoint save"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +160,9 @@ def main():
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
+    ap.add_argument("--e2e", type=int, default=0, metavar="EPOCHS",
+                    help="also time graph2graph.train (the main.py --Type train loop) for "
+                         "EPOCHS epochs of one --batch-commit step each (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +311,9 @@ def main():
                             "operations, so this is work-equivalent throughput, not a "
                             "hardware roofline (no frac)"},
                 "executed": executed}
+    e2e = None
+    if world == 1 and args.e2e > 0:
+        e2e = e2e_train(B, ne, nc, v, args.e2e, dev)
     cpu = None
     if world == 1 and not args.no_cpu and v == 2:
         threads = min(16, os.cpu_count() or 1)
@@ -295,6 +341,8 @@ def main():
             "upload_prepare_ms": round(upload_ms, 3),
             "pcie_inclusive_commits_per_s": round(world * B / ((ms_per_step + upload_ms) * 1e-3), 1),
             "kernels_ms": {k: round(v, 5) for k, v in kern_ms.items()}}
+    if e2e:
+        line["e2e"] = e2e
     print(json.dumps(line), flush=True)
     if launched:
         torch.distributed.destroy_process_group()

@@ -716,6 +716,20 @@ __device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) 
   return r;
 }
 
+// the same with x taken from the low / high half of a packed pair (op_sel: no copy of the
+// half into a register of its own)
+__device__ __forceinline__ f2 clamp_fma2_lo(const f2 x, const f2 a, const f2 b) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(r) : "v"(x), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 clamp_fma2_hi(const f2 x, const f2 a, const f2 b) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] clamp"
+      : "=v"(r) : "v"(x), "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
 
 
@@ -996,6 +1010,24 @@ __global__ __launch_bounds__(512) void k_prep_counts(const uint32_t* __restrict_
   }
 }
 
+// Upload-time marshalling (hdg_pack_classes): (B, N, N) u8 class grid -> (B, N, ceil(N/32))
+// u32 rows, bit j of row i = (class(i, j) == 1), diagonal cleared -- the E_edge / C_edge
+// one-hots of utils2.py:82, 105 as hdg_batch's abits / ybits.  One thread per word.
+__global__ __launch_bounds__(256) void k_pack_classes(const uint8_t* __restrict__ cls, const int N,
+                                                      const int W, const long long words,
+                                                      uint32_t* __restrict__ bits) {
+  const long long w = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (w >= words) return;
+  const long long row = w / W;
+  const int wi = (int)(w - row * W), i = (int)(row % N), j0 = 32 * wi;
+  const uint8_t* src = cls + row * N + j0;
+  const int n = N - j0 < 32 ? N - j0 : 32;
+  uint32_t b = 0u;
+  for (int l = 0; l < n; ++l) b |= (src[l] == 1 ? 1u : 0u) << l;
+  if (i >= j0 && i < j0 + 32) b &= ~(1u << (i - j0));   // a_ii is not a relation
+  bits[w] = b;
+}
+
 // grid (B): mode 0 zeroes the class-count words of each commit, mode 1 turns the summed
 // u32 counts into the f32 values the step kernels read (exact: counts < 2^24)
 __global__ __launch_bounds__(256) void k_prep_ncst(uint32_t* __restrict__ prep, int Nc,
@@ -1041,7 +1073,7 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.dxp = o;  o += NE4;
   L.xsrt = o; o += NE4;
   L.perm = o; o += NE4;
-  L.xu = o;   o += NE4;
+  L.xu = o;   o += 2 * NE4;           // nd values, then +inf padding (E1's clamp-free search)
   L.cum = o;  o += NE4 + 4;
   L.pxd = o;  o += 2 * (NE4 + 4);     // f64 (offset is a multiple of 4 words)
   L.offr = o; o += NE4 + 4;           // CSR offsets of the entity neighbour lists
@@ -1208,30 +1240,41 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
     const float xi = xs[ic];
     const f2 u = __builtin_elementwise_fma((f2){xi, xi}, w0, c0);
     const f2 v = xi * w1;
+    // binary searches over the nd distinct values, padded with +inf up to 2 top_pow2(nd)
+    // (k_commit_step's stage): a probe past nd has z = +-inf (w = 0: NaN), which never
+    // moves a search whose answer is < nd; an answer of nd runs into the padding and is
+    // clamped once at the end -- no per-probe index clamp
     int br[2] = {0, 0}, bc[2] = {0, 0};
     for (int s = (ABL & 1) ? 0 : top_pow2(nd); s > 0; s >>= 1) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int mr = br[h] + s - 1, mc = bc[h] + s - 1;
-        const float xr = xu[mr < nd ? mr : nd - 1], xc = xu[mc < nd ? mc : nd - 1];
+        const float xr = xu[br[h] + s - 1], xc = xu[bc[h] + s - 1];
         const bool fr = (u[h] + xr * w1[h]) > 0.f;
         const bool fc = (fmaf(xc, w0[h], c0[h]) + v[h]) > 0.f;
-        br[h] = ((mr < nd) & (fr != ra[h])) ? br[h] + s : br[h];   // '&': no branch around
-        bc[h] = ((mc < nd) & (fc != ca[h])) ? bc[h] + s : bc[h];   // the clamped loads
+        br[h] = (fr != ra[h]) ? br[h] + s : br[h];
+        bc[h] = (fc != ca[h]) ? bc[h] + s : bc[h];
       }
     }
-    double tot[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      br[h] = br[h] < nd ? br[h] : nd;
+      bc[h] = bc[h] < nd ? bc[h] : nd;
+    }
+    // the a = 0 set sums: cnt u + w1 sum x (row side), cnt (v + c0) + w0 sum x (column
+    // side).  The x sums are differences of the f64 prefix table (exact to 2^-53 of the
+    // set, rounded once to f32); the rest in f32 with fma: the same rounding order as the
+    // reference graph's own f32 pair sums (f64 arithmetic costs ~5x f32 on gfx950)
+    float tot[2] = {0.f, 0.f};
     if constexpr (!(ABL & 2)) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int rlo = ra[h] ? br[h] : 0, rhi = ra[h] ? nd : br[h];
         const int clo = ca[h] ? bc[h] : 0, chi = ca[h] ? nd : bc[h];
-        double acc = (double)(cum[rhi] - cum[rlo]) * (double)u[h] +
-                     (double)w1[h] * (pxd[rhi] - pxd[rlo]);
-        acc += (double)(cum[chi] - cum[clo]) * ((double)v[h] + (double)c0[h]) +
-               (double)w0[h] * (pxd[chi] - pxd[clo]);
-        acc -= 2.0 * (double)reluf(u[h] + v[h]);
-        tot[h] = acc;
+        const float sxr = (float)(pxd[rhi] - pxd[rlo]), sxc = (float)(pxd[chi] - pxd[clo]);
+        const float nr = (float)(cum[rhi] - cum[rlo]), nc = (float)(cum[chi] - cum[clo]);
+        float acc = fmaf(nr, u[h], w1[h] * sxr);
+        acc += fmaf(nc, v[h] + c0[h], w0[h] * sxc);
+        tot[h] = fmaf(-2.f, reluf(u[h] + v[h]), acc);
       }
     }
     // a = 1 corrections relu(z0 + d) - relu(z0) = d clamp((s z0 + t) / d, 0, 1) with
@@ -1249,26 +1292,31 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
     // lanes of a node group (LDS broadcast): no id lookup, no cross-lane traffic
     // (eight per trip: two 16-byte reads in flight; xlr / xlc point into LDS when staged,
     // so the reads are ds_read_b128, not flat)
+    // (two accumulation chains; the x values used in place as packed halves)
     auto xsum = [&](const float* xl, int o, const int o1, const f2 ca, const f2 cb) {
+      f2 s0 = {0.f, 0.f}, s1 = s0;
       for (; o + 8 <= o1; o += 8) {
         const float4 xa = *reinterpret_cast<const float4*>(xl + o);
         const float4 xb = *reinterpret_cast<const float4*>(xl + o + 4);
-        sp += clamp_fma2(xa.x, ca, cb);
-        sp += clamp_fma2(xa.y, ca, cb);
-        sp += clamp_fma2(xa.z, ca, cb);
-        sp += clamp_fma2(xa.w, ca, cb);
-        sp += clamp_fma2(xb.x, ca, cb);
-        sp += clamp_fma2(xb.y, ca, cb);
-        sp += clamp_fma2(xb.z, ca, cb);
-        sp += clamp_fma2(xb.w, ca, cb);
+        const f2 a0 = {xa.x, xa.y}, a1 = {xa.z, xa.w}, b0 = {xb.x, xb.y}, b1 = {xb.z, xb.w};
+        s0 += clamp_fma2_lo(a0, ca, cb);
+        s1 += clamp_fma2_hi(a0, ca, cb);
+        s0 += clamp_fma2_lo(a1, ca, cb);
+        s1 += clamp_fma2_hi(a1, ca, cb);
+        s0 += clamp_fma2_lo(b0, ca, cb);
+        s1 += clamp_fma2_hi(b0, ca, cb);
+        s0 += clamp_fma2_lo(b1, ca, cb);
+        s1 += clamp_fma2_hi(b1, ca, cb);
       }
       if (o < o1) {
         const float4 xa = *reinterpret_cast<const float4*>(xl + o);
-        sp += clamp_fma2(xa.x, ca, cb);
-        sp += clamp_fma2(xa.y, ca, cb);
-        sp += clamp_fma2(xa.z, ca, cb);
-        sp += clamp_fma2(xa.w, ca, cb);
+        const f2 a0 = {xa.x, xa.y}, a1 = {xa.z, xa.w};
+        s0 += clamp_fma2_lo(a0, ca, cb);
+        s1 += clamp_fma2_hi(a0, ca, cb);
+        s0 += clamp_fma2_lo(a1, ca, cb);
+        s1 += clamp_fma2_hi(a1, ca, cb);
       }
+      sp += s0 + s1;
     };
     xsum(xlr, ((ABL & 4) || !live) ? 0 : offr[ic], ((ABL & 4) || !live) ? 0 : offr[ic + 1],
          sg * w1 * rd, __builtin_elementwise_fma(sg, u, tg) * rd);
@@ -1276,7 +1324,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
          sg * w0 * rd, __builtin_elementwise_fma(sg, c0 + v, tg) * rd);
     sp *= dd;
     if (live && kp < EG_L) {
-      const float2 P = make_float2((float)tot[0] + sp.x, (float)tot[1] + sp.y);
+      const float2 P = make_float2(tot[0] + sp.x, tot[1] + sp.y);
       *reinterpret_cast<float2*>(Ps + i * HS + k0) = P;
       *reinterpret_cast<float2*>(EG + i * HS + k0) = P;
       rq[i * HS + k0] = (uint16_t)br[0];
@@ -1557,6 +1605,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     msl = t / HS;                                                                       \
   } while (0)
   MID_STAMP();
+  // diagnostic (STAMPS builds only): lane 0 of every wave stamps slot s of its own row
+  // [2B][16 waves][8] after the 32-slot phase rows
+#define WAVE_STAMP(s)                                                                   \
+  do {                                                                                  \
+    if constexpr (STAMPS) {                                                             \
+      if ((threadIdx.x & 63) == 0)                                                      \
+        stamps[(size_t)(gridDim.x) * 32 + (prow * 16 + (threadIdx.x >> 6)) * 8 + (s)] = \
+            __builtin_amdgcn_s_memrealtime();                                           \
+    }                                                                                   \
+  } while (0)
   float* Ws = lds + L.W;
   float* xs = lds + L.xs;
   float* xps = lds + L.xps;
@@ -1666,10 +1724,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     perm[t] = pmv;
   }
   if (t <= nd) {
-    if (t < nd) xu[t] = xuv;
     cum[t] = cmv;
     pxd[t] = pxv;
   }
+  // the nd distinct values, +inf past them up to 2 NE4 >= 2 top_pow2(nd): E1's binary
+  // search probes indices < 2 top_pow2(nd) without clamping (entity_fwd)
+  if (t < 2 * NE4) xu[t] = t < nd ? xuv : INFINITY;     // 2 NE4 <= 512 < NT_MID
   if (t <= Ne) {
     offr[t] = orv;
     offc[t] = ocv;
@@ -1719,6 +1779,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
                EG, rq);
   else
     entity_fwd(t, Ws, xs, xu, cum, pxd, nd, offr, offc, xlistg, xlistg, nlo, nhi, Ps, EG, rq);
+  WAVE_STAMP(0);
   __syncthreads();
   MID_STAMP();
 
@@ -1998,9 +2059,8 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
   float ce_acc = 0.f, gsum = 0.f, corr = 0.f;
-  float zacc[HS];          // sum relu(kappa_k) gamma  (dU2, model_2.py:318-321)
-#pragma unroll
-  for (int k = 0; k < HS; ++k) zacc[k] = 0.f;
+  // dU2 = sum relu(kappa) gamma (model_2.py:318-321) is not accumulated per pair: it is
+  // rebuilt after the classifier backward from its row / column sums (M9)
   {
     const int Nc1i = Nc - 1;
     const float invNc1 = 1.f / (float)Nc1i;
@@ -2092,14 +2152,6 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         const float gmm = ce_scale * (p1 - yf);   // dL/dz1 = -dL/dz0
         gam[p * GLD + q] = gmm;
         gsum += gmm;
-#pragma unroll
-        for (int k = 0; k < HS; k += 2) {       // packed: two hidden units per v_pk_fma
-          typedef float p2 __attribute__((ext_vector_type(2)));
-          const p2 za = __builtin_elementwise_fma((p2){kap[k], kap[k + 1]}, (p2){gmm, gmm},
-                                                  (p2){zacc[k], zacc[k + 1]});
-          zacc[k] = za.x;
-          zacc[k + 1] = za.y;
-        }
       }
       qq += dqq;                              // next pair of this thread
       r += dr;
@@ -2109,15 +2161,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       }
     }
   }
-  if constexpr (TRAIN) {   // red[wv][0] CE, [1] sum gamma, [2 + k] dU2 terms, [2 + HS] count
-    float v[3 + HS];
-    v[0] = ce_acc;
-    v[1] = gsum;
-#pragma unroll
-    for (int k = 0; k < HS; ++k) v[2 + k] = zacc[k];
-    v[2 + HS] = corr;
+  WAVE_STAMP(1);
+  if constexpr (TRAIN) {   // red[wv][0] CE, [1] sum gamma, [2 + HS] count
+    float v[3] = {ce_acc, gsum, corr};
     float* rw = red + wv * 32;
-    wave_sums(v, lane, [&](int n, float x) { rw[n] = x; });
+    wave_sums(v, lane, [&](int n, float x) { rw[n < 2 ? n : 2 + HS] = x; });
   } else {
     const float s0 = wave_sum(ce_acc);
     const float sc = wave_sum(corr);
@@ -2125,14 +2173,13 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   __syncthreads();
   MID_STAMP();
-  if (t < 3 + HS) {
+  if (t < 3 + HS && (t < 2 || t == 2 + HS)) {
     float s = 0.f;
     for (int w = 0; w < NT_MID / 64; ++w) s += red[w * 32 + t];
     if (t == 0) pb[NP] = s;
     if (t == 2 + HS) pb[NP + 1] = s;        // correct-prediction count (integer, exact)
     if constexpr (TRAIN) {
       if (t == 1) { pb[H2_B2] = -s; pb[H2_B2 + 1] = s; }
-      if (t >= 2 && t < 2 + HS) { pb[H2_W2 + 2 * (t - 2)] = -s; pb[H2_W2 + 2 * (t - 2) + 1] = s; }
     }
   }
   if constexpr (!TRAIN) {         // uniform exit: forward-only launch (the H exchange was
@@ -2153,16 +2200,12 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   //          row sums Dsig (in place over sigma), column sums Dtau (over tau) -------
   float* Dsig = sig;
   float* Dtau = tau;
-  {
-    auto m8fix = [&](int j, int kk, float v) {     // dkappa = c (.) [kappa > 0] gamma
-      const float ck = cvec[kk];
-      Dsig[j * HS + kk] *= ck;
-      Dtau[j * HS + kk] = v * ck;
-    };
-    pair_pass<KK_MID, SMAXC, 2, HS, true, decltype(m8fix)>(
-        Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr, nullptr, gam, GLD, Dsig, Dtau, ysumv,
-        credg, rmul, radd, m8fix);
-  }
+  // Dsig / Dtau here are the sums of [kappa > 0] gamma WITHOUT the factor c of
+  // dkappa = c (.) [kappa > 0] gamma: M9 applies c to the sums it forms, and the dG / dH
+  // tiles take it in M c (c scales a column of the sums, so nothing is lost)
+  pair_pass<KK_MID, SMAXC, 2, HS, true>(Nc, tg, sig, tau, g * KK_MID, eps, yb, WC, nullptr,
+                                           nullptr, gam, GLD, Dsig, Dtau, ysumv, credg, rmul,
+                                           radd);
   if constexpr (SPLIT) pair_send(Dtau, Nc * HS, xout + XS, xtag(epoch, 2) ^ xsend, t);   // received in M9
   MID_STAMP();
   // ---- M9: X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p; classifier / hunk-MLP grads ----
@@ -2203,16 +2246,21 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     }
     if (half == 1) xtile();
     __syncthreads();
+    float* Xp = xpart + 16 * 256;                      // X' (no c) [22][HS], then M c [HS][HS]
+    float* Mc = Xp + 22 * HS;
     {
       const int tl2 = t >> 8, e = t & 255;
       const float v = (xpart[(0 * 4 + tl2) * 256 + e] + xpart[(1 * 4 + tl2) * 256 + e]) +
                       (xpart[(2 * 4 + tl2) * 256 + e] + xpart[(3 * 4 + tl2) * 256 + e]);
       const int l = (tl2 >> 1) * 16 + (e >> 4), m = (tl2 & 1) * 16 + (e & 15);
-      if (m < HS) {
-        if (l < HS) Xm[l * HS + m] = v;
-        else if (l == HS) sumD[m] = v;                  // sum_p Dsig (completed below)
-        else if (l == HS + 1) red[m] = v;               // sum_p Dtau
+      if (m < HS && l < HS + 2) {
+        Xp[l * HS + m] = v;
+        const float vc = v * cvec[m];                   // dkappa's factor c (see M8)
+        if (l < HS) Xm[l * HS + m] = vc;
+        else if (l == HS) sumD[m] = vc;                 // sum_p Dsig (completed below)
+        else red[m] = vc;                               // sum_p Dtau
       }
+      if (t < HS * HS) Mc[t] = Mm[t] * cvec[t % HS];   // dG = Dsig' (M c)^T
     }
     __syncthreads();
     if (t < HS) {
@@ -2222,6 +2270,16 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       pb[H2_W1 + HS + t] = dy1;
       pb[H2_W1 + t] = dd1 - dy1;
       sumD[t] = dd1 + dt;
+      // dU2 (model_2.py:318-321): Z_k = sum_pq relu(kappa_pq,k) gamma_pq
+      //   = sum_pq [kappa > 0] gamma (sigma_pk + tau_qk + y eps_k)
+      //   = sum_l M_lk X'_lk + s0_k sum_p Dsig'_pk + t0_k sum_q Dtau'_qk + eps_k ysum_k
+      // (sigma = G M + s0, tau = H M + t0; X' = sum_p G_p (x) Dsig'_p + H_p (x) Dtau'_p):
+      // the per-pair accumulation of the classifier pass, from sums this block has anyway
+      float z = fmaf(s0v[t], Xp[HS * HS + t], fmaf(t0v[t], Xp[(HS + 1) * HS + t], eps[t] * ysumv[t]));
+#pragma unroll
+      for (int l = 0; l < HS; ++l) z = fmaf(Mm[l * HS + t], Xp[l * HS + t], z);
+      pb[H2_W2 + 2 * t] = -z;
+      pb[H2_W2 + 2 * t + 1] = z;
     }
   }
   __syncthreads();
@@ -2257,8 +2315,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     const int which = tt & 1, row0 = (tt >> 2) * 16, col0 = ((tt >> 1) & 1) * 16;
     const float* src = which ? Dtau : Dsig;
     const int pr = row0 + (lane & 15), lc = col0 + (lane & 15);
+    const float* Mcm = U + NBUF_H * NC16 * HS + 16 * 256 + 22 * HS;   // M c (M9)
     const f4v c = mfma_tile16_p(pr < Nc ? src + pr * HS : kzero, pr < Nc ? 1 : 0,
-                                lc < HS ? Mm + lc * HS : kzero, lc < HS ? 1 : 0, HS, lane);
+                                lc < HS ? Mcm + lc * HS : kzero, lc < HS ? 1 : 0, HS, lane);
     const int l = col0 + (lane & 15);
     if (l < HS) {
       float* dst = which ? dH : dG;
@@ -2581,6 +2640,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     if (4 * t < rl) *reinterpret_cast<float4*>(Ps + xl2o + 4 * t) = e2x;
   }
   if (t <= Ne) offc[t] = e2off;
+  WAVE_STAMP(3);
   for (int k = wv; k < HS; k += NT_MID / 64) {        // wave-uniform; both tables of unit k
     const bool suf = Ws[E1_W1 + HS + k] >= 0.f;      // from one gather of rho
     float* T0 = Tr + k * TL;
@@ -2621,6 +2681,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       T1[suf ? Ne : 0] = 0.f;
     }
   }
+  WAVE_STAMP(4);
   __syncthreads();
   MID_STAMP();
   if (rfit)
@@ -2630,6 +2691,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc,
                reinterpret_cast<const uint8_t*>(pp + PL.lists),
                reinterpret_cast<const float*>(pp + PL.xl), nlo, nhi, red2);
+  WAVE_STAMP(2);
   __syncthreads();
   if (t < 4 * HS) {
     const int w = t / HS, k = t - w * HS;
@@ -2657,6 +2719,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   MID_STAMP();
 #undef MID_STAMP
+#undef WAVE_STAMP
 }
 
 // ------------------------------------------------------------------------------
@@ -2766,6 +2829,8 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
   if (threadIdx.x >= RED_P) return;
   if (p == CNT_SLOT) put_count(grad + p, cnt);
   else if (p < CNT_SLOT || (p > CNT_SLOT + 2 && p < GRAD_LEN)) grad[p] = g;
+  if (stats && p == CNT_SLOT) put_count(stats + 4, cnt);
+  if (stats && p == NP + HDG_TR_FAULT) stats[7] = g;
   if (p == NP) {
     const float ce = g * inv_pairs;
     if (stats) {
@@ -2857,6 +2922,7 @@ __global__ __launch_bounds__(1024) void k_adam_tf(float* __restrict__ params,
     stats[1] = lmap;
     stats[2] = lpara;
     stats[3] = 10.f * ce + 0.1f * lmap + lpara;
+    for (int q = 0; q < 4; ++q) stats[4 + q] = grad[np + HDG_TR_COUNT + q];   // count, fault
   }
   if (fault != 0.f) return;   // a pair exchange timed out on some rank: no update
   const float b1 = 0.9f, b2 = 0.999f, ep = 1e-8f;
@@ -3014,6 +3080,8 @@ __global__ __launch_bounds__(1024) void k_dp_tail(const float* __restrict__ src,
   if (anylate && t == 0 && status) xstore1(status, HDG_STATUS_DP_TIMEOUT);
   if constexpr (MODE == dpk::SUM) return;
   const int TH1 = np - 4, TH2 = np - 2;
+  if (stats && p >= np + HDG_TR_COUNT && p <= np + HDG_TR_FAULT)   // count parts, fault
+    stats[4 + (p - np - HDG_TR_COUNT)] = tot;
   if (p == np + HDG_TR_CE && stats) {
     const float ce = tot * inv_pairs;
     stats[0] = ce;
@@ -3254,31 +3322,35 @@ hipError_t set_step_attr() {
   return hipSuccess;
 }
 
-// resident split-mode blocks per CU for this shape (cached per device and tile count)
+// resident split-mode blocks per CU for this shape: the kernel's register / wave limit
+// (occupancy query, memoized per device and tile count: it does not depend on the
+// shape) combined per call with the shape's LDS bytes
 template <int SMAXC>
 int split_blocks_per_cu(const hdg_shape* s) {
-  static int cache[16] = {0};
+  static int regs_cache[16] = {0};   // idempotent memo of a device query
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
-  if (cache[dev] == 0) {
+  int nb = __atomic_load_n(&regs_cache[dev], __ATOMIC_RELAXED);
+  if (nb == 0) {
     if (set_step_attr<SMAXC, true, false, true>() != hipSuccess) return 0;
     // registers / waves from the occupancy query (without dynamic LDS: the query rejects
-    // sizes above the default 64 KiB limit), LDS from the CU's 160 KiB
-    int nb = 0;
-    const size_t lds = (size_t)step_layout(s->ne, s->nc, SMAXC).total * 4;
+    // sizes above the default 64 KiB limit)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &nb, (const void*)k_commit_step<SMAXC, true, false, true>, NT_MID, 0) != hipSuccess) {
       (void)hipGetLastError();      // leave no sticky error for the launch's check
       return 0;
     }
-    const int by_lds = lds > 0 ? (int)((160 * 1024) / lds) : nb;
-    nb = nb < by_lds ? nb : by_lds;
-    cache[dev] = nb > 0 ? nb : -1;
+    nb = nb > 0 ? nb : -1;
+    __atomic_store_n(&regs_cache[dev], nb, __ATOMIC_RELAXED);
   }
-  return cache[dev] > 0 ? cache[dev] : 0;
+  if (nb < 0) return 0;
+  const size_t lds = (size_t)step_layout(s->ne, s->nc, SMAXC).total * 4;   // this shape
+  const int by_lds = lds > 0 ? (int)((160 * 1024) / lds) : nb;
+  return nb < by_lds ? nb : by_lds;
 }
 
 bool use_split(const hdg_shape* s) {
+  if (s->flags & HDG_FLAG_NO_SPLIT) return false;
   const char* e = getenv("HDG_FUSED_SPLIT");
   if (e && e[0] == '0') return false;
   int per_cu = 0;
@@ -3497,6 +3569,18 @@ int hdg_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, int
   *ks = L.ks;
   *kt = L.kt;
   *ncst = L.ncst;
+  return 0;
+}
+
+int hdg_pack_classes(const uint8_t* cls, int32_t batch, int32_t n, uint32_t* bits,
+                     void* stream) {
+  if (!cls || !bits || batch < 1 || n < 1)
+    return fail(HDG_EINVAL, "hdg_pack_classes: NULL pointer or batch=%d n=%d", batch, n);
+  const int W = (n + 31) / 32;
+  const long long words = (long long)batch * n * W;
+  hipLaunchKernelGGL(k_pack_classes, dim3((unsigned)((words + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, cls, n, W, words, bits);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

@@ -17,7 +17,7 @@ __global__ __launch_bounds__(1024) void mb_e1(int Ne, int iters, float* out, flo
   for (int i = t; i < 2128; i += 1024) Ws[i] = 0.01f * (float)((i * 2654435761u) % 200) - 1.f;
   for (int i = t; i < Ne; i += 1024) xs[i] = (float)((i * 7 + b) % 10);
   __syncthreads();
-  if (t < 10) { xu[t] = (float)t; }
+  if (t < 256) xu[t] = t < 10 ? (float)t : INFINITY;   // entity_fwd: +inf past nd
   if (t <= 10) { cum[t] = t * Ne / 10; pxd[t] = 0.0; }
   if (t == 0) {              // ~5 % density: degree 8..12 per row and column
     int ar = 0, ac = 0;

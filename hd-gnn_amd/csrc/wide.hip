@@ -2416,9 +2416,15 @@ __device__ __forceinline__ void reduce_adam_slot(int p, int np, float g, unsigne
     grad[p] = (float)(c & 0xFFFFull);
     grad[p + 1] = (float)((c >> 16) & 0xFFFFull);
     grad[p + 2] = (float)(c >> 32);
+    if (stats) {                                   // stats[4..6]: the count's parts
+      stats[4] = grad[p];
+      stats[5] = grad[p + 1];
+      stats[6] = grad[p + 2];
+    }
     return;
   }
   grad[p] = g;
+  if (p == np + HDG_TR_FAULT && stats) stats[7] = g;
   if (p == np + HDG_TR_CE && stats) {
     const float ce = g * inv_pairs;
     stats[0] = ce;

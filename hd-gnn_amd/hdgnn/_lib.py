@@ -17,10 +17,12 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libhdgnn.so")
 class Shape(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("ne", ctypes.c_int32), ("nc", ctypes.c_int32),
                 ("variant", ctypes.c_int32), ("batch_global", ctypes.c_int32),
-                ("path", ctypes.c_int32)]
+                ("path", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 PATH_AUTO, PATH_FUSED, PATH_GENERAL = 0, 1, 2
+FLAG_NO_SPLIT = 1
+STATS_LEN = 8          # hdg_outputs.stats: ce, loss_map, loss_para, train_loss, count x3, fault
 
 
 class Batch(ctypes.Structure):
@@ -64,7 +66,8 @@ EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count
            "hdg_fwd_bwd_events", "hdg_adam_tf", "hdg_train_step", "hdg_forward",
            "hdg_debug_step_stamps", "hdg_prep_counts_layout", "hdg_dp_mailbox_bytes",
            "hdg_dp_mailbox_alloc", "hdg_dp_mailbox_open", "hdg_dp_mailbox_close",
-           "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce"]
+           "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce",
+           "hdg_pack_classes"]
 
 _lib = None
 
@@ -94,6 +97,7 @@ def load(path=None):
     lib.hdg_prep_counts_layout.argtypes = [P(Shape)] + [P(ctypes.c_int64)] * 4
     lib.hdg_prep_counts_layout.restype = ctypes.c_int
     lib.hdg_prepare.argtypes = [P(Shape), P(Batch), vp]
+    lib.hdg_pack_classes.argtypes = [vp, i32, i32, vp, vp]
     lib.hdg_fwd_bwd.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp]
     lib.hdg_fwd_bwd_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp, vp]
     lib.hdg_debug_step_stamps.argtypes = [P(Shape), P(Batch), vp, vp, vp, vp]

@@ -87,8 +87,9 @@ class CommitBatch:
         Nc = self.y.shape[1]
         assert self.a.shape == (B, Ne, Ne) and self.y.shape == (B, Nc, Nc)
         assert self.hid.shape == (B, Ne) and self.nlen.shape == (B,)
-        if not np.all(np.isin(self.a, (0, 1))) or not np.all(np.isin(self.y, (0, 1))):
-            raise ValueError("edge classes must be 0/1")
+        for m in (self.a, self.y):         # classes in {0, 1}: two reductions, no np.isin
+            if m.size and (m.max() > 1 or (m.dtype.kind != "u" and m.min() < 0)):
+                raise ValueError("edge classes must be 0/1")
         if np.any(self.hid < -1) or np.any(self.hid >= Nc):
             raise ValueError("hid entries must be in [-1, Nc)")
         if np.any(self.nlen < 0) or np.any(self.nlen > Ne):
@@ -127,14 +128,35 @@ class DeviceBatch:
 
     @classmethod
     def from_host(cls, cb, device="cuda", variant=2, path=0):
+        """Upload: the compact u8 class grids travel as they are (through pinned staging
+        buffers, asynchronously) and are packed into bit rows on the GPU
+        (hdg_pack_classes); then hdg_prepare.  No host-side bit packing."""
         import torch
+        from . import _lib
         cb.validate()
-        t = lambda arr, dt: torch.from_numpy(np.ascontiguousarray(arr)).to(device=device, dtype=dt)
-        return cls(t(cb.x.astype(np.float32), torch.float32),
-                   t(pack_bits(cb.a).view(np.int32), torch.int32),
-                   t(pack_bits(cb.y).view(np.int32), torch.int32),
-                   t(cb.hid.astype(np.int32), torch.int32),
-                   t(cb.nlen.astype(np.int32), torch.int32), cb.Ne, cb.Nc, variant, path)
+        device = torch.device(device)
+
+        def up(arr, dt):
+            host = torch.from_numpy(np.ascontiguousarray(arr))
+            if host.dtype != dt:
+                host = host.to(dt)
+            staged = torch.empty(host.shape, dtype=dt, pin_memory=True)
+            staged.copy_(host)
+            return staged.to(device, non_blocking=True)
+
+        lib = _lib.load()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+        def bits(grid):
+            g = up(grid, torch.uint8)
+            B, N = grid.shape[0], grid.shape[1]
+            out = torch.empty((B, N, (N + 31) // 32), dtype=torch.int32, device=device)
+            _lib.check(lib.hdg_pack_classes(ctypes.c_void_p(g.data_ptr()), B, N,
+                                            ctypes.c_void_p(out.data_ptr()), stream))
+            return out                      # g's memory is reused in stream order only
+
+        return cls(up(cb.x, torch.float32), bits(cb.a), bits(cb.y), up(cb.hid, torch.int32),
+                   up(cb.nlen, torch.int32), cb.Ne, cb.Nc, variant, path)
 
     def struct(self):
         from ._lib import Batch

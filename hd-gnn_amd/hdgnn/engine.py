@@ -10,6 +10,7 @@ every rank is on this node, else torch.distributed (RCCL); HDG_DP_ALLREDUCE or t
 """
 import ctypes
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -50,7 +51,8 @@ class Engine:
         self.v = torch.zeros(self.np, dtype=f32, device=dev)
         self.beta_pow = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
         self.grad = torch.zeros(self.glen, dtype=f32, device=dev)
-        self.stats = torch.zeros(4, dtype=f32, device=dev)
+        # ce, loss_map, loss_para, train_loss, count parts (3), fault count (hdg_outputs.stats)
+        self.stats = torch.zeros(_lib.STATS_LEN, dtype=f32, device=dev)
         # sticky status word (HDG_STATUS_* bits); check_status() reads it
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ce_sum = torch.zeros(1, dtype=f32, device=dev)
@@ -109,10 +111,63 @@ class Engine:
             raise ValueError("batch prepared for path %d, engine runs path %d (use "
                              "Engine.upload)" % (dbatch.path, self.path))
 
-    def _outputs(self, outputs, logits):
+    def _outputs(self, outputs, logits, stats=None):
         if not outputs:
             return self._out_none
-        return self._out if logits else self._out_train
+        out = self._out if logits else self._out_train
+        if stats is None:
+            return out
+        # a caller-provided stats row (a training loop's per-step row of an epoch buffer)
+        assert stats.device == self.device and stats.dtype == torch.float32 and \
+            stats.is_contiguous() and stats.numel() >= _lib.STATS_LEN
+        return _lib.Outputs(out.probs, out.logits, stats.data_ptr(), out.status, out.ehr)
+
+    # ---- split mode (fused path: two co-resident blocks per commit) -------------------
+    @property
+    def split(self):
+        """False once set_split(False) forced one block per commit (HDG_FLAG_NO_SPLIT)."""
+        return not (self.shape.flags & _lib.FLAG_NO_SPLIT)
+
+    def set_split(self, on):
+        self.shape.flags = (self.shape.flags & ~_lib.FLAG_NO_SPLIT) | (0 if on else
+                                                                       _lib.FLAG_NO_SPLIT)
+
+    def snapshot(self):
+        """Device copies of the training state (parameters, Adam moments, beta powers)."""
+        return [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
+
+    def restore(self, snap):
+        for t, v in zip((self.params, self.m, self.v, self.beta_pow), snap):
+            t.copy_(v)
+
+    def split_fault_retry(self):
+        """After a step whose block-pair exchange timed out (HDG_STATUS_XCH_TIMEOUT; its
+        update was skipped on every rank, the fault count travels in the all-reduced
+        gradient trailer): switch to one block per commit for the rest of the run and
+        clear the status, so the caller re-runs the step.  Returns False when already in
+        one-block mode (the fault is then not a residency problem)."""
+        if not self.split:
+            return False
+        warnings.warn("libhdgnn: a split-mode block-pair exchange timed out (the two blocks "
+                      "of a commit were not co-resident); re-running in one-block-per-commit "
+                      "mode for the rest of this run", RuntimeWarning, stacklevel=2)
+        self.set_split(False)
+        self.clear_status()
+        return True
+
+    def train_step_checked(self, dbatch, outputs=True, logits=False, stats=None):
+        """train_step that survives a split-mode pair timeout: on a faulted step (read from
+        the gradient trailer, identical on every rank) the state is restored and the step
+        re-run with one block per commit.  Synchronises with the device once."""
+        snap = self.snapshot() if self.split else None
+        self.train_step(dbatch, outputs, logits, stats)
+        fault = float(self.grad[self.np + _lib.TR_FAULT].item())
+        if fault != 0.0 and snap is not None and self.split_fault_retry():
+            self.restore(snap)
+            self.train_step(dbatch, outputs, logits, stats)
+            fault = float(self.grad[self.np + _lib.TR_FAULT].item())
+        if fault != 0.0 or int(self.status.item()):
+            self.check_status()
 
     # ---- status / trailer -----------------------------------------------------
     def check_status(self):
@@ -143,6 +198,7 @@ class Engine:
         return _lib.trailer_count(tr.cpu().numpy() if hasattr(tr, "cpu") else tr)
 
     def fwd_bwd(self, dbatch, outputs=True, logits=True):
+        self._reduced = False
         self._check(dbatch)
         b = dbatch.struct()
         out = self._outputs(outputs, logits)
@@ -154,13 +210,27 @@ class Engine:
                                         self._stream()))
 
     def allreduce(self):
-        """RCCL path: all-reduce the flat gradient in place.  xGMI path: nothing here, the
-        exchange runs inside adam() (hdg_adam_dp)."""
-        if self._distributed() and not self.xgmi:
-            torch.distributed.all_reduce(self.grad, group=self.pg)
+        """All-reduce the flat gradient: RCCL in place on self.grad; xGMI from the local
+        gradient fwd_bwd wrote (grad_local) into self.grad (hdg_dp_allreduce).  Either way
+        self.grad then holds the world sum, and adam() applies TF Adam to it."""
+        if not self._distributed():
+            return
+        if self.xgmi:
+            _lib.check(self.lib.hdg_dp_allreduce(ctypes.byref(self.xgmi.dp),
+                                                 ctypes.c_void_p(self.grad_local.data_ptr()),
+                                                 ctypes.c_void_p(self.grad.data_ptr()),
+                                                 ctypes.c_int32(self.glen),
+                                                 ctypes.c_void_p(self.status.data_ptr()),
+                                                 self._stream()))
+            self._reduced = True
+            return
+        torch.distributed.all_reduce(self.grad, group=self.pg)
 
     def adam(self):
-        if self.xgmi:
+        """TF Adam on the world gradient.  xGMI: when allreduce() already summed it into
+        self.grad, a local update of that sum (every rank holds the same bits); otherwise
+        the exchange and the update in one kernel (hdg_adam_dp, from grad_local)."""
+        if self.xgmi and not getattr(self, "_reduced", False):
             _lib.check(self.lib.hdg_adam_dp(ctypes.byref(self.shape), ctypes.byref(self._state),
                                             ctypes.c_void_p(self.grad_local.data_ptr()),
                                             ctypes.c_void_p(self.grad.data_ptr()),
@@ -169,6 +239,7 @@ class Engine:
                                             ctypes.c_void_p(self.status.data_ptr()),
                                             ctypes.byref(self.xgmi.dp), self._stream()))
             return
+        self._reduced = False
         _lib.check(self.lib.hdg_adam_tf(ctypes.byref(self.shape), ctypes.byref(self._state),
                                         ctypes.c_void_p(self.grad.data_ptr()),
                                         ctypes.c_float(self.lr),
@@ -179,17 +250,19 @@ class Engine:
                                        and torch.distributed.is_initialized()
                                        and torch.distributed.get_world_size() > 1)
 
-    def train_step(self, dbatch, outputs=True, logits=False):
+    def train_step(self, dbatch, outputs=True, logits=False, stats=None):
         """sess.run([C_edge_output2, loss_Hedge_mse, loss_map, theta, trainer]) equivalent:
         outputs land in self.probs / self.stats (pre-update), params updated in place;
-        self.logits only with logits=True (the reference's training run does not fetch them).
+        self.logits only with logits=True (the reference's training run does not fetch them);
+        stats: a device row of >= 8 floats for this step's hdg_outputs.stats instead of
+        self.stats (so a loop can keep every step's values and read them once).
         Single process: hdg_train_step (step kernel + fused reduce/Adam).  Data parallel
         over xGMI: hdg_train_step_dp (the same two kernels, the exchange inside the second).
         Over RCCL: hdg_fwd_bwd -> all-reduce of the flat gradient -> hdg_adam_tf."""
         if self.xgmi:
             self._check(dbatch)
             b = dbatch.struct()
-            out = self._outputs(outputs, logits)
+            out = self._outputs(outputs, logits, stats)
             _lib.check(self.lib.hdg_train_step_dp(ctypes.byref(self.shape), ctypes.byref(b),
                                                   ctypes.byref(self._state),
                                                   ctypes.c_float(self.lr), ctypes.byref(out),
@@ -201,10 +274,12 @@ class Engine:
             self.fwd_bwd(dbatch, outputs, logits)
             self.allreduce()
             self.adam()
+            if stats is not None:
+                stats[:_lib.STATS_LEN].copy_(self.stats)
             return
         self._check(dbatch)
         b = dbatch.struct()
-        out = self._outputs(outputs, logits)
+        out = self._outputs(outputs, logits, stats)
         _lib.check(self.lib.hdg_train_step(ctypes.byref(self.shape), ctypes.byref(b),
                                            ctypes.byref(self._state), ctypes.c_float(self.lr),
                                            ctypes.byref(out),

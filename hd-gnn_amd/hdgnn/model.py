@@ -119,7 +119,7 @@ class graph2graph(object):
 
     def __init__(self, sess, Ds, Ne, Nc, Ner, Ncr, Dr, De_e, De_er, Mini_batch, checkpoint_dir,
                  epoch, Ds_inter, Dr_inter, Step, Repo, *, reader=None, device=None, seed=0,
-                 lr=3e-4, process_group=None, loader="utils2", data_root="."):
+                 lr=3e-4, process_group=None, loader="utils2", data_root=".", compact=None):
         self.sess = sess                       # accepted and ignored (no TF session)
         self.Ds, self.Ne, self.Nc, self.Ner, self.Ncr, self.Dr = Ds, Ne, Nc, Ner, Ncr, Dr
         self.Ds_inter, self.Dr_inter = Ds_inter, Dr_inter
@@ -132,6 +132,9 @@ class graph2graph(object):
         if loader not in ("utils2", "fast"):
             raise ValueError("loader must be 'utils2' (the reference read_data) or 'fast'")
         self.loader, self.data_root = loader, data_root
+        # (train, test, maps) CommitBatches already in compact form (hdgnn.loader.read_compact,
+        # a synthetic generator): used instead of reading the dataset
+        self._given = compact
         self.seed, self.lr, self.pg = seed, lr, process_group
         self.device = device
         if (Ds, Dr, De_e, De_er) != (1, 2, HS, HS):
@@ -189,6 +192,9 @@ class graph2graph(object):
         """-> (C_edge_train, C_edge_test, train, test, maps).  'utils2': the reference's
         read_data 12-tuple through the bit-exact adapter; 'fast': hdgnn.loader reads the same
         files straight into the compact form (no dense arrays, no progress-bar sleeps)."""
+        if self._given is not None:
+            train, test, maps = self._given
+            return onehot_relations(train.y), onehot_relations(test.y), train, test, maps
         if self.loader == "fast":
             from .loader import read_compact
             train, test, maps = read_compact(self.Repo, self.Step, self.Ne, self.Nc,
@@ -226,7 +232,20 @@ class graph2graph(object):
         return t.item()
 
     # ------------------------------------------------------------------ train
+    def _barrier(self):
+        """Ranks meet before the first step and after rank 0's host work of an epoch, so no
+        rank enters a data-parallel step far behind its peers (the xGMI exchange waits a
+        bounded time for peer words)."""
+        if self.world > 1:
+            import torch
+            torch.distributed.barrier(group=self.pg)
+
     def train(self, args):
+        """model_2.py:335-424.  Every step's pre-update losses and top_ACC count land in its
+        own row of an epoch buffer on the device (hdg_outputs.stats), read once per epoch:
+        no host synchronisation inside the epoch.  A split-mode exchange timeout (the
+        step's update skipped, the fault count in every rank's stats) re-runs the epoch
+        from its starting state with one block per commit (Engine.split_fault_retry)."""
         import torch
         self._initialize()
         _, _, train, _, maps = self._compact()
@@ -235,28 +254,30 @@ class graph2graph(object):
         counter = 1
         start_time1 = time.time()
         eng = self.engine
+        es = torch.zeros(max(nb, 1), _lib.STATS_LEN, dtype=torch.float32, device=eng.device)
+        self._barrier()
         for i in range(self.epoch):
-            tr_loss_Hedge = 0.0
-            tr_loss_map = 0.0
-            correct = 0
-            for j, db in enumerate(batches):
-                eng.train_step(db, logits=self.fetch_logits)
-                # one small copy per step: pre-update losses (like sess.run), the
-                # on-device top_ACC numerator (gradient trailer count slots; already
-                # summed over ranks by the data-parallel all-reduce) and the status word
-                host = torch.cat([eng.stats, eng.grad[eng.np:eng.np + _lib.TRAILER],
-                                  eng.status.float()]).cpu().numpy()
-                if host[-1] != 0:
-                    eng.check_status()
-                tr_loss_Hedge += float(host[0])
-                tr_loss_map += float(host[1])
-                self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[0]),
-                                                                      float(host[1]),
-                                                                      float(host[2]))
+            snap = eng.snapshot() if eng.split and eng.path == _lib.PATH_FUSED else None
+            while True:
+                for j, db in enumerate(batches):
+                    eng.train_step(db, logits=self.fetch_logits, stats=es[j])
+                host = es.cpu().numpy().astype(np.float64)    # the epoch's one synchronisation
+                if host[:nb, 7].any() and snap is not None and eng.split_fault_retry():
+                    eng.restore(snap)
+                    continue
+                break
+            if host[:nb, 7].any() or int(eng.status.item()):
+                eng.check_status()
+            tr_loss_Hedge = float(host[:nb, 0].sum())
+            tr_loss_map = float(host[:nb, 1].sum())
+            correct = sum(int(round(r[4])) + (int(round(r[5])) << 16) + (int(round(r[6])) << 32)
+                          for r in host[:nb])
+            if nb:
+                self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[nb - 1, 0]),
+                                                                      float(host[nb - 1, 1]),
+                                                                      float(host[nb - 1, 2]))
                 self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
                 self.C_edge_output2_logits = eng.logits if self.fetch_logits else None
-                correct += _lib.trailer_count(host[4:4 + _lib.TRAILER])
-            torch.cuda.synchronize(eng.device)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
             theta = self.theta.reshape([2])
             resultString = "Epoch " + str(i + 1) + \
@@ -273,6 +294,7 @@ class graph2graph(object):
                 print(resultString)
             counter += 1
             self.save(args.checkpoint_dir, counter)
+            self._barrier()
         end_time1 = time.time()
         if self.rank == 0:
             print('test time:' + str(end_time1 - start_time1))

@@ -24,7 +24,9 @@
  *     of a failed launch; hdg_last_error() gives a thread-local message.
  *   - parameters are one flat fp32 vector in tf.global_variables() order with TF
  *     (in,out) row-major weights (hdg_param_count()).
- *   - the library keeps no global mutable state apart from the thread-local error.
+ *   - the library keeps no global mutable state apart from the thread-local error and
+ *     memos of per-device queries (kernel attributes set, occupancy per kernel and LDS
+ *     size): idempotent, the same answer for every caller.
  */
 #ifndef HDGNN_H
 #define HDGNN_H
@@ -48,7 +50,13 @@ typedef struct hdg_shape {
                            4 HD-GNN                                      */
     int32_t batch_global; /* commits summed by the CE mean across all ranks         */
     int32_t path;       /* HDG_PATH_AUTO / _FUSED / _GENERAL (see below)           */
+    int32_t flags;      /* HDG_FLAG_* bits, 0 for the defaults                      */
 } hdg_shape;
+/* HDG_FLAG_NO_SPLIT: the fused path runs one block per commit even where split mode
+ * (two co-resident blocks per commit, see hdg_workspace_bytes) would apply: what a
+ * caller retries with after HDG_STATUS_XCH_TIMEOUT.  Same results up to fp32
+ * re-association of the block-pair sums.                                              */
+#define HDG_FLAG_NO_SPLIT 1
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
  * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge
@@ -87,8 +95,11 @@ typedef struct hdg_state {
 typedef struct hdg_outputs {
     float* probs;        /* [B][2][nc(nc-1)]  C_edge_output2        */
     float* logits;       /* [B][2][nc(nc-1)]  C_edge_output2_logits */
-    float* stats;        /* [4] ce (loss_Hedge_mse), loss_map, loss_para, train_loss
-                            (pre-update values, as sess.run returns them)              */
+    float* stats;        /* [8] ce (loss_Hedge_mse), loss_map, loss_para, train_loss
+                            (pre-update values, as sess.run returns them), then the
+                            step's gradient trailer slots HDG_TR_COUNT..HDG_TR_FAULT
+                            (top_ACC count parts, fault count): a training loop points
+                            each step at its own row and reads a whole epoch at once  */
     uint32_t* status;    /* [1] sticky device status word: the library ORs HDG_STATUS_*
                             bits into it (write-through store) and never clears it; the
                             caller zeroes it and reads it whenever it synchronises     */
@@ -149,6 +160,12 @@ int         hdg_prep_counts_layout(const hdg_shape* shape, int64_t* stride_words
  * re-call whenever the batch contents change.  Replaces nothing in the reference: it is
  * the device-side half of the feed_dict marshalling (utils2.py:111-137, 248-253).    */
 int hdg_prepare(const hdg_shape* shape, const hdg_batch* batch, void* stream);
+/* Upload helper: a (batch, n, n) u8 class grid on the device (class of relation (i, j),
+ * 0 or 1: the E_edge / C_edge one-hots of utils2.py:82, 105) -> the (batch, n,
+ * ceil(n/32)) u32 bit rows hdg_batch.abits / ybits hold (bit j of row i = class 1,
+ * diagonal cleared).  Lets a caller ship the compact grids and pack them on the GPU. */
+int hdg_pack_classes(const uint8_t* cls, int32_t batch, int32_t n, uint32_t* bits,
+                     void* stream);
 
 int hdg_fwd_bwd(const hdg_shape* shape, const hdg_batch* batch, const float* params,
                 float* grad, hdg_outputs* out, void* workspace, void* stream);

@@ -138,3 +138,58 @@ def test_count_beyond_fp32_integer_range():
     want = metrics.top_acc_count(onehot_relations(cb.y), eng.probs.cpu().numpy())
     assert want > 2 ** 24
     assert eng.correct_count() == want
+
+
+def test_train_timeout_retried_in_one_block_mode(fused_split, monkeypatch):
+    """Engine.train_step_checked: the faulted split step (update skipped) is re-run with one
+    block per commit (HDG_FLAG_NO_SPLIT) and the run stays there; the result equals a
+    clean one-block step.  HDG_DEBUG_XCH_FAULT only corrupts split-mode exchanges."""
+    eng, db = fused_split
+    monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+    with pytest.warns(RuntimeWarning, match="one-block"):
+        eng.train_step_checked(db)
+    assert not eng.split and int(eng.status.item()) == 0
+    eng.train_step_checked(db)                 # stays in one-block mode: no new fault
+    torch.cuda.synchronize()
+    monkeypatch.delenv("HDG_DEBUG_XCH_FAULT")
+    from hdgnn.engine import Engine
+    ref = Engine(NE, NC, B, variant=eng.variant, path=_lib.PATH_FUSED)
+    ref.set_split(False)
+    ref.set_params(layout.init_flat(5, eng.variant))
+    rdb = ref.upload(synth_commits(B, NE, NC, 7))
+    ref.train_step(rdb)
+    ref.train_step(rdb)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.params, ref.params)
+    assert torch.equal(eng.m, ref.m) and torch.equal(eng.beta_pow, ref.beta_pow)
+
+
+def test_model_train_epoch_retry(monkeypatch, tmp_path):
+    """graph2graph.train re-runs a faulted epoch from its starting state in one-block mode
+    (the losses it prints and the parameters equal a clean one-block run)."""
+    from hdgnn.model import graph2graph
+    monkeypatch.setenv("HDG_FUSED_SPLIT", "1")
+    monkeypatch.chdir(tmp_path)
+    cb = synth_commits(2 * B, NE, NC, 9)
+    tr, te = cb.slice(0, B), cb.slice(B, 2 * B)
+
+    class Args:
+        checkpoint_dir, Repo = str(tmp_path / "ck"), "glide"
+
+    def run(fault, split):
+        if fault:
+            monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+        else:
+            monkeypatch.delenv("HDG_DEBUG_XCH_FAULT", raising=False)
+        m = graph2graph(None, 1, NE, NC, NE * (NE - 1), NC * (NC - 1), 2, 20, 20, B,
+                        Args.checkpoint_dir, 2, 1, 2, 2, "glide", compact=(tr, te, tr))
+        m.engine.set_split(split)
+        m.train(Args)
+        return m
+
+    with pytest.warns(RuntimeWarning, match="one-block"):
+        got = run(True, True)
+    want = run(False, False)
+    assert not got.engine.split
+    assert torch.equal(got.engine.params, want.engine.params)
+    assert got.loss_Hedge_mse == want.loss_Hedge_mse

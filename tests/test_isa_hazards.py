@@ -52,3 +52,24 @@ def test_scanner_flags_a_close_write(tmp_path):
                  "\tv_add_f32_dpp v9, v9, v9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n")
     bad = dpp_hazards.scan(str(s))
     assert [b[2].split()[0] for b in bad] == ["v_add_f32_dpp", "v_permlane16_swap_b32"]
+
+
+def test_scanner_follows_control_flow(tmp_path):
+    """A write at the end of a predecessor block (fall-through into a label, a loop back
+    edge, a conditional branch's target) reaches a cross-lane read at the top of the next
+    block; an s_nop at the block start covers every path."""
+    import dpp_hazards
+    s = tmp_path / "k.s"
+    s.write_text("g:\n\tv_add_f32_e32 v5, v1, v2\n.LBB0_1:\n"
+                 "\tv_add_f32_dpp v5, v5, v5 row_mirror row_mask:0xf bank_mask:0xf\n"
+                 "\ts_cbranch_scc1 .LBB0_3\n\tv_add_f32_e32 v9, v1, v2\n.LBB0_3:\n"
+                 "\tv_permlane16_swap_b32 v7, v9\n\ts_endpgm\n"
+                 "h:\n.LBB1_1:\n\ts_nop 1\n"
+                 "\tv_add_f32_dpp v3, v3, v3 row_mirror row_mask:0xf bank_mask:0xf\n"
+                 "\tv_add_f32_e32 v3, v4, v4\n\ts_cbranch_scc1 .LBB1_1\n\ts_endpgm\n"
+                 "k:\n.LBB2_1:\n"
+                 "\tv_add_f32_dpp v6, v6, v6 row_mirror row_mask:0xf bank_mask:0xf\n"
+                 "\tv_add_f32_e32 v6, v4, v4\n\ts_cbranch_scc1 .LBB2_1\n\ts_endpgm\n")
+    bad = dpp_hazards.scan(str(s))
+    got = sorted((b[0], b[1].split()[1].rstrip(",")) for b in bad)
+    assert got == [("g", "v5"), ("g", "v9"), ("k", "v6")], bad

@@ -97,3 +97,22 @@ def test_neighbour_lists_bit_exact(B, ne, nc, variant):
                 assert cnt[side, b, i] == n, (side, b, i)
                 np.testing.assert_array_equal(ids[side, b, i, :n], exp)
                 assert (ids[side, b, i, n:(n + 3) & ~3] == ne).all()
+
+
+@pytest.mark.parametrize("B,n", [(3, 7), (2, 33), (4, 200), (1, 1100)])
+def test_pack_classes_matches_host(B, n):
+    """hdg_pack_classes (the upload's device-side bit packing) == data.pack_bits."""
+    import ctypes
+    import torch
+    from hdgnn import _lib
+    from hdgnn.data import pack_bits
+    rng = np.random.default_rng(n)
+    grid = (rng.random((B, n, n)) < 0.3).astype(np.uint8)
+    g = torch.from_numpy(grid).cuda()
+    out = torch.full((B, n, (n + 31) // 32), -1, dtype=torch.int32, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.hdg_pack_classes(ctypes.c_void_p(g.data_ptr()), B, n,
+                                    ctypes.c_void_p(out.data_ptr()),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), pack_bits(grid))

@@ -21,15 +21,19 @@ eng = Engine(ne, nc, B)
 eng.set_params(layout.init_flat(0))
 for _ in range(3):
     eng.train_step(db)
-st = torch.zeros(2 * B * 32, dtype=torch.int64, device="cuda")   # one row per block (split: 2 per commit)
+# one row of 32 phase stamps per block (split: 2 per commit), then [2B][16 waves][8] wave stamps
+st = torch.zeros(2 * B * 32 + 2 * B * 16 * 8, dtype=torch.int64, device="cuda")
 for _ in range(3):
     _lib.check(eng.lib.hdg_debug_step_stamps(ctypes.byref(eng.shape), ctypes.byref(db.struct()),
                                             ctypes.c_void_p(eng.params.data_ptr()),
                                             ctypes.c_void_p(eng.workspace.data_ptr()),
                                             ctypes.c_void_p(st.data_ptr()), eng._stream()))
 torch.cuda.synchronize()
-s = st.view(2 * B, 32).cpu().numpy().astype(np.int64)
-s = s[s[:, 0] > 0]
+allst = st.cpu().numpy().astype(np.int64)
+nblk = 2 * B if allst[B * 32] > 0 or allst[(2 * B - 1) * 32] > 0 else B
+s = allst[:2 * B * 32].reshape(2 * B, 32)
+wst = allst[nblk * 32: nblk * 32 + nblk * 128].reshape(nblk, 16, 8)
+s = s[:nblk]
 n = int((s[0] > 0).sum())
 d = np.diff(s[:, :n], axis=1) * 10e-3   # us
 med = np.median(d, axis=0)
@@ -39,3 +43,14 @@ print("total (median block) %.1f us; block span max %.1f us" % (np.median(d.sum(
 t0 = s[:, 0] - s[:, 0].min()
 print("block start skew: median %.2f us, max %.2f us; first start -> last end %.1f us" % (
     np.median(t0) * 10e-3, t0.max() * 10e-3, (s[:, n - 1].max() - s[:, 0].min()) * 10e-3))
+
+# per-wave stamps: (slot, phase stamp it is measured from, label)
+WAVE = [(0, 1, "E1 done (from E1 start)"), (1, 8, "M7 loop done (from M7 start)"),
+        (3, 19, "scan start (from M13 start)"), (4, 19, "scans done (from M13 start)"),
+        (2, 21, "E2 done (from E2 start)")]
+for slot, ph, label in WAVE:
+    if wst[:, :, slot].max() == 0:
+        continue
+    rel = (wst[:, :, slot] - s[:, ph:ph + 1]) * 10e-3
+    print("%-32s per wave (median over blocks, us): %s" % (
+        label, " ".join("%.2f" % v for v in np.median(rel, axis=0))))

@@ -19,7 +19,11 @@ __global__ void k_rate(float* out, int iters, float s) {
       for (int i = 0; i < 8; ++i) {
         if constexpr (KIND == 0) a[i] = __builtin_elementwise_fma(a[i], m, c);   // v_pk_fma_f32
         else if constexpr (KIND == 1) b[i] = fmaf(b[i], s, 0.25f);               // v_fma_f32
-        else {                                                                    // pk_mul clamp
+        else if constexpr (KIND == 3) {                                          // v_fma_f64
+          double d = (double)b[i];
+          d = fma(d, (double)s, 0.25);
+          b[i] = (float)d;
+        } else {                                                                  // pk_mul clamp
           f2 r2;
           asm volatile("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r2) : "v"(a[i]), "v"(m));
           a[i] = r2;
@@ -40,13 +44,14 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 2000;
-  const char* names[3] = {"v_pk_fma_f32", "v_fma_f32", "v_pk_mul_f32 clamp"};
-  for (int kind = 0; kind < 3; ++kind) {
+  const char* names[4] = {"v_pk_fma_f32", "v_fma_f32", "v_pk_mul_f32 clamp", "f64 fma+cvt"};
+  for (int kind = 0; kind < 4; ++kind) {
     for (int thr : {256, 512, 1024}) {
       auto launch = [&]() {
         if (kind == 0) hipLaunchKernelGGL(k_rate<0>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
         else if (kind == 1) hipLaunchKernelGGL(k_rate<1>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
-        else hipLaunchKernelGGL(k_rate<2>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else if (kind == 2) hipLaunchKernelGGL(k_rate<2>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else hipLaunchKernelGGL(k_rate<3>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
       };
       launch();
       hipDeviceSynchronize();
