@@ -45,7 +45,7 @@ print("block start skew: median %.2f us, max %.2f us; first start -> last end %.
     np.median(t0) * 10e-3, t0.max() * 10e-3, (s[:, n - 1].max() - s[:, 0].min()) * 10e-3))
 
 # per-wave stamps: (slot, phase stamp it is measured from, label)
-WAVE = [(0, 1, "E1 done (from E1 start)"), (1, 8, "M7 loop done (from M7 start)"),
+WAVE = [(5, 0, "stage staged (from kernel start)"), (0, 1, "E1 done (from E1 start)"), (1, 8, "M7 loop done (from M7 start)"),
         (3, 19, "scan start (from M13 start)"), (4, 19, "scans done (from M13 start)"),
         (2, 21, "E2 done (from E2 start)")]
 for slot, ph, label in WAVE:
