@@ -29,6 +29,17 @@ FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA pea
 HBM_PEAK_GBS = 8000.0
 
 
+def _prof(name):
+    """The newest round's copy of a committed profile file (profiles/rNN/<name>)."""
+    pd = os.path.join(ROOT, "profiles")
+    rounds = sorted(d for d in os.listdir(pd) if d.startswith("r") and d[1:].isdigit()) \
+        if os.path.isdir(pd) else []
+    for d in reversed(rounds):
+        if os.path.exists(os.path.join(pd, d, name)):
+            return os.path.join(pd, d, name)
+    return os.path.join(pd, "r02", name)
+
+
 def flops_per_commit(ne, nc, variant=2):
     """Algorithmic training FLOPs per commit, SURVEY 8(d) / BASELINE.md:
     3 * F_fwd(model_2), F_fwd = 1008 Pe + 880 Ne + 2200 Pc (the dense TF graph's pair
@@ -160,6 +171,12 @@ def main():
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
+    ap.add_argument("--edensity", type=float, default=0.05,
+                    help="synthetic entity-adjacency density (data-dependence runs)")
+    ap.add_argument("--hdensity", type=float, default=0.10,
+                    help="synthetic hunk-label density (data-dependence runs)")
+    ap.add_argument("--xkind", default="int10", choices=("int10", "real"),
+                    help="node attributes: integers 0..9, or Ne distinct signed reals")
     ap.add_argument("--e2e", type=int, default=0, metavar="EPOCHS",
                     help="also time graph2graph.train (the main.py --Type train loop) for "
                          "EPOCHS epochs of one --batch-commit step each (0: skip)")
@@ -183,7 +200,9 @@ def main():
     from hdgnn import _lib
 
     B, ne, nc, v = args.batch, args.ne, args.nc, args.variant
-    cb = synth_commits(B, ne, nc, seed_for(1, rank))
+    knobs = {"edensity": args.edensity, "hdensity": args.hdensity, "xkind": args.xkind}
+    default_data = knobs == {"edensity": 0.05, "hdensity": 0.10, "xkind": "int10"}
+    cb = synth_commits(B, ne, nc, seed_for(1, rank), **knobs)
     eng = Engine(ne, nc, B, variant=v, device=dev, batch_global=B * world, path=args.path,
                  process_group=torch.distributed.group.WORLD if launched else None)
     eng.set_params(layout.init_flat(0, v))
@@ -238,6 +257,7 @@ def main():
     acc = dict.fromkeys(names, 0.0)
     nev = max(10, min(args.steps, 50))
     import ctypes
+    tails = []                  # data parallel: the all-reduce + Adam tail after fwd_bwd
     for _ in range(nev):
         bstruct = db.struct()
         _lib.check(eng.lib.hdg_fwd_bwd_events(ctypes.byref(eng.shape), ctypes.byref(bstruct),
@@ -248,10 +268,16 @@ def main():
                                               eng._stream(), ev.ev))
         for i, n in enumerate(names):
             acc[n] += ev.elapsed_ms(i, i + 1)
-        eng.allreduce()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if not eng.xgmi:         # xGMI: adam() exchanges + updates in one kernel
+            eng.allreduce()
         eng.adam()
+        e1.record()
+        tails.append((e0, e1))
     torch.cuda.synchronize(dev)
     kern_ms = {n: acc[n] / nev for n in names}
+    tail_ms = sum(a.elapsed_time(b) for a, b in tails) / nev
 
     if rank != 0:
         torch.distributed.destroy_process_group()
@@ -261,7 +287,7 @@ def main():
     dense_tflops = dense_launch / (kern_ms[dom] * 1e-3) / 1e12
     # executed FP32 FLOPs of one launch (rocprofv3 PMC, calibrated: tools/flops_summary.py)
     exec_flops, flops_src = None, None
-    fj = os.path.join(ROOT, "profiles", "r02", "flops_pmc.json")
+    fj = _prof("flops_pmc.json")
     if fused and os.path.exists(fj):
         with open(fj) as f:
             pj = json.load(f)
@@ -269,7 +295,7 @@ def main():
             ks = [k for k in pj["kernels"] if k.startswith(dom)]
             if ks:
                 exec_flops = pj["kernels"][ks[0]]["executed_flops_per_launch"]
-                flops_src = ("profiles/r02/flops_pmc.json: 64 x SQ_INSTS_VALU_FLOPS_FP32 + 512 x "
+                flops_src = (os.path.relpath(fj, ROOT) + ": 64 x SQ_INSTS_VALU_FLOPS_FP32 + 512 x "
                              "SQ_INSTS_VALU_MFMA_MOPS_F32 per launch, counters calibrated "
                              "on known instruction streams (tools/probe/flops_cal.hip)")
     achieved = exec_flops / (kern_ms[dom] * 1e-3) / 1e12 if exec_flops else None
@@ -278,21 +304,23 @@ def main():
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if (tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne
-                and tj.get("nc") == nc and fused):
+                and tj.get("nc") == nc and fused and default_data):
             traffic = tj.get("bytes_per_launch")
     executed = None              # executed-instruction view (SQ counters, tools/valu_issue.py)
-    vj = os.path.join(ROOT, "profiles", "r02", "valu_issue.json")
-    if fused and (ne, nc, B) == (200, 74, 100) and os.path.exists(vj):
+    vj = _prof("valu_issue.json")
+    if fused and (ne, nc, B) == (200, 74, 100) and default_data and os.path.exists(vj):
         with open(vj) as f:
             ev = json.load(f)
         executed = {"valu_wave_insts_per_launch": ev.get("sq_insts_valu_per_launch"),
                     "issue_frac_chip": round(ev.get("issue_frac_chip", 0.0), 4),
                     "issue_frac_busy_cus": round(ev.get("issue_frac_busy_cus", 0.0), 4),
-                    "source": "profiles/r02/valu_issue.json (rocprofv3 SQ_INSTS_VALU over the "
+                    "source": os.path.relpath(vj, ROOT) + " (rocprofv3 SQ_INSTS_VALU over the "
                               "kernel's rocprof duration; 4 cycles per wave64 VALU op per SIMD)"}
-    # bound "mfma" = the FP32 compute roof: VALU and MFMA share the 157.3 TFLOP/s peak on
-    # gfx950 (MI355X_MICROARCH.md), and the kernel's FP32 work runs on both
-    roofline = {"bound": "mfma",
+    # bound: VALU issue.  The kernel's work is FP32 on the vector ALUs (2/3 of its executed
+    # FLOPs) and MFMA; what binds it is instruction issue and latency, not the FP32 FLOP
+    # roof, so achieved/peak is the executed-FLOP fraction of the 157.3 TFLOP/s FP32 peak
+    # and executed.issue_frac_* is the issue-slot fraction next to it
+    roofline = {"bound": "valu-issue" if fused else "mfma",
                 "achieved": round(achieved, 3) if achieved else None,
                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4) if achieved else None,
@@ -326,7 +354,8 @@ def main():
                           "rccl": "rccl all_reduce of the flat gradient per step"}.get(
                               eng.allreduce_kind) if launched else None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)",
+            "data": "synthetic glide-shaped commits (SURVEY 8(d) generator, resident in HBM)" + (
+                "" if default_data else "; data knobs %s" % json.dumps(knobs)),
             "config": {"workload": "model_%d (%s) train step: fwd+bwd+TF-Adam, %s" % (
                            v, {1: "HD-GNN/ES", 2: "HD-GNN/S", 3: "HD-GNN/E", 4: "HD-GNN"}[v],
                            "glide step=2" if (ne, nc) == (200, 74) else "Ne=%d Nc=%d" % (ne, nc)),
@@ -336,8 +365,13 @@ def main():
                        "launch": "eager" if args.no_graph else
                                  "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": "dp%d" % world},
+                       "parallelism": "dp%d" % world,
+                       **({} if default_data else {"data_knobs": knobs})},
             "roofline": roofline, "cpu_baseline": cpu,
+            "dp": {"allreduce": eng.allreduce_kind, "selftest": eng.allreduce_selftest,
+                   "tail_ms_per_step": round(tail_ms, 5),
+                   "tail": "k_grad_reduce excluded; xgmi: hdg_adam_dp (exchange + Adam, the "
+                           "k_dp_tail work); rccl: all_reduce + hdg_adam_tf"} if launched else None,
             "upload_prepare_ms": round(upload_ms, 3),
             "pcie_inclusive_commits_per_s": round(world * B / ((ms_per_step + upload_ms) * 1e-3), 1),
             "kernels_ms": {k: round(v, 5) for k, v in kern_ms.items()}}

@@ -29,6 +29,8 @@ class Engine:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("Engine needs a HIP device (got %s)" % self.device)
+        if self.device.index is None:          # "cuda" -> the current device, explicitly,
+            self.device = torch.device("cuda", torch.cuda.current_device())  # as tensors report
         self.ne, self.nc, self.batch, self.variant = ne, nc, batch, variant
         self.batch_global = batch_global or batch
         self.lr = lr
@@ -70,7 +72,7 @@ class Engine:
                                        None)
         self._out_none = _lib.Outputs(None, None, None, st, None)   # status only
         # data parallelism: which all-reduce joins the ranks' gradients
-        self.xgmi, self.allreduce_kind = None, None
+        self.xgmi, self.allreduce_kind, self.allreduce_selftest = None, None, None
         if self._distributed():
             mode = allreduce or os.environ.get("HDG_DP_ALLREDUCE", "auto")
             if mode not in ("auto", "xgmi", "rccl"):
@@ -79,6 +81,9 @@ class Engine:
                 from .xgmi import XgmiGroup
                 self.xgmi = XgmiGroup.create(self.lib, self.pg or torch.distributed.group.WORLD,
                                              dev, required=mode == "xgmi")
+                self.allreduce_selftest = XgmiGroup.verdict
+            else:
+                self.allreduce_selftest = "xGMI not tried (HDG_DP_ALLREDUCE=rccl)"
             self.allreduce_kind = "xgmi" if self.xgmi else "rccl"
         # hdg_fwd_bwd's own (local) gradient: the xGMI tail reads it while writing the
         # world sum into self.grad, so the two must not overlap

@@ -14,6 +14,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: larger CPU cases")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    path = os.environ.get("HDG_PARITY_REPORT")
+    if not path:
+        return
+    import json
+    from tests import _errlog
+    if _errlog.RECORDS:
+        with open(path, "w") as f:
+            json.dump(_errlog.RECORDS, f, indent=0)
+
+
 def gpu_available():
     try:
         import torch

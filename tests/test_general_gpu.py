@@ -4,7 +4,8 @@ Variants: 1 model_1 HD-GNN/ES (hunk stage on B_1), 2 model_2 HD-GNN
 3 model_3 HD-GNN/E (entity-edge stage computed, unused), 4 model_4 HD-GNN (entity-edge
 probabilities replace E_edge in B_2).  Same tolerances as tests/test_gpu_parity.py:
 logits 1e-4 |ref| + 1e-5 max(1, max|ref|); probs = softmax(logits) to 1e-6; CE rel 1e-5;
-gradients rtol 1e-3 + 1e-3 max|ref| per variable; weights after TF-Adam atol 2e-6.
+gradients rtol 1e-3 + 1e-4 max|ref| per variable (achieved <= 2.5e-5 max|ref|, at the
+4096-node shape; <= 3.5e-6 at glide); weights after TF-Adam atol 2e-6.
 """
 import numpy as np
 import pytest
@@ -15,6 +16,7 @@ from hdgnn.data import CommitBatch
 from hdgnn.synth import synth_commits
 from oracle import layout as olayout
 from oracle import model_ref
+from tests import _errlog
 
 pytestmark = pytest.mark.gpu
 
@@ -52,6 +54,7 @@ def _check_outputs(logits, probs, out):
     scale = np.maximum(1.0, np.abs(ref).reshape(ref.shape[0], -1).max(1))[:, None, None]
     tol = 1e-4 * np.abs(ref) + 1e-5 * scale
     err = np.abs(logits - ref)
+    _errlog.record("logits", (err / scale).max(), (err / tol).max())
     assert np.all(err <= tol), "logits: max err %.3g" % err.max()
     sm = np.exp(logits - logits.max(1, keepdims=True))
     sm /= sm.sum(1, keepdims=True)
@@ -64,8 +67,9 @@ def _grad_close(g_eng, g_ref, v):
         n = int(np.prod(shape))
         a, r = g_eng[o:o + n], g_ref[o:o + n]
         scale = max(np.abs(r).max(), 1e-12)
-        tol = 1e-3 * np.abs(r) + 1e-3 * scale + 1e-9
+        tol = 1e-3 * np.abs(r) + 1e-4 * scale + 1e-9
         err = np.abs(a - r)
+        _errlog.record("grad:" + name, err.max() / scale, (err / tol).max())
         if not np.all(err <= tol):
             bad.append("%s: max err %.3g, scale %.3g, %d/%d bad" % (
                 name, np.nanmax(err) if np.isfinite(err).any() else np.nan, scale,

@@ -5,7 +5,9 @@ Tolerances (fp32 engine vs float64 oracle; SURVEY 8(d) made scale-aware):
            logits reach |z| ~ 3e3 at glide sizes, where a fixed 1e-5 is below fp32 resolution
   probs    == softmax(engine logits) to 1e-6, and vs oracle |d| <= 0.5 * logit tolerance
   CE, loss_map, loss_para, train_loss: rel 1e-5
-  gradients rtol 1e-3, atol 1e-3 * max|ref| of the variable
+  gradients rtol 1e-3, atol 2e-5 * max|ref| of the variable (SURVEY 8(d) says atol 1e-6;
+           the scale-relative form because the variables' gradients span 1e-4 .. 1e1.
+           Achieved: <= 3.0e-6 * max|ref| over every case here)
   weights after TF-Adam steps: atol 2e-6 (lr 3e-4 per step)
 """
 import numpy as np
@@ -16,6 +18,7 @@ from hdgnn import layout
 from hdgnn.data import CommitBatch
 from hdgnn.synth import synth_commits
 from oracle import model_ref
+from tests import _errlog
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +62,8 @@ def _check_outputs(logits, probs, out):
     ref_l = out["logits"].transpose(0, 2, 1)            # (B, 2, Pc) like TF
     tol = _logit_tol(ref_l)
     err = np.abs(logits - ref_l)
+    scale = np.maximum(1.0, np.abs(ref_l).reshape(ref_l.shape[0], -1).max(1))[:, None, None]
+    _errlog.record("logits", (err / scale).max(), (err / tol).max())
     assert np.all(err <= tol), "logits: max err %.3g (tol %.3g)" % (err.max(), tol[err > tol].min())
     sm = np.exp(logits - logits.max(1, keepdims=True))
     sm /= sm.sum(1, keepdims=True)
@@ -68,7 +73,7 @@ def _check_outputs(logits, probs, out):
     assert np.all(perr <= 0.5 * tol + 1e-6), "probs: max err %.3g" % perr.max()
 
 
-def _grad_close(g_eng, g_ref, rtol=1e-3, atol_rel=1e-3):
+def _grad_close(g_eng, g_ref, rtol=1e-3, atol_rel=2e-5):
     bad = []
     for name, (o, shape) in layout.offsets(2).items():
         n = int(np.prod(shape))
@@ -76,6 +81,7 @@ def _grad_close(g_eng, g_ref, rtol=1e-3, atol_rel=1e-3):
         scale = max(np.abs(r).max(), 1e-12)
         tol = rtol * np.abs(r) + atol_rel * scale + 1e-9
         err = np.abs(a - r)
+        _errlog.record("grad:" + name, err.max() / scale, (err / tol).max())
         if not np.all(err <= tol):       # NaN fails too
             bad.append("%s: max err %.3g, scale %.3g, %d/%d bad" % (
                 name, np.nanmax(err) if np.isfinite(err).any() else np.nan, scale,

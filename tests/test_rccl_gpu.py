@@ -75,3 +75,9 @@ def test_bench_under_torchrun_uses_rccl():
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["allreduce"] and d["value"] > 0 and d["n_gpus"] == 1
+    # the line explains the data-parallel path: which all-reduce, the xGMI self-test
+    # verdict (world 1: the mailbox exchange with itself), the tail time per step
+    dp = d["dp"]
+    assert dp["allreduce"] in ("xgmi", "rccl") and dp["selftest"]
+    assert dp["allreduce"] != "xgmi" or dp["selftest"].startswith("passed")
+    assert dp["tail_ms_per_step"] > 0

@@ -10,7 +10,7 @@ step() {   # step <name> <timeout> <cmd...>
   grep -v amdgpu.ids "gpurun_out/$name.log" | tail -${TAILN:-4}
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+HDG_PARITY_REPORT=gpurun_out/parity_report.json step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python __graft_entry__.py smoke
 step bench 600 python bench.py --e2e 50
 step phases 200 python tools/mid_phases.py
