@@ -30,6 +30,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "hdgnn.h"
 #include "hdgnn_internal.h"
 
@@ -1348,8 +1350,11 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
   const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f};
   f2 S0 = {0.f, 0.f}, S1 = S0, S2 = S0, S3 = S0;
-  for (int base = n0 + EG_N * wv; base < n1; base += EG_N * (NT_MID / 64)) {   // wave-uniform
-    const int i = base + sub;
+  // rounds of 96 nodes; wave w takes nodes w + 16 s (s < 6) of a round, so the last,
+  // partial round's nodes land on as many waves -- and SIMDs -- as there are nodes
+  constexpr int NWV = NT_MID / 64;
+  for (int base = n0; base + wv < n1; base += EG_N * NWV) {   // wave-uniform
+    const int i = base + wv + NWV * sub;
     const bool live = sub < EG_N && i < n1;
     const int ic = live ? i : 0;
     const float xi = xs[ic];
@@ -1554,17 +1559,21 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const StepLayout L = step_layout(Ne, Nc, SMAXC);
   const PrepLayout PL = prep_layout(Ne, Nc);
-  // split mode: commit b runs on blocks 2b + h, h = 0, 1; block h owns the hunk rows
-  // p = 2r + h and the entity nodes of its half for E2
+  // split mode: commit b runs on two blocks h = 0, 1; block h owns the hunk rows p = 2r + h
+  // and the entity nodes of its half for E2.  The pair's block ids are 8 apart (blocks are
+  // dealt round-robin over the 8 XCDs, so b and b + 8 share one: the pair's exchanges and
+  // its shared input reads stay in one XCD's L2 -- speed only, the protocol does not
+  // assume it): ids 16q + 8h + r (r < 8) run commit 8q + r; the grid is padded to whole
+  // groups of 16 and the padding commits (b >= B) exit at once.
   int b, h;
   if constexpr (SPLIT) {
-    b = blockIdx.x >> 1;
-    h = blockIdx.x & 1;
+    b = ((blockIdx.x >> 1) & ~7) | (blockIdx.x & 7);
+    h = (blockIdx.x >> 3) & 1;
   } else {
     b = blockIdx.x;
     h = 0;
   }
-  if (b >= B) return;                                // (uniform; the grid is exact)
+  if (b >= B) return;                                // (uniform: split-mode padding)
   const int rmul = SPLIT ? 2 : 1, radd = h;          // own hunk rows p = rmul r + radd
   const int prow = SPLIT ? 2 * b + h : b;            // this block's partial-gradient row
   bool xlate = false;
@@ -2641,8 +2650,10 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   if (t <= Ne) offc[t] = e2off;
   WAVE_STAMP(3);
-  for (int k = wv; k < HS; k += NT_MID / 64) {        // wave-uniform; both tables of unit k
-    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;      // from one gather of rho
+  // TB: 1 = the rho table, 2 = the x rho table, 3 = both from one gather of rho
+  auto unit_scan = [&](const int k, auto tbc) {
+    constexpr int TB = decltype(tbc)::value;
+    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
     float* T0 = Tr + k * TL;
     float* T1 = Tx + k * TL;
     float run0[4], run1[4];
@@ -2654,32 +2665,38 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       if (s < Ne) {
         const int m = suf ? Ne - 1 - s : s;
         v0 = rho[perm[m] * HS + k];
-        v1 = v0 * xsrt[m];
+        if constexpr (TB & 2) v1 = v0 * xsrt[m];
       }
       r0 += v0;
       r1 += v1;
       run0[q] = r0;
       run1[q] = r1;
     }
-    const float off0 = wave_incl_scan_dpp(r0) - r0;
-    const float off1 = wave_incl_scan_dpp(r1) - r1;
+    const float off0 = (TB & 1) ? wave_incl_scan_dpp(r0) - r0 : 0.f;
+    const float off1 = (TB & 2) ? wave_incl_scan_dpp(r1) - r1 : 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int s = 4 * lane + q;
       if (s < Ne) {
-        if (suf) {                                  // sums over sorted slots [m, Ne)
-          T0[Ne - 1 - s] = off0 + run0[q];
-          T1[Ne - 1 - s] = off1 + run1[q];
-        } else {                                    // sums over sorted slots [0, m)
-          T0[s + 1] = off0 + run0[q];
-          T1[s + 1] = off1 + run1[q];
-        }
+        const int o = suf ? Ne - 1 - s : s + 1;    // suffix: slots [m, Ne); prefix: [0, m)
+        if constexpr (TB & 1) T0[o] = off0 + run0[q];
+        if constexpr (TB & 2) T1[o] = off1 + run1[q];
       }
     }
     if (lane == 0) {
-      T0[suf ? Ne : 0] = 0.f;
-      T1[suf ? Ne : 0] = 0.f;
+      if constexpr (TB & 1) T0[suf ? Ne : 0] = 0.f;
+      if constexpr (TB & 2) T1[suf ? Ne : 0] = 0.f;
     }
+  };
+  // units 0..15: both tables on wave k; units 16.. (HS > 16): one table each on waves
+  // 4, 5, ...: the second unit no longer runs alone on waves 0-3 at the phase's tail
+  constexpr int NWV = NT_MID / 64;
+  static_assert(HS <= NWV + (NWV - 4) / 2, "scan map: extra units beyond waves 4..15");
+  if (wv < HS) unit_scan(wv, std::integral_constant<int, 3>{});
+  if (wv >= 4 && wv < 4 + 2 * (HS - NWV)) {
+    const int k = NWV + ((wv - 4) >> 1);
+    if ((wv - 4) & 1) unit_scan(k, std::integral_constant<int, 2>{});
+    else unit_scan(k, std::integral_constant<int, 1>{});
   }
   WAVE_STAMP(4);
   __syncthreads();
@@ -3349,6 +3366,10 @@ int split_blocks_per_cu(const hdg_shape* s) {
   return nb < by_lds ? nb : by_lds;
 }
 
+// split-mode grid: two blocks per commit, padded to whole groups of 16 (k_commit_step's
+// XCD-paired block map)
+int split_grid(int batch) { return (2 * batch + 15) & ~15; }
+
 bool use_split(const hdg_shape* s) {
   if (s->flags & HDG_FLAG_NO_SPLIT) return false;
   const char* e = getenv("HDG_FUSED_SPLIT");
@@ -3359,7 +3380,7 @@ bool use_split(const hdg_shape* s) {
     case 8: per_cu = split_blocks_per_cu<8>(s); break;
     default: per_cu = split_blocks_per_cu<10>(s); break;
   }
-  return 2 * s->batch <= cu_count() * per_cu;
+  return split_grid(s->batch) <= cu_count() * per_cu;
 }
 
 int part_rows(const hdg_shape* s, bool split) { return split ? 2 * s->batch : s->batch; }
@@ -3399,7 +3420,7 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
   const StepLayout L = step_layout(s->ne, s->nc, SMAXC);
   const size_t lds = (size_t)L.total * 4;
   if (hipError_t e = set_step_attr<SMAXC, TRAIN, STAMPS, SPLIT>(); e != hipSuccess) return e;
-  const int grid = SPLIT ? 2 * s->batch : s->batch;
+  const int grid = SPLIT ? split_grid(s->batch) : s->batch;
   hipLaunchKernelGGL((k_commit_step<SMAXC, TRAIN, STAMPS, SPLIT>), dim3(grid), dim3(NT_MID), lds,
                      st, bt->x, bt->abits, bt->ybits, (const uint32_t*)bt->prep, params,
                      ws + w.Esave, (uint16_t*)(ws + w.rowq), ws + w.gam, ws + w.part, o.probs,
