@@ -127,13 +127,16 @@ def test_adam_trajectory_50_steps(v, path):
         n = int(np.prod(shape))
         e, r = err[o:o + n], theta_f[o:o + n]
         _errlog.record("free_weights@50:" + name, e.max() / max(np.abs(r).max(), 1e-12),
-                       (e / tol[o:o + n]).max(), err_over_lr=float(e.max() / lr))
+                       e.max() / (2 * lr) if v == 4 else (e / tol[o:o + n]).max(),
+                       err_over_lr=float(e.max() / lr))
         if not np.all(e <= tol[o:o + n]):
             worst.append("%s: max err %.3g = %.3g lr (|w| %.3g)" % (
                 name, e.max(), e.max() / lr, np.abs(r).max()))
     moved = np.abs(theta_f - flat.astype(np.float64)).max()
-    _errlog.record("free_weights@50", err.max() / np.abs(theta_f).max(), (err / tol).max(),
-                   err_over_lr=float(err.max() / lr), max_displacement=float(moved))
+    _errlog.record("free_weights@50", err.max() / np.abs(theta_f).max(),
+                   err.max() / (2 * lr) if v == 4 else (err / tol).max(),
+                   err_over_lr=float(err.max() / lr), max_displacement=float(moved),
+                   tolerance="2 lr" if v == 4 else "1e-3 |w| + 1e-3 lr steps")
 
     assert moved > 1e-3                                   # the weights did train
     assert max(step_err) <= 1.0, "teacher-forced step error %.3g x (1e-3 lr + 2 ulp)" % max(step_err)
