@@ -205,7 +205,17 @@ int hdg_forward(const hdg_shape* shape, const hdg_batch* batch, const float* par
  * its own mailbox for the peers' words, sums the world's values in rank order (the same
  * bits on every rank: replicas stay bitwise equal) and applies TF Adam -- one kernel, no
  * collective launch.  A peer that does not arrive within wait_ticks fails the launch
- * loudly: HDG_STATUS_DP_TIMEOUT, NaN loss, no update.  All ranks must issue the same
+ * loudly, but only where the wait happened: each tail block waits for the peers' words of
+ * ITS OWN slots, and a block that times out sets HDG_STATUS_DP_TIMEOUT in this rank's
+ * status word, writes a NaN loss and skips the update of its slots.  The other blocks of
+ * the same rank (block 0's beta-power update included) and every peer that did receive
+ * the words still apply the step, so after a timeout the parameters are partly updated
+ * and the ranks disagree: DP_TIMEOUT is unrecoverable -- no retry; restore every rank
+ * from a checkpoint.  (The split-mode pair timeout, HDG_STATUS_XCH_TIMEOUT, is different:
+ * its step is skipped whole and a one-block retry is exact.)  The deadline counts from
+ * the moment each block starts waiting, so host-side skew between ranks (data loading,
+ * rank-0 file writes) counts against it: callers barrier the ranks before the first step
+ * and after rank-only host work (graph2graph.train does).  All ranks must issue the same
  * sequence of hdg_*_dp calls (per-block launch counters in the mailbox tag the words).
  * The mailbox calls are the one place the library allocates device memory (IPC needs an
  * allocation of its own); everything else stays caller-owned.

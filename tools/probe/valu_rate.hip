@@ -2,6 +2,7 @@
 // occupancy (one 1024-thread block per CU = 4 waves per SIMD) and at 1 / 2 waves per SIMD.
 // hipcc --offload-arch=gfx950 -O3 valu_rate.hip -o valu_rate
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #include <stdio.h>
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -23,6 +24,19 @@ __global__ void k_rate(float* out, int iters, float s) {
           double d = (double)b[i];
           d = fma(d, (double)s, 0.25);
           b[i] = (float)d;
+        } else if constexpr (KIND == 4) {                                        // v_pk_fma_f16
+          uint32_t u = __builtin_bit_cast(uint32_t, b[i]), r2;
+          asm volatile("v_pk_fma_f16 %0, %1, %2, %3" : "=v"(r2) : "v"(u), "v"(0x3c003c00u), "v"(u));
+          b[i] = __builtin_bit_cast(float, r2);
+        } else if constexpr (KIND == 5) {                                        // v_dot2_f32_bf16
+          const uint32_t u = __builtin_bit_cast(uint32_t, a[i].y);
+          float r2;
+          asm volatile("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(r2) : "v"(u), "v"(0x3f803f80u), "v"(b[i]));
+          b[i] = r2;
+        } else if constexpr (KIND == 6) {                                        // cvt f32 -> bf16 x2
+          uint32_t r2;
+          asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r2) : "v"(b[i]), "v"(a[i].x));
+          b[i] = __builtin_bit_cast(float, r2 ^ 0x00010001u);
         } else {                                                                  // pk_mul clamp
           f2 r2;
           asm volatile("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r2) : "v"(a[i]), "v"(m));
@@ -44,14 +58,18 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 2000;
-  const char* names[4] = {"v_pk_fma_f32", "v_fma_f32", "v_pk_mul_f32 clamp", "f64 fma+cvt"};
-  for (int kind = 0; kind < 4; ++kind) {
+  const char* names[7] = {"v_pk_fma_f32", "v_fma_f32", "v_pk_mul_f32 clamp", "f64 fma+cvt",
+                          "v_pk_fma_f16", "v_dot2_f32_bf16", "v_cvt_pk_bf16_f32"};
+  for (int kind = 0; kind < 7; ++kind) {
     for (int thr : {256, 512, 1024}) {
       auto launch = [&]() {
         if (kind == 0) hipLaunchKernelGGL(k_rate<0>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
         else if (kind == 1) hipLaunchKernelGGL(k_rate<1>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
         else if (kind == 2) hipLaunchKernelGGL(k_rate<2>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
-        else hipLaunchKernelGGL(k_rate<3>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else if (kind == 3) hipLaunchKernelGGL(k_rate<3>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else if (kind == 4) hipLaunchKernelGGL(k_rate<4>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else if (kind == 5) hipLaunchKernelGGL(k_rate<5>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
+        else hipLaunchKernelGGL(k_rate<6>, dim3(256), dim3(thr), 0, 0, out, iters, 0.999f);
       };
       launch();
       hipDeviceSynchronize();
