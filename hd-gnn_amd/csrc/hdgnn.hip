@@ -1620,7 +1620,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   do {                                                                                  \
     if constexpr (STAMPS) {                                                             \
       if ((threadIdx.x & 63) == 0)                                                      \
-        stamps[(size_t)(gridDim.x) * 32 + (prow * 16 + (threadIdx.x >> 6)) * 8 + (s)] = \
+        stamps[(size_t)(SPLIT ? 2 * B : B) * 32 + (prow * 16 + (threadIdx.x >> 6)) * 8 + (s)] = \
             __builtin_amdgcn_s_memrealtime();                                           \
     }                                                                                   \
   } while (0)

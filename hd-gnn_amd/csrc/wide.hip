@@ -585,7 +585,7 @@ __device__ __forceinline__ int set_bound(const SortTabs& T, bool inc, P pred) {
 // zero term).  One independent group of loads per trip instead of a bit walk whose trip
 // count is the set bits of every word.
 // part / nparts: this caller's share of the list's 4-id groups (contiguous, in order).
-template <class F>
+template <int LB = 4, class F>
 __device__ __forceinline__ void for_list(const uint32_t* prep, int side, int b, int i, int Ne,
                                          int Nc, F f, int part = 0, int nparts = 1) {
   const int B = gridDim.y, LS = list_stride(Ne);
@@ -595,12 +595,22 @@ __device__ __forceinline__ void for_list(const uint32_t* prep, int side, int b, 
   const uint2* ids = reinterpret_cast<const uint2*>(
       reinterpret_cast<const uint16_t*>(prep + L.ids) + r * LS);
   const int g1 = (ng * (part + 1)) / nparts;
-  for (int gq = (ng * part) / nparts; gq < g1; ++gq) {
-    const uint2 q = ids[gq];
-    f((int)(q.x & 0xffffu));
-    f((int)(q.x >> 16));
-    f((int)(q.y & 0xffffu));
-    f((int)(q.y >> 16));
+  // LB groups' loads issued together before any is used (clamped to the list, so always in
+  // bounds): one HBM round trip per LB groups instead of one per group -- the walk is
+  // latency-bound, the trip count being the longest list of the wave's lanes
+  for (int g0 = (ng * part) / nparts; g0 < g1; g0 += LB) {
+    uint2 q[LB];
+#pragma unroll
+    for (int u = 0; u < LB; ++u) q[u] = ids[g0 + u < g1 ? g0 + u : g0];
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      if (g0 + u < g1) {
+        f((int)(q[u].x & 0xffffu));
+        f((int)(q[u].x >> 16));
+        f((int)(q[u].y & 0xffffu));
+        f((int)(q[u].y >> 16));
+      }
+    }
   }
 }
 
@@ -716,13 +726,13 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
     rat = q[4].ca; rbt = q[4].cb; cat = qc[4].ca; cbt = qc[4].cb;
     f2 sr[2] = {(f2){0.f, 0.f}, (f2){0.f, 0.f}}, sc[2] = {sr[0], sr[1]};
     float srt = 0.f, sct = 0.f;
-    for_list(prep, 0, b, i, Ne, Nc, [&](int j) {   // xb[Ne] = NaN: clamps to 0
+    for_list<2>(prep, 0, b, i, Ne, Nc, [&](int j) {   // xb[Ne] = NaN: clamps to 0
       const float xj = xb[j];
       sr[0] += clamp_fma2(xj, ra[0], rb2[0]);
       sr[1] += clamp_fma2(xj, ra[1], rb2[1]);
       srt += clamp_fma1(xj, rat, rbt);
     });
-    for_list(prep, 1, b, i, Ne, Nc, [&](int j) {
+    for_list<2>(prep, 1, b, i, Ne, Nc, [&](int j) {
       const float xj = xb[j];
       sc[0] += clamp_fma2(xj, ca[0], cb[0]);
       sc[1] += clamp_fma2(xj, ca[1], cb[1]);

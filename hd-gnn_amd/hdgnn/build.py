@@ -14,14 +14,16 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 
-def build(verbose=False):
+def build(verbose=False, out=None, force=False):
     srcs = [os.path.join(CSRC, f) for f in ("hdgnn.hip", "wide.hip")]
-    out = os.path.join(CSRC, "libhdgnn.so")
+    out = out or os.path.join(CSRC, "libhdgnn.so")
     deps = srcs + [os.path.join(CSRC, "hdgnn_internal.h"), os.path.join(ROOT, "include", "hdgnn.h")]
-    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp"] + srcs
+    extra = os.environ.get("HDG_HIPCC_FLAGS", "").split()   # experiments (A/B builds)
+    cmd[1:1] = extra
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
