@@ -3555,9 +3555,13 @@ extern "C" {
 int hdg_version(void) { return HDG_ABI_VERSION; }
 const char* hdg_last_error(void) { return hdg::g_err; }
 int hdg_resolve_path(const hdg_shape* shape) { return resolve(shape); }
-int hdg_param_count(int32_t variant) { return hdg::param_offsets(variant).NP; }
-int hdg_grad_len(int32_t variant) {
+int hdg_param_count(int32_t variant) {
   const int np = hdg::param_offsets(variant).NP;
+  if (np < 0) fail(HDG_EINVAL, "variant must be 1..4 (model_1 .. model_4), got %d", (int)variant);
+  return np < 0 ? -1 : np;
+}
+int hdg_grad_len(int32_t variant) {
+  const int np = hdg_param_count(variant);
   return np < 0 ? -1 : np + HDG_TRAILER;
 }
 

@@ -131,6 +131,8 @@ int         hdg_version(void);
 const char* hdg_last_error(void);
 /* the path AUTO resolves to for this shape (HDG_PATH_FUSED / _GENERAL), or -1 */
 int         hdg_resolve_path(const hdg_shape* shape);
+/* flat parameter count of model_<variant> (SURVEY Appendix A order), or -1 (message in
+ * hdg_last_error) for a variant outside 1..4                                         */
 int         hdg_param_count(int32_t variant);
 /* length of the gradient buffer hdg_fwd_bwd fills: param_count + HDG_TRAILER (the
  * trailer slots above); all-reduce the whole buffer.                                */
