@@ -3753,6 +3753,38 @@ static_assert(sizeof(hipIpcMemHandle_t) == HDG_DP_HANDLE_BYTES, "IPC handle size
 
 size_t hdg_dp_mailbox_bytes(void) { return dpk::BYTES; }
 
+// CRC-32C (Castagnoli, reflected 0x82F63B78), slicing by 8: the checksum of the TF V2
+// checkpoint bundle's records (hdgnn.tfckpt; LevelDB / TF masked CRCs)
+uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc) {
+  static uint32_t tab[8][256];
+  static bool init = false;                     // idempotent: same table for every caller
+  if (!__atomic_load_n(&init, __ATOMIC_ACQUIRE)) {
+    uint32_t t[8][256];
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFFu];
+    memcpy(tab, t, sizeof t);
+    __atomic_store_n(&init, true, __ATOMIC_RELEASE);
+  }
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  uint32_t c = crc ^ 0xFFFFFFFFu;
+  for (; n >= 8; n -= 8, p += 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = tab[7][lo & 0xFFu] ^ tab[6][(lo >> 8) & 0xFFu] ^ tab[5][(lo >> 16) & 0xFFu] ^
+        tab[4][lo >> 24] ^ tab[3][hi & 0xFFu] ^ tab[2][(hi >> 8) & 0xFFu] ^
+        tab[1][(hi >> 16) & 0xFFu] ^ tab[0][hi >> 24];
+  }
+  for (; n; --n, ++p) c = tab[0][(c ^ *p) & 0xFFu] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle) {
   if (!mailbox || !handle) return fail(HDG_EINVAL, "NULL mailbox/handle pointer");
   *mailbox = nullptr;

@@ -67,7 +67,7 @@ EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count
            "hdg_debug_step_stamps", "hdg_prep_counts_layout", "hdg_dp_mailbox_bytes",
            "hdg_dp_mailbox_alloc", "hdg_dp_mailbox_open", "hdg_dp_mailbox_close",
            "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce",
-           "hdg_pack_classes"]
+           "hdg_pack_classes", "hdg_crc32c"]
 
 _lib = None
 
@@ -113,6 +113,8 @@ def load(path=None):
                                       P(Dp), vp]
     lib.hdg_adam_dp.argtypes = [P(Shape), P(State), vp, vp, f32, vp, vp, P(Dp), vp]
     lib.hdg_dp_allreduce.argtypes = [P(Dp), vp, vp, i32, vp, vp]
+    lib.hdg_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+    lib.hdg_crc32c.restype = ctypes.c_uint32
     for name in EXPORTS:
         getattr(lib, name)
     _lib = lib

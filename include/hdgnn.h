@@ -235,6 +235,9 @@ typedef struct hdg_dp {
 } hdg_dp;
 
 size_t hdg_dp_mailbox_bytes(void);
+/* Host utility: CRC-32C (Castagnoli) of n bytes, continuing from crc (0 to start) -- the
+ * record checksum of the TF V2 checkpoint bundles graph2graph.saver writes.          */
+uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc);
 /* allocate + zero this rank's mailbox on the current device; handle: 64 bytes out */
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle);
 /* map a peer's mailbox (its handle) into this process; close / free undo the calls */

@@ -166,3 +166,18 @@ def test_checkpoint_state_file(tmp_path):
         'all_model_checkpoint_paths: "./checkpoint40/glide/glide/model_2/2/g2g.model-5"\n')
     assert tfckpt.latest(str(tmp_path)) == "g2g.model-5"
     assert tfckpt.latest(str(tmp_path / "nope")) is None
+
+
+def test_native_crc32c_matches_table_loop():
+    """libhdgnn's slicing-by-8 CRC-32C (hdg_crc32c) = the reference table loop, at every
+    length mod 8 and with a running crc; the standard check value of "123456789"."""
+    import random
+    from hdgnn import _lib
+    lib = _lib.load()
+    rng = random.Random(7)
+    for n in (0, 1, 3, 7, 8, 9, 15, 16, 17, 255, 4096, 4099):
+        data = bytes(rng.getrandbits(8) for _ in range(n))
+        for c0 in (0, 0xDEADBEEF):
+            assert lib.hdg_crc32c(data, n, c0) == tfckpt.crc32c_py(data, c0)
+    assert lib.hdg_crc32c(b"123456789", 9, 0) == 0xE3069283
+    assert tfckpt.crc32c(b"123456789") == 0xE3069283
