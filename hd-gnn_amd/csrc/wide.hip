@@ -201,6 +201,47 @@ __device__ __forceinline__ void half_sums20(const float (&v)[20], const int lane
   if (cnt >= 1) store(lane >> 5, base, w5);
 }
 
+// Sums of the 20 values v[k] over each 16-lane DPP row (a quarter of the wave) by the same
+// transposed butterfly inside the row (row_ror:8, row_half_mirror, quad_perm ^2, ^1); a
+// lane ends with 0-2 of its quarter's totals: store(slot, k, total), slot 0 / 1, on one
+// lane per quarter and value (the same lane and slot for every call)
+template <class F>
+__device__ __forceinline__ void quarter_sums20(const float (&v)[20], const int lane, F store) {
+  float w1[10], w2[5], w3[3], w4[2];
+  bool up = lane & 8;                                     // 20 -> 10 | 10
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const float a = v[i], b = v[i + 10];
+    w1[i] = (up ? b : a) + dppf<0x128>(up ? a : b);
+  }
+  int base = up ? 10 : 0;
+  up = lane & 4;                                          // 10 -> 5 | 5
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float a = w1[i], b = w1[i + 5];
+    w2[i] = (up ? b : a) + dppf<0x141>(up ? a : b);
+  }
+  base += up ? 5 : 0;
+  up = lane & 2;                                          // 5 -> 3 | 2
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float a = w2[i], b = i + 3 < 5 ? w2[i + 3] : 0.f;
+    w3[i] = (up ? b : a) + dppf<0x4E>(up ? a : b);
+  }
+  base += up ? 3 : 0;
+  int cnt = up ? 2 : 3;
+  up = lane & 1;                                          // 3 -> 2 | 1  (2 -> 2 | 0)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float a = w3[i], b = i + 2 < 3 ? w3[i + 2] : 0.f;
+    w4[i] = (up ? b : a) + dppf<0xB1>(up ? a : b);
+  }
+  base += up ? 2 : 0;
+  cnt = up ? cnt - 2 : (cnt < 2 ? cnt : 2);
+  if (cnt >= 1) store(0, base, w4[0]);
+  if (cnt >= 2) store(1, base + 1, w4[1]);
+}
+
 __device__ __forceinline__ unsigned long long qfix(float v) {
   return (unsigned long long)__double2ll_rn((double)v * FIX);
 }
@@ -2096,7 +2137,113 @@ __device__ __forceinline__ void ee_clsb_rows(
   }
 }
 
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw_ee_clsb(
+// The same pair loop with two columns per lane (c and c + 16 of the tile): a wave's four
+// 16-lane quarters take four rows at once, the lane adds its two columns' s-vectors
+// before the row sums, and the row sums close over 16 lanes (quarter_sums20): one
+// transposed butterfly per two pairs instead of one 32-lane butterfly per pair.
+__device__ __forceinline__ void ee_clsb_rows_q(
+    const int lo, const int hi, const int c0, const float* os_, const uint32_t* abl,
+    const int Ne, const int t0, const int nrel, const int dn1, const float inv,
+    const bool aligned, const float* Eq, const float4* gl, const float4* gdl,
+    const float* __restrict__ D, float* rowp, f2 (&acc0)[H2], f2 (&acc1)[H2], f2 (&ag)[H2],
+    float& sdl, float (&zr)[2], int (&kst)[2]) {
+  const int lane = threadIdx.x & 63, qr = lane >> 4, cq = lane & 15;
+  const float bq = D[D_EEBQ];
+  const int trips = (hi - lo + 3) >> 2;
+  const int jn0 = t0 + cq, jn1 = t0 + cq + 16;
+  const bool live0 = jn0 < Ne, live1 = jn1 < Ne;
+  const float Ej0 = Eq[live0 ? jn0 : Ne - 1], Ej1 = Eq[live1 ? jn1 : Ne - 1];
+  int wi = -1;
+  uint32_t word0 = 0, word1 = 0;
+  for (int it = 0; it < trips; ++it) {
+    const int mr = lo + 4 * it + qr;             // the quarter's row
+    const bool inr = mr < hi;
+    const int m = inr ? mr : lo;                 // past the share: a staged row, d1 = 0
+    if ((m >> 5) != wi) {
+      wi = m >> 5;
+      word0 = abl[wi * TB + cq];
+      word1 = abl[wi * TB + cq + 16];
+    }
+    const float* orow = os_ + (m - c0) * H;
+    const float4* o4 = reinterpret_cast<const float4*>(orow);
+    float sv[H];
+    auto column = [&](const int jn, const bool live, const float Ej, const uint32_t word,
+                      const int cc, f2 (&acc)[H2], const bool first) {
+      const bool a1 = (word >> (m & 31)) & 1u;
+      const float af = a1 ? 1.f : 0.f;
+      const f2 a2 = {af, af};
+      const int r = m * (Ne - 1) + jn - (jn > m ? 1 : 0);
+      const bool valid = live && inr && m != jn && r < nrel;
+      float dp;
+      if (aligned) {                   // n = Ne: (i', j') = (i, j)   (block-uniform branch)
+        dp = Eq[m] + Ej;
+      } else {
+        int ip, jj;
+        divmod_sel(r < nrel ? r : 0, dn1, inv, ip, jj);
+        dp = Eq[ip] + Eq[jj + (jj >= ip ? 1 : 0)];
+      }
+      const float4* g4 = (a1 ? gdl : gl) + cc;   // gam_j + a d: the LDS table by address
+      f2 pre[H2], st[H2];
+#pragma unroll
+      for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + (gam_j + a d), as kw_ee_fwd
+        const float4 q = o4[v], g = g4[v * TB];
+        pre[2 * v] = (f2){q.x, q.y} + (f2){g.x, g.y};
+        pre[2 * v + 1] = (f2){q.z, q.w} + (f2){g.z, g.w};
+      }
+      f2 dz = {bq, 0.f}, dzb = {0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < H2; ++kk) {  // relu(kappa) = kappa [kappa > 0]
+        st[kk] = step2(pre[kk]);
+        if (kk & 1)
+          dzb = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dzb);
+        else
+          dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
+      }
+      dz += dzb;
+      const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
+      const float p1 = __builtin_amdgcn_rcpf(1.f + e);
+      const float d1 = valid ? (e * p1) * (p1 * dp) : 0.f;
+      const f2 d2 = {d1, d1};
+      sdl += d1;
+#pragma unroll
+      for (int kk = 0; kk < H2; ++kk) {
+        const f2 sd = st[kk] * d2;
+        acc[kk] += sd;
+        ag[kk] = fma2(a2, sd, ag[kk]);
+        if (first) {
+          sv[2 * kk] = sd.x;
+          sv[2 * kk + 1] = sd.y;
+        } else {
+          sv[2 * kk] += sd.x;
+          sv[2 * kk + 1] += sd.y;
+        }
+      }
+    };
+    column(jn0, live0, Ej0, word0, cq, acc0, true);
+    column(jn1, live1, Ej1, word1, cq + 16, acc1, false);
+    // the quarter's row sums over the tile's 32 columns (drho partial, without c), and the
+    // classifier's rho part of sum_j relu(kappa) dz1 = rho_i . (row sum), as ee_clsb_rows
+    quarter_sums20(sv, lane, [&](int slot, int k, float x) {
+      if (inr) rowp[(size_t)m * H + k] = x;
+      zr[slot] = fmaf(orow[k], x, zr[slot]);
+      kst[slot] = k;
+    });
+  }
+}
+
+// sum over the four 16-lane quarters of a wave (lanes l, l^16, l^32, l^48); every lane
+// receives the total of its column lane
+__device__ __forceinline__ float quarters_sum(float v) {
+  float x = v, y = v;
+  swap32(x, y);
+  v = x + y;
+  x = v;
+  y = v;
+  swap16(x, y);
+  return x + y;
+}
+
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw_ee_clsb(
     const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
     const int32_t* __restrict__ hidg, const int32_t* __restrict__ nleng,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
@@ -2108,12 +2255,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
   (void)o;
   extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][TB]
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
-  __shared__ float buf[NW * 2 * TB * HP];
+  __shared__ float buf[NW * TB * HP];
   __shared__ float res[TB * HP];
   __shared__ float red[NW * 21];
   __shared__ float tot[21];
   __shared__ float cl[H];
-  __shared__ float zred[NW * 2 * H];
+  __shared__ float zred[NW * 4 * H];
   __shared__ float4 gl4[(H / 4) * TB];            // the columns' gam rows, [v][column]
   __shared__ float4 gdl4[(H / 4) * TB];           // gam + d
   const int b = blockIdx.y, t0 = blockIdx.x * TB, te = gridDim.x;
@@ -2142,17 +2289,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
     gl4[e] = g;
     gdl4[e] = make_float4(g.x + d.x, g.y + d.y, g.z + d.z, g.w + d.w);
   }
-  const int col = lane & (TB - 1);
-  const int jn = t0 + col, jc = jn < Ne ? jn : Ne - 1;
-  const bool live = jn < Ne;
-  f2 acc[H2], ag[H2];
+  f2 acc0[H2], acc1[H2], ag[H2];        // columns c and c + 16 of the lane; a = 1 sums
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
-    acc[kk] = (f2){0.f, 0.f};
-    ag[kk] = acc[kk];
+    acc0[kk] = (f2){0.f, 0.f};
+    acc1[kk] = acc0[kk];
+    ag[kk] = acc0[kk];
   }
-  float sdl = 0.f, zr = 0.f;
-  int kst = -1;
+  float sdl = 0.f, zr[2] = {0.f, 0.f};
+  int kst[2] = {-1, -1};
   // rows holding relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
   float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // this tile's partial rows
@@ -2161,31 +2306,42 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
   const float inv = 1.f / (float)dn1;
   const bool aligned = n == Ne;
   __syncthreads();                                 // Eq, abl, cl, gl4, gdl4
-  const float Ej = Eq[jc];
   for (int c0 = 0; c0 < rows; c0 += CHM) {
     const int c1 = c0 + CHM < rows ? c0 + CHM : rows;
     __syncthreads();
     stage_rows(os_, rb, c0, c1);
     __syncthreads();
     const int lo = c0 + ((c1 - c0) * uni(wv)) / NW, hi = c0 + ((c1 - c0) * (uni(wv) + 1)) / NW;
-    ee_clsb_rows(lo, hi, c0, os_, abl + col, Ne, jn, live, nrel, dn1, inv, aligned, Eq, Ej,
-                 gl4 + col, gdl4 + col, D, rowp, acc, ag, sdl, zr, kst);
+    ee_clsb_rows_q(lo, hi, c0, os_, abl, Ne, t0, nrel, dn1, inv, aligned, Eq, gl4, gdl4, D,
+                   rowp, acc0, acc1, ag, sdl, zr, kst);
   }
-  if (lane < 2 * H) zred[wv * 2 * H + lane] = 0.f;
+  for (int e = lane; e < 4 * H; e += 64) zred[wv * 4 * H + e] = 0.f;
   __syncthreads();
-  if (kst >= 0) zred[(wv * 2 + (lane >> 5)) * H + kst] = zr;   // one storing lane per (half, unit)
-  // column sums over the waves and the two halves (fixed order) -> res[TB][HP]
 #pragma unroll
-  for (int kk = 0; kk < H2; ++kk) {
-    buf[(wv * 2 * TB + lane) * HP + 2 * kk] = acc[kk].x;
-    buf[(wv * 2 * TB + lane) * HP + 2 * kk + 1] = acc[kk].y;
+  for (int s = 0; s < 2; ++s)                      // one storing lane per (quarter, unit)
+    if (kst[s] >= 0) zred[(wv * 4 + (lane >> 4)) * H + kst[s]] = zr[s];
+  // column sums over the quarters (in registers), then the waves (fixed order) -> res
+  {
+    const int cq = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < H2; ++kk) {
+      const float x0 = quarters_sum(acc0[kk].x), y0 = quarters_sum(acc0[kk].y);
+      const float x1 = quarters_sum(acc1[kk].x), y1 = quarters_sum(acc1[kk].y);
+      if (lane < 16) {
+        buf[(wv * TB + cq) * HP + 2 * kk] = x0;
+        buf[(wv * TB + cq) * HP + 2 * kk + 1] = y0;
+      } else if (lane < 32) {
+        buf[(wv * TB + 16 + cq) * HP + 2 * kk] = x1;
+        buf[(wv * TB + 16 + cq) * HP + 2 * kk + 1] = y1;
+      }
+    }
   }
   __syncthreads();
   for (int e = t; e < TB * H; e += NT) {
     const int nn = e / H, k = e - nn * H;
     float sum = 0.f;
 #pragma unroll
-    for (int q = 0; q < 2 * NW; ++q) sum += buf[(q * TB + nn) * HP + k];   // row q*TB+nn: wave q/2, half q&1
+    for (int q = 0; q < NW; ++q) sum += buf[(q * TB + nn) * HP + k];   // wave q's column sums
     res[nn * HP + k] = sum;
   }
   __syncthreads();
@@ -2215,7 +2371,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
       zg = fmaf(glf[((t >> 2) * TB + nn) * 4 + (t & 3)], cs, zg);
     }
     float zw = 0.f;
-    for (int q = 0; q < 2 * NW; ++q) zw += zred[q * H + t];
+    for (int q = 0; q < 4 * NW; ++q) zw += zred[q * H + t];
     const float zk = (zw + zg) + D[D_EED + t] * tot[t];
     const float sg_ = sc * cl[t];                    // sum of g over the tile
     const float a1 = tot[t] * cl[t];
