@@ -959,6 +959,25 @@ __host__ __device__ inline size_t ee_fwd_lds(int Ne, int Nc) {
   return head + (Ne <= EE_TAB_LDS_MAX ? (size_t)2 * Ne * H * 4 : 0);
 }
 
+#ifdef HDG_EE_PROBE   // timing probe builds only (tools/probe/eefwd_probe.hip)
+__device__ unsigned long long* g_ee_stamps;
+#define EE_STAMP(k) const unsigned long long ee_ts##k = __builtin_amdgcn_s_memrealtime()
+#define EE_FLUSH()                                                                         \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0) {                                                         \
+      unsigned long long* w_ = g_ee_stamps +                                               \
+          ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NWP + (threadIdx.x >> 6)) * 8;  \
+      w_[0] = ee_ts0; w_[1] = ee_ts1; w_[2] = ee_ts2; w_[3] = ee_ts3; w_[4] = ee_ts4;      \
+      w_[5] = __builtin_amdgcn_s_memrealtime();                                            \
+      w_[6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));                                   \
+      w_[7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));                                  \
+    }                                                                                      \
+  } while (0)
+#else
+#define EE_STAMP(k) do {} while (0)
+#define EE_FLUSH() do {} while (0)
+#endif
+
 template <bool LDS>
 __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                  const int32_t* __restrict__ hidg,
@@ -975,9 +994,31 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   float* tsum = reinterpret_cast<float*>(bins + ((2 * Nc + 1) & ~1));         // [Ne][2]
   float* gl = tsum + ((2 * Ne + 3) & ~3);                                     // gam [Ne][H]
   float* gdl = gl + Ne * H;                                                   // gam + d
+  EE_STAMP(0);
   const int b = blockIdx.y, t0 = blockIdx.x * TF;
   const int t = threadIdx.x, lane = t & 63, wv = uni(t >> 6), half = lane >> 5;
   unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
+  const float* rb = rho + (size_t)b * Ne * H;
+  const float* gb = gmm + (size_t)b * Ne * H;
+  // the gam table (Ne H <= 4 NTP float4 for Ne <= EE_TAB_LDS_MAX) is fetched in one batch of
+  // float4 loads before the commit's length is known: one memory round trip for the stage
+  // instead of one per loop trip, and none waiting on nleng
+  constexpr int GQ = (EE_TAB_LDS_MAX * H / 4 + NTP - 1) / NTP;
+  const int nq = Ne * H / 4;                       // H % 4 == 0: whole float4 per row
+  float4 gv[LDS ? GQ : 1];
+  if constexpr (LDS) {
+#pragma unroll
+    for (int u = 0; u < GQ; ++u) {
+      const int q = t + u * NTP;
+      gv[u] = q < nq ? reinterpret_cast<const float4*>(gb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // the hunk ids the bins take after the loop (the lane's row i', the thread's first target
+  // column), fetched with the same batch
+  const int32_t* hb = hidg + (size_t)b * Ne;
+  const int ipl = t0 + (lane & 31);
+  const int hsv = hb[ipl < Ne ? ipl : Ne - 1];
+  const int htv = hb[(t >> 1) < Ne ? (t >> 1) : Ne - 1];
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   for (int c = t; c < 2 * Nc; c += NTP) bins[c] = 0ull;
@@ -985,17 +1026,21 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     for (int c = t; c < 2 * Nc; c += NTP) outp[c] = 0ull;
     return;
   }
-  const float* rb = rho + (size_t)b * Ne * H;
-  const float* gb = gmm + (size_t)b * Ne * H;
   for (int e = t; e < 2 * n; e += NTP) tsum[e] = 0.f;
   if constexpr (LDS) {
-    for (int e = t; e < Ne * H; e += NTP) {
-      const float g = gb[e];
-      gl[e] = g;
-      gdl[e] = g + D[D_EED + e % H];
+#pragma unroll
+    for (int u = 0; u < GQ; ++u) {
+      const int q = t + u * NTP;
+      if (q < nq) {
+        const float4 d = *reinterpret_cast<const float4*>(D + D_EED + (4 * q) % H);
+        reinterpret_cast<float4*>(gl)[q] = gv[u];
+        reinterpret_cast<float4*>(gdl)[q] =
+            make_float4(gv[u].x + d.x, gv[u].y + d.y, gv[u].z + d.z, gv[u].w + d.w);
+      }
     }
   }
   __syncthreads();
+  EE_STAMP(1);
   const int WE = (Ne + 31) >> 5;
   const int ip = t0 + (lane & 31);
   const bool live = ip < n;
@@ -1014,6 +1059,15 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   for (int kk = 0; kk < H2; ++kk) rh[kk] = ld2(rsrc + (ei < Ne ? ei : Ne - 1) * H + 2 * kk);
   int cur = ei;
   const float bq = D[D_EEBQ];
+  // the classifier's prescaled weight differences in VGPRs for the whole loop (as scalar
+  // operands they were refetched through the scalar cache every relation, and the wait for
+  // them joined the wait for the gam rows)
+  f2 cq[H2];
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    cq[kk] = ld2(D + D_EECQ + 2 * kk);
+    asm volatile("" : "+v"(cq[kk].x), "+v"(cq[kk].y));
+  }
   float s0 = 0.f, s1 = 0.f;
   // class-bit words: the lane's relations walk the a-bit rows in order, so the word index
   // ei * WE + (j >> 5) grows by at most one per relation; the next word is prefetched
@@ -1023,6 +1077,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   int widx = (ei < Ne ? ei : Ne - 1) * WE + ((ejj + (ejj >= ei ? 1 : 0)) >> 5);
   widx = widx < wlast ? widx : wlast;
   uint32_t wcur = ab[widx], wnxt = ab[widx + 1 < wlast ? widx + 1 : wlast];
+  EE_STAMP(2);
   for (int it = 0; it < trips; ++it) {
     const int jp = jlo + it;
     const bool valid = live && jp < jhi && jp != ip;
@@ -1049,8 +1104,8 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
           const float4 g = g4[v];
           const f2 ka = relu2(rh[2 * v] + (f2){g.x, g.y});
           const f2 kb = relu2(rh[2 * v + 1] + (f2){g.z, g.w});
-          dz = fma2(ka, ld2(D + D_EECQ + 4 * v), dz);
-          dzb = fma2(kb, ld2(D + D_EECQ + 4 * v + 2), dzb);
+          dz = fma2(ka, cq[2 * v], dz);
+          dzb = fma2(kb, cq[2 * v + 1], dzb);
         }
       } else {
         const float af = a1 ? 1.f : 0.f;
@@ -1061,8 +1116,8 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
           const float4 g = g4[v];
           const f2 ka = relu2(rh[2 * v] + fma2(a2, ld2(D + D_EED + 4 * v), (f2){g.x, g.y}));
           const f2 kb = relu2(rh[2 * v + 1] + fma2(a2, ld2(D + D_EED + 4 * v + 2), (f2){g.z, g.w}));
-          dz = fma2(ka, ld2(D + D_EECQ + 4 * v), dz);
-          dzb = fma2(kb, ld2(D + D_EECQ + 4 * v + 2), dzb);
+          dz = fma2(ka, cq[2 * v], dz);
+          dzb = fma2(kb, cq[2 * v + 1], dzb);
         }
       }
       dz += dzb;
@@ -1080,8 +1135,9 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     const float v = row_total16(x + y);
     if ((lane & 15) == 0 && jp < jhi) tsum[2 * jp + ((lane >> 4) & 1)] = v;
   }
+  EE_STAMP(3);
   if (live) {                          // source bins: the lane's row i'
-    const int hs = hidg[(size_t)b * Ne + ip];
+    const int hs = hsv;
     if (hs >= 0 && hs < Nc) {
       atomicAdd(&bins[2 * hs], qfix(s0));
       atomicAdd(&bins[2 * hs + 1], qfix(s1));
@@ -1089,13 +1145,15 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   }
   __syncthreads();
   for (int e = t; e < 2 * n; e += NTP) {   // target bins: column j' of the tile's rows
-    const int ht = hidg[(size_t)b * Ne + (e >> 1)];
+    const int ht = e == t ? htv : hb[e >> 1];
     if (ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (e & 1)], qfix(tsum[e]));
   }
   __syncthreads();
   // per-tile partial bins, summed in tile order by kw_cross_fwd / k_commit_step (no global
   // atomics: the L2s of the 8 XCDs are not coherent for device-scope atomics)
+  EE_STAMP(4);
   for (int c = t; c < 2 * Nc; c += NTP) outp[c] = bins[c];
+  EE_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------
