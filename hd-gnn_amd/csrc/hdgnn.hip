@@ -1480,7 +1480,6 @@ __device__ __forceinline__ xu4 xload(const xu4* p) {
                : "=v"(w) : "v"(p) : "memory");
   return w;
 }
-
 // The send first waits for this thread's earlier stores (vmcnt counts stores on gfx9):
 // rows parked write-through before a send are in memory once the partner sees the tags.
 __device__ __forceinline__ void pair_send(const float* v, const int n, xu4* __restrict__ out,

@@ -2685,20 +2685,15 @@ __global__ __launch_bounds__(NT) void kw_reduce_adam(
     float inv_pairs, float* __restrict__ stats) {
   __shared__ float rs[16][17];
   __shared__ unsigned long long rc[16];
-  __shared__ int fl[1];
   const int t = threadIdx.x, lane = t & 63;
   const int pc = np + HDG_TR_COUNT;
-  bool fault = false;
-  if (fr.fp) {   // the step kernel's fault slot: any block-pair exchange timed out
-    if (t == 0) fl[0] = 0;
-    __syncthreads();
-    bool bad = false;
+  // Every load of the block (the fault slots, the Adam operands, the rows) is issued before
+  // the first one is used, and the fault flag is OR-ed at the block's one barrier: the
+  // kernel is one memory round trip deep.  Sums keep their fixed row order.
+  bool bad = false;   // the step kernel's fault slot: any block-pair exchange timed out
+  if (fr.fp)
     for (int r = t; r < fr.frows; r += NT)
       bad |= fr.fp[(size_t)r * fr.fstride + fr.f_np + HDG_TR_FAULT] != 0.f;
-    if (bad) fl[0] = 1;
-    __syncthreads();
-    fault = fl[0] != 0;
-  }
   if ((int)blockIdx.x < nfb) {
     const int sl = t & 15, ph = t >> 4;
     const int p2 = blockIdx.x * 16 + sl;
@@ -2710,15 +2705,26 @@ __global__ __launch_bounds__(NT) void kw_reduce_adam(
     const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
     float a = 0.f;
     unsigned long long c = 0ull;
+    constexpr int RU = 16;                       // rows of a phase in flight at once
     if (ok)
-      for (int r = ph; r < fr.frows; r += 16) {
-        const float v = fr.fp[(size_t)r * fr.fstride + p2];
-        if (isc) c += (unsigned long long)v;
-        else a += v;
+      for (int r0 = ph; r0 < fr.frows; r0 += 16 * RU) {
+        float v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int r = r0 + 16 * u;
+          v[u] = r < fr.frows ? fr.fp[(size_t)r * fr.fstride + p2] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          if (r0 + 16 * u < fr.frows) {
+            if (isc) c += (unsigned long long)v[u];
+            else a += v[u];
+          }
+        }
       }
     rs[ph][sl] = a;
     if (isc) rc[ph] = c;
-    __syncthreads();
+    const bool fault = __syncthreads_or(bad);
     if (ph == 0 && ok && !(p > pc && p <= pc + 2)) {   // count parts: the count slot's thread
       float g = 0.f;
       unsigned long long cc = 0ull;
@@ -2733,26 +2739,40 @@ __global__ __launch_bounds__(NT) void kw_reduce_adam(
   }
   const int wv = t >> 6;
   const int p = seg_lo + ((int)blockIdx.x - nfb) * NW + wv;
-  if (p >= seg_hi || (p > pc && p <= pc + 2)) return;   // count parts: the count slot's wave
-  const bool isp = lane == 0 && p < np;
+  const bool live = p < seg_hi && !(p > pc && p <= pc + 2);   // count parts: the count slot's wave
+  const bool isp = live && lane == 0 && p < np;
   const float w = isp ? params[p] : 0.f, m0 = isp ? mm[p] : 0.f, v0 = isp ? vv[p] : 0.f;
   float a = 0.f;
   unsigned long long c = 0ull;
-  for (int q = 0; q < sg.count; ++q) {
-    const Seg& sgq = sg.s[q];
-    if (sgq.n > 0 && p >= sgq.p0 && p < sgq.p0 + sgq.n) {
-      const float* src = part + sgq.off + (long long)(p - sgq.p0) * sgq.rows;
-      if (p == pc)
-        for (int r = lane; r < sgq.rows; r += 64) c += (unsigned long long)src[r];
-      else
-        for (int r = lane; r < sgq.rows; r += 64) a += src[r];
-      break;
+  if (live)
+    for (int q = 0; q < sg.count; ++q) {
+      const Seg& sgq = sg.s[q];
+      if (sgq.n > 0 && p >= sgq.p0 && p < sgq.p0 + sgq.n) {
+        const float* src = part + sgq.off + (long long)(p - sgq.p0) * sgq.rows;
+        constexpr int RU = 8;
+        for (int r0 = lane; r0 < sgq.rows; r0 += 64 * RU) {
+          float v[RU];
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            const int r = r0 + 64 * u;
+            v[u] = r < sgq.rows ? src[r] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            if (r0 + 64 * u < sgq.rows) {
+              if (p == pc) c += (unsigned long long)v[u];
+              else a += v[u];
+            }
+          }
+        }
+        break;
+      }
     }
-  }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   const float g = wsum(a);
-  if (lane == 0)
+  const bool fault = __syncthreads_or(bad);
+  if (live && lane == 0)
     reduce_adam_slot(p, np, g, c, w, m0, v0, fault, grad, params, mm, vv, bpow, D, lr, inv_pairs,
                      stats);
 }

@@ -2,6 +2,7 @@
 // L2 writeback fence: data stored write-through (system-scope relaxed atomic stores ->
 // global_store sc0 sc1), s_waitcnt vmcnt(0) + barrier, flag store sc0 sc1; the reader
 // spins on an sc0 sc1 load, then reads the partner's words with sc0 sc1 loads (L2 miss).
+// mode 4: mode 3 at agent scope (sc1 stores / loads: the L2 of the XCD, not memory).
 // mode 0: agent release fence (buffer_wbl2) + agent acquire, for comparison.
 // xcd 0: partner on the same XCD (blk, blk+8); 1: different XCD (blk, blk+1).
 // hipcc --offload-arch=gfx950 -O3 xchg2.hip -o xchg2
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(1024) void k_pair(float* xbuf, unsigned* flags, flo
   __shared__ int bad;
   if (t == 0) { bad = 0; st[0] = __builtin_amdgcn_s_memrealtime(); }
   __syncthreads();
-  if (mode == 3) {
+  if (mode == 3 || mode == 4) {
     // mode 3: mode 2 with two (value, tag) pairs per 16-byte write-through store / load
     // (global_store_dwordx4 / global_load_dwordx4 sc0 sc1): half the round trips
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -50,14 +51,20 @@ __global__ __launch_bounds__(1024) void k_pair(float* xbuf, unsigned* flags, flo
         const float v0 = (float)(e * 100000 + h * 10000 + 2 * i) + lds[2 * i];
         const float v1 = (float)(e * 100000 + h * 10000 + 2 * i + 1) + lds[2 * i + 1];
         const u4 w = {__float_as_uint(v0), (unsigned)e, __float_as_uint(v1), (unsigned)e};
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(mine + i), "v"(w) : "memory");
+        if (mode == 3)
+          asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(mine + i), "v"(w) : "memory");
+        else
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(mine + i), "v"(w) : "memory");
       }
       int lb = 0;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       for (int i = t; i < nv; i += 1024) {
         u4 w;
         do {
-          asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(w) : "v"(theirs + i) : "memory");
+          if (mode == 3)
+            asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(w) : "v"(theirs + i) : "memory");
+          else
+            asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(w) : "v"(theirs + i) : "memory");
         } while ((w.y != (unsigned)e || w.w != (unsigned)e) &&
                  __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull);
         const float want0 = (float)(e * 100000 + (1 - h) * 10000 + 2 * i) + lds[2 * i];
@@ -158,7 +165,7 @@ int main() {
   unsigned long long* hs = (unsigned long long*)malloc((size_t)G * (NEX + 1) * 8);
   int* he = (int*)malloc(G * 4);
   const int wl[3] = {256, 1480, 4096};
-  for (int mode = 2; mode < 4; ++mode)
+  for (int mode = 3; mode < 5; ++mode)
     for (int xcd = 0; xcd < 2; ++xcd)
       for (int wi = 0; wi < 3; ++wi) {
         const int words = wl[wi];
