@@ -1480,11 +1480,14 @@ __device__ __forceinline__ xu4 xload(const xu4* p) {
                : "=v"(w) : "v"(p) : "memory");
   return w;
 }
-// The send first waits for this thread's earlier stores (vmcnt counts stores on gfx9):
-// rows parked write-through before a send are in memory once the partner sees the tags.
+// The send does not wait for this thread's earlier memory operations: the partner reads
+// nothing of this block's but the mailbox words themselves (value and tag in one 16-byte
+// store), and the receive's polls wait for every outstanding operation (vmcnt(0)), which
+// orders a thread's earlier stores before a fault path's poison of the same slots.  (A
+// vmcnt(0) here cost 0.3 us per launch, the waves stalling on stores before the send's
+// overlapped work.)
 __device__ __forceinline__ void pair_send(const float* v, const int n, xu4* __restrict__ out,
                                           const uint32_t tag, const int t) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int e = t; 2 * e < n; e += NT_MID)
     xstore(out + e, (xu4){__float_as_uint(v[2 * e]), tag, __float_as_uint(v[2 * e + 1]), tag});
 }
@@ -2725,8 +2728,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
     pb[E1_B1 + t] = s2;
   }
   // a pair exchange timed out: every late thread poisons the CE slot, sets the fault slot
-  // and the status word (identical values; the slots' earlier stores completed at the
-  // pair sends' vmcnt(0)).  No block-wide vote here: the tail sits at the VGPR ceiling.
+  // and the status word (identical values; thread 0's earlier CE store completed at its
+  // polls' vmcnt(0) in the M9 receive, before the barriers that precede this).  No
+  // block-wide vote here: the tail sits at the VGPR ceiling.
   // The step's probs stay as computed; the status word and the NaN CE void them.
   if (SPLIT && xlate) {
     pb[NP + HDG_TR_CE] = __builtin_nanf("");
