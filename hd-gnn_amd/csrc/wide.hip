@@ -205,22 +205,45 @@ __device__ __forceinline__ void half_sums20(const float (&v)[20], const int lane
 // transposed butterfly inside the row (row_ror:8, row_half_mirror, quad_perm ^2, ^1); a
 // lane ends with 0-2 of its quarter's totals: store(slot, k, total), slot 0 / 1, on one
 // lane per quarter and value (the same lane and slot for every call)
+// One level of a transposed butterfly on five pairs (a_i, b_i) without selects: lanes in
+// the DPP banks of LO get a_i + a_i(partner), lanes in HI b_i + b_i(partner), as two DPP
+// adds into one register whose bank masks split the lanes (a lane kept by the mask is
+// written by exactly one of the two).  CTRL: row_ror:8 (partner lane ^ 8; LO = banks 0, 1)
+// or row_half_mirror (partner 7 - lane within 8; LO = banks 0, 2).  Same sums, same bits
+// as keep + dpp(send) with two selects per pair; one s_nop for the block (its inputs'
+// VALU writes precede it, the block writes only its outputs).
+#define HDG_XLEVEL5(CTRL, LO, HI)                                                          \
+  asm volatile("s_nop 1\n\t"                                                             \
+               "v_add_f32_dpp %0, %5, %5 " CTRL " row_mask:0xf bank_mask:" LO "\n\t"        \
+               "v_add_f32_dpp %0, %10, %10 " CTRL " row_mask:0xf bank_mask:" HI "\n\t"      \
+               "v_add_f32_dpp %1, %6, %6 " CTRL " row_mask:0xf bank_mask:" LO "\n\t"        \
+               "v_add_f32_dpp %1, %11, %11 " CTRL " row_mask:0xf bank_mask:" HI "\n\t"      \
+               "v_add_f32_dpp %2, %7, %7 " CTRL " row_mask:0xf bank_mask:" LO "\n\t"        \
+               "v_add_f32_dpp %2, %12, %12 " CTRL " row_mask:0xf bank_mask:" HI "\n\t"      \
+               "v_add_f32_dpp %3, %8, %8 " CTRL " row_mask:0xf bank_mask:" LO "\n\t"        \
+               "v_add_f32_dpp %3, %13, %13 " CTRL " row_mask:0xf bank_mask:" HI "\n\t"      \
+               "v_add_f32_dpp %4, %9, %9 " CTRL " row_mask:0xf bank_mask:" LO "\n\t"        \
+               "v_add_f32_dpp %4, %14, %14 " CTRL " row_mask:0xf bank_mask:" HI               \
+               : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4])               \
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(b[0]), "v"(b[1]),  \
+                 "v"(b[2]), "v"(b[3]), "v"(b[4]))
+__device__ __forceinline__ void xlevel5_ror8(const float* a, const float* b, float* o) {
+  HDG_XLEVEL5("row_ror:8", "0x3", "0xc");
+}
+__device__ __forceinline__ void xlevel5_hmirror(const float* a, const float* b, float* o) {
+  HDG_XLEVEL5("row_half_mirror", "0x5", "0xa");
+}
+#undef HDG_XLEVEL5
+
 template <class F>
 __device__ __forceinline__ void quarter_sums20(const float (&v)[20], const int lane, F store) {
   float w1[10], w2[5], w3[3], w4[2];
   bool up = lane & 8;                                     // 20 -> 10 | 10
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const float a = v[i], b = v[i + 10];
-    w1[i] = (up ? b : a) + dppf<0x128>(up ? a : b);
-  }
+  xlevel5_ror8(v, v + 10, w1);                            // pairs (v[i], v[i + 10]), i < 5
+  xlevel5_ror8(v + 5, v + 15, w1 + 5);                    //   and i = 5..9
   int base = up ? 10 : 0;
   up = lane & 4;                                          // 10 -> 5 | 5
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const float a = w1[i], b = w1[i + 5];
-    w2[i] = (up ? b : a) + dppf<0x141>(up ? a : b);
-  }
+  xlevel5_hmirror(w1, w1 + 5, w2);
   base += up ? 5 : 0;
   up = lane & 2;                                          // 5 -> 3 | 2
 #pragma unroll
