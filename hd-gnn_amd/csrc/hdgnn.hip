@@ -99,6 +99,40 @@ __device__ __forceinline__ void row16_sum5(float* v) {
 #undef HDG_DPP_STEP4
 #undef HDG_DPP_STEP3
 #undef HDG_DPP_STEP
+#ifndef HDG_XROW
+#define HDG_XROW 1
+#endif
+// Row sums of 5 values over a 16-lane DPP row as a transposed butterfly: 12 DPP adds
+// instead of 20, no selects -- at the two bank-crossing levels (row_mirror: lanes 0-7 vs
+// 8-15; row_half_mirror: banks 0, 2 vs 1, 3) one register takes the a-values' sums in
+// one half of the lanes and the b-values' in the other through the DPP bank mask; the
+// last two levels reduce the remaining two values in full.  Afterwards (tj = lane & 15):
+//   tj 0-3: y0 = v0, y1 = v1;  4-7: y0 = v2, y1 = v1;  8-11: y0 = v3, y1 = v4;
+//   12-15: y0 = v2, y1 = v4   (every lane of a group holds the same bits).
+// Hazards: one s_nop 1 for the producers of v, then every DPP read >= 2 wait states after
+// the write of its operand (the instruction order and the two inner s_nops ensure it).
+__device__ __forceinline__ void row16_xsum5(const float* v, float& y0, float& y1) {
+  float x0, x1, x2;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %2, %7, %7 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %0, %5, %5 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_f32_dpp %0, %8, %8 row_mirror row_mask:0xf bank_mask:0xc\n\t"
+      "v_add_f32_dpp %1, %6, %6 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+      "v_add_f32_dpp %1, %9, %9 row_mirror row_mask:0xf bank_mask:0xc\n\t"
+      "v_add_f32_dpp %3, %0, %0 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+      "v_add_f32_dpp %3, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa\n\t"
+      "v_add_f32_dpp %4, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %4, %4, %4 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_add_f32_dpp %3, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %4, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(y0), "=&v"(y1)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]));
+}
+
 // N = 3 G + R (R < 3): G - 1 groups of 3 and one of 3 + R
 template <int N>
 __device__ __forceinline__ void row16_sums(float (&v)[N]) {
@@ -306,6 +340,9 @@ __device__ __forceinline__ void pair_tile(
   const int nown = (N - radd + rmul - 1) / rmul;   // rows i = rmul r + radd < N
   const int S = (nown + 15) >> 4;
   const p2 z2 = {0.f, 0.f};
+  // row16_xsum5's storing lanes and their units (KK = 5)
+  const bool xst = tj == 0 || tj == 4 || tj == 8;
+  const int xk0 = kof(tj == 0 ? 0 : (tj == 4 ? 2 : 3)), xk1 = kof(tj < 8 ? 1 : 4);
 
   p2 cacc2[SMAX][KP > 0 ? KP : 1];
   float cacct[SMAX];
@@ -413,10 +450,21 @@ __device__ __forceinline__ void pair_tile(
       rs[2 * p + 1] = racc2[p].y;
     }
     if constexpr (KT) rs[KK - 1] = racct;
-    if constexpr (!(ABL & 2)) row16_sums(rs);
-    if (tj == 0 && iv) {       // one predicated block: no per-value branch / address spill
+    if constexpr (KK == 5 && HDG_XROW && !(ABL & 2)) {
+      // transposed: lanes tj = 0, 4, 8 store two row values each (tj = 4's y1 is v1, the
+      // same bits tj = 0 stores at the same address)
+      float y0, y1;
+      row16_xsum5(rs, y0, y1);
+      if (xst && iv) {
+        Rout[i * LD + xk0] = y0;
+        Rout[i * LD + xk1] = y1;
+      }
+    } else {
+      if constexpr (!(ABL & 2)) row16_sums(rs);
+      if (tj == 0 && iv) {     // one predicated block: no per-value branch / address spill
 #pragma unroll
-      for (int k = 0; k < KK; ++k) Rout[i * LD + kof(k)] = rs[k];
+        for (int k = 0; k < KK; ++k) Rout[i * LD + kof(k)] = rs[k];
+      }
     }
   }
   float cacc[SMAX][KK], yacc[KK];
