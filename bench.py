@@ -177,7 +177,7 @@ def main():
                     help="synthetic hunk-label density (data-dependence runs)")
     ap.add_argument("--xkind", default="int10", choices=("int10", "real"),
                     help="node attributes: integers 0..9, or Ne distinct signed reals")
-    ap.add_argument("--e2e", type=int, default=0, metavar="EPOCHS",
+    ap.add_argument("--e2e", type=int, default=50, metavar="EPOCHS",
                     help="also time graph2graph.train (the main.py --Type train loop) for "
                          "EPOCHS epochs of one --batch-commit step each (0: skip)")
     args = ap.parse_args()
@@ -341,7 +341,10 @@ def main():
                 "executed": executed}
     e2e = None
     if world == 1 and args.e2e > 0:
-        e2e = e2e_train(B, ne, nc, v, args.e2e, dev)
+        try:                     # a side measurement: never costs the bench line
+            e2e = e2e_train(B, ne, nc, v, args.e2e, dev)
+        except Exception as ex:  # noqa: BLE001
+            e2e = {"error": "%s: %s" % (type(ex).__name__, ex)}
     cpu = None
     if world == 1 and not args.no_cpu and v == 2:
         threads = min(16, os.cpu_count() or 1)

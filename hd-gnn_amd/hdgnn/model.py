@@ -84,15 +84,43 @@ class Saver(object):
         self._model = model
         self.max_to_keep = max_to_keep
         self._last = []              # prefixes saved by this Saver, oldest first
+        self._pool = None            # one writer thread: background saves stay in order
+        self._pending = []
 
-    def save(self, sess, save_path, global_step=None):
-        prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+    def _host_state(self):
+        """Parameters, Adam moments and beta powers in one device->host copy."""
+        import torch
         eng = self._model.engine
+        n = eng.params.numel()
+        h = torch.cat([eng.params.detach(), eng.m, eng.v, eng.beta_pow]).cpu().numpy()
+        return h[:n].copy(), h[n:2 * n].copy(), h[2 * n:3 * n].copy(), h[3 * n:].copy()
+
+    def save(self, sess, save_path, global_step=None, background=False):
+        """background=True: the state is copied to the host now (the bundle holds exactly
+        this step's values), the bundle is written by the writer thread while the caller's
+        next steps run; flush() waits for it and re-raises its error."""
+        prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+        state = self._host_state()
+        if not background:
+            self.flush()
+            return self._write(prefix, state)
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hdg-saver")
+        self._pending = [f for f in self._pending if not f.done() or f.exception()]
+        self._pending.append(self._pool.submit(self._write, prefix, state))
+        return prefix
+
+    def flush(self):
+        pending, self._pending = self._pending, []
+        for f in pending:
+            f.result()
+
+    def _write(self, prefix, state):
+        params, m, v, bp = state
         d = os.path.dirname(prefix) or "."
         os.makedirs(d, exist_ok=True)
-        tfckpt.write(prefix, tfckpt.state_tensors(eng.get_params(), self._model.variant,
-                                                  eng.m.cpu().numpy(), eng.v.cpu().numpy(),
-                                                  eng.beta_pow.cpu().numpy()))
+        tfckpt.write(prefix, tfckpt.state_tensors(params, self._model.variant, m, v, bp))
         if prefix in self._last:
             self._last.remove(prefix)
         self._last.append(prefix)
@@ -105,6 +133,7 @@ class Saver(object):
 
     def restore(self, sess, save_path):
         import torch
+        self.flush()
         eng = self._model.engine
         flat, m, v, bp = tfckpt.engine_state(tfckpt.read(save_path), self._model.variant)
         eng.set_params(flat)
@@ -293,8 +322,9 @@ class graph2graph(object):
                     f.write(resultString)
                 print(resultString)
             counter += 1
-            self.save(args.checkpoint_dir, counter)
+            self.save(args.checkpoint_dir, counter, background=True)
             self._barrier()
+        self.saver.flush()          # every epoch's bundle on disk before train() returns
         end_time1 = time.time()
         if self.rank == 0:
             print('test time:' + str(end_time1 - start_time1))
@@ -303,21 +333,25 @@ class graph2graph(object):
     def _model_dir(self, checkpoint_dir):
         return os.path.join(checkpoint_dir, "%s/model_%d/%s" % (self.Repo, self.variant, self.Step))
 
-    def save(self, checkpoint_dir, step):
+    def save(self, checkpoint_dir, step, background=False):
         """saver.save(sess, <dir>/g2g.model, global_step=step) (model_2.py:427-437): a TF V2
         bundle g2g.model-<step>.index / .data-00000-of-00001 under the TF variable names
         (hdgnn.tfckpt), plus TF1 Adam's slots and beta powers so training can resume, and
-        the 'checkpoint' state file tf.train.get_checkpoint_state reads."""
+        the 'checkpoint' state file tf.train.get_checkpoint_state reads.  train() saves in
+        the background (Saver.save(background=True)): the state is read at the epoch's end,
+        the files are written while the next epoch runs, and train() flushes before it
+        returns."""
         if self.rank != 0:
             return
         self.saver.save(self.sess, os.path.join(self._model_dir(checkpoint_dir), "g2g.model"),
-                        global_step=step)
+                        global_step=step, background=background)
 
     def load(self, checkpoint_dir):
         """get_checkpoint_state + saver.restore (model_2.py:439-451).  Reads TF V2 bundles
         (this framework's or the reference's own; the latter carry no Adam slots, so the
         optimizer state is left as initialised) and this framework's older .npz files."""
         print(" [*] Reading checkpoint...")
+        self.saver.flush()
         d = self._model_dir(checkpoint_dir)
         name = tfckpt.latest(d)
         if not name:

@@ -46,6 +46,7 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
     train, test, maps = data.compact_from_read_data(tup, ne, nc, mb)
     theta = layout.init_flat(7, v).astype(np.float64)
     opt = model_ref.AdamTF(theta.size)
+    epoch_theta = []
     for _ in range(2):
         for j in range(2):
             sh = train.slice(j * mb, (j + 1) * mb).with_maps(maps)
@@ -55,6 +56,7 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
             from oracle import layout as olayout
             keys = [k for k, _, _ in olayout.keyed_specs(v)]
             theta = opt.step(theta, np.concatenate([g[k].reshape(-1) for k in keys]))
+        epoch_theta.append(theta.copy())
     np.testing.assert_allclose(m.engine.get_params(), theta, rtol=0, atol=5e-6)
 
     res = tmp_path / "outputSelf" / "tiny" / ("model_%d" % v) / "2" / "result_2.npy"
@@ -68,6 +70,11 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
     first, shape = layout.specs(v)[0]
     np.testing.assert_array_equal(z[first.split(":")[0]].reshape(-1),
                                   m.engine.get_params()[:int(np.prod(shape))])
+    # the epoch-1 bundle (written in the background while epoch 2 ran) holds epoch 1's state
+    z1 = tfckpt.read(str(ck / "g2g.model-2"))
+    np.testing.assert_allclose(z1[first.split(":")[0]].reshape(-1).astype(np.float64),
+                               epoch_theta[0][:int(np.prod(shape))], rtol=0, atol=5e-6)
+    assert not np.array_equal(z1[first.split(":")[0]], z[first.split(":")[0]])
     # resume: a fresh model restores weights, Adam slots and beta powers bit-exactly
     m2 = graph2graph(None, Ds=1, Ne=ne, Nc=nc, Ner=ne * (ne - 1), Ncr=nc * (nc - 1), Dr=2,
                      De_e=20, De_er=20, Mini_batch=mb, checkpoint_dir=args.checkpoint_dir,

@@ -181,3 +181,36 @@ def test_native_crc32c_matches_table_loop():
             assert lib.hdg_crc32c(data, n, c0) == tfckpt.crc32c_py(data, c0)
     assert lib.hdg_crc32c(b"123456789", 9, 0) == 0xE3069283
     assert tfckpt.crc32c(b"123456789") == 0xE3069283
+
+
+def test_background_saver_keeps_order_and_state(tmp_path):
+    """graph2graph.train saves every epoch in the background (Saver.save(background=True)):
+    each bundle holds the state at its save() call even when the engine's tensors change
+    before the writer thread runs, max_to_keep and the state file behave as Saver.save's."""
+    import types
+
+    import torch
+
+    from hdgnn.model import Saver
+    v = 2
+    flat = layout.init_flat(3, v).astype(np.float32)
+    eng = types.SimpleNamespace(params=torch.from_numpy(flat.copy()),
+                                m=torch.zeros(flat.size), v=torch.zeros(flat.size),
+                                beta_pow=torch.tensor([0.9, 0.999]))
+    sv = Saver(types.SimpleNamespace(engine=eng, variant=v))
+    want = {}
+    for step in range(1, 8):
+        eng.params += 1.0               # the "next epoch" runs while the bundle is written
+        eng.m.fill_(step)
+        want[step] = (eng.params.numpy().copy(), float(step))
+        sv.save(None, str(tmp_path / "g2g.model"), global_step=step, background=True)
+    sv.flush()
+    assert tfckpt.latest(str(tmp_path)) == "g2g.model-7"
+    for step in range(1, 8):
+        present = (tmp_path / ("g2g.model-%d.index" % step)).exists()
+        assert present == (step >= 3)                       # newest 5 kept
+        if present:
+            fl, m, _, bp = tfckpt.engine_state(tfckpt.read(str(tmp_path / ("g2g.model-%d" % step))), v)
+            np.testing.assert_array_equal(fl, want[step][0])
+            assert np.all(m == want[step][1])
+            np.testing.assert_array_equal(bp, np.float32([0.9, 0.999]))
