@@ -34,6 +34,7 @@ installed, so reading real TF files is "parity unpinned"; tests/test_tfckpt.py p
 container format by hand-built SSTables, CRC-32C / Snappy known answers and round trips.
 """
 import os
+import functools
 import struct
 
 import numpy as np
@@ -97,7 +98,12 @@ def mask_crc(c):
 
 
 # ------------------------------------------------------------------ varints / protobuf
+_VARINT1 = [bytes((i,)) for i in range(128)]   # one-byte varints (most of a bundle's)
+
+
 def _put_varint(v):
+    if 0 <= v < 128:
+        return _VARINT1[v]
     if v < 0:
         v &= (1 << 64) - 1           # protobuf int32/int64: negatives as 10-byte varints
     out = bytearray()
@@ -173,15 +179,21 @@ def encode_header(num_shards=1):
     return _pb_varint(1, num_shards) + _pb_bytes(3, version)   # endianness LITTLE = default
 
 
-def encode_entry(dtype_enum, shape, shard_id, offset, size, masked_crc):
+@functools.lru_cache(maxsize=4096)
+def _entry_head(dtype_enum, shape, shard_id, offset, size):
+    """BundleEntryProto fields 1-5 (a checkpoint of fixed shapes repeats them every save)."""
     shp = b"".join(_pb_bytes(2, _pb_varint(1, int(d))) for d in shape)
     msg = _pb_varint(1, dtype_enum) + _pb_bytes(2, shp)
     if shard_id:
         msg += _pb_varint(3, shard_id)
     if offset:
         msg += _pb_varint(4, offset)
-    msg += _pb_varint(5, size) + _pb_fixed32(6, masked_crc)
-    return msg
+    return msg + _pb_varint(5, size)
+
+
+def encode_entry(dtype_enum, shape, shard_id, offset, size, masked_crc):
+    return (_entry_head(int(dtype_enum), tuple(int(d) for d in shape), int(shard_id),
+                        int(offset), int(size)) + _pb_fixed32(6, masked_crc))
 
 
 def decode_entry(buf):
