@@ -17,7 +17,7 @@ for path in m2_fused m2_general m4_hybrid; do
     for hd in 0.1 0.3; do
       for xk in int10 real; do
         tag=${path}_e${ed}_h${hd}_${xk}
-        timeout -k 10 200 python bench.py --no-cpu --steps 20 --warmup 4 $pa \
+        timeout -k 10 200 python bench.py --no-cpu --e2e 0 --steps 20 --warmup 4 $pa \
             --edensity $ed --hdensity $hd --xkind $xk > gpurun_out/data/$tag.log 2>&1
         rc=$?
         if [ $rc -ne 0 ]; then echo "$tag rc=$rc"; tail -3 gpurun_out/data/$tag.log; exit $rc; fi

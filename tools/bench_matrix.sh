@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/matrix
 run() {   # run <tag> <bench args...>
   local tag=$1; shift
-  timeout -k 10 300 python bench.py --no-cpu --steps 20 --warmup 3 "$@" > gpurun_out/matrix/$tag.log 2>&1
+  timeout -k 10 300 python bench.py --no-cpu --e2e 0 --steps 20 --warmup 3 "$@" > gpurun_out/matrix/$tag.log 2>&1
   local rc=$?
   echo "$tag rc=$rc $(grep -h '^{' gpurun_out/matrix/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms/step")' 2>/dev/null)"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
@@ -26,5 +26,5 @@ run m4_stress --variant 4 --ne 1024 --nc 512 --batch 32
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_general -o run -- \
-    python3 $R/bench.py --variant 4 --steps 20 --warmup 3 --no-cpu > $R/gpurun_out/matrix/prof_m4.log 2>&1
+    python3 $R/bench.py --variant 4 --steps 20 --warmup 3 --no-cpu --e2e 0 > $R/gpurun_out/matrix/prof_m4.log 2>&1
 echo "prof rc=$?"

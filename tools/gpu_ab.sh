@@ -7,7 +7,7 @@ rc=$?; tail -3 gpurun_out/ab_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 python tools/mid_phases.py > gpurun_out/ab_phases.log 2>&1 || exit $?
 grep -v amdgpu gpurun_out/ab_phases.log
 for i in 1 2; do
-timeout -k 10 300 python bench.py --no-cpu ${BENCH_ARGS} > gpurun_out/ab_bench.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --no-cpu --e2e 0 ${BENCH_ARGS} > gpurun_out/ab_bench.log 2>&1 || exit $?
 python - <<'PY'
 import json
 for l in open("gpurun_out/ab_bench.log"):

@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 R=$(pwd)
 for L in gpurun_lib/lib*.so; do
   n=$(basename $L .so)
-  (cd /tmp && export TMPDIR=/tmp HDG_LIB_PATH=$R/$L && timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/abl_$n -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu ${ABL_ARGS:---path 2} > $R/gpurun_out/abl_$n.log 2>&1) || exit $?
+  (cd /tmp && export TMPDIR=/tmp HDG_LIB_PATH=$R/$L && timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/abl_$n -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --e2e 0 ${ABL_ARGS:---path 2} > $R/gpurun_out/abl_$n.log 2>&1) || exit $?
   python3 - $n <<'PY'
 import csv, glob, re, sys
 f = sorted(glob.glob("gpurun_out/abl_%s/**/*kernel_stats.csv" % sys.argv[1], recursive=True))[0]

@@ -14,4 +14,4 @@ if [ -n "$FIRST" ]; then
 fi
 step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread
 step smoke 300 python __graft_entry__.py smoke
-step bench 600 python bench.py ${BENCH_ARGS:---no-cpu}
+step bench 600 python bench.py ${BENCH_ARGS:---no-cpu --e2e 0}

@@ -4,5 +4,5 @@ cd $GRAFT_REPO_ROOT
 timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
 if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/bench1.log 2>&1; echo "bench rc=$?"; tail -5 gpurun_out/bench1.log
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu --e2e 0 > gpurun_out/bench1.log 2>&1; echo "bench rc=$?"; tail -5 gpurun_out/bench1.log
 fi

@@ -6,7 +6,7 @@ BA=${BENCH_ARGS:---variant 4}
 timeout -k 10 600 python -u -m pytest tests/test_general_gpu.py tests/test_fault_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gen_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/gen_tests.log; [ $rc -ne 0 ] && exit $rc
 R=$(pwd)
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/gen_prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu $BA > $R/gpurun_out/gen_prof.log 2>&1) || exit $?
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/gen_prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --e2e 0 $BA > $R/gpurun_out/gen_prof.log 2>&1) || exit $?
 python3 - <<'PY'
 import csv, glob, json, re
 f = sorted(glob.glob("gpurun_out/gen_prof/**/*kernel_stats.csv", recursive=True))[0]

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 for tag in "$@"; do
   cp $R/hd-gnn_amd/csrc/ab_$tag.so $L
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/m4split/$tag -o run -- \
-      python3 $R/bench.py --variant 4 --steps 50 --warmup 10 --no-cpu > $R/gpurun_out/m4split/$tag.log 2>&1 || exit $?
+      python3 $R/bench.py --variant 4 --steps 50 --warmup 10 --no-cpu --e2e 0 > $R/gpurun_out/m4split/$tag.log 2>&1 || exit $?
   f=$(find $R/gpurun_out/m4split/$tag -name '*kernel_stats.csv' | head -1)
   python3 - "$f" "$tag" <<'PY'
 import csv, sys

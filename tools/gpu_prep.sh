@@ -22,7 +22,7 @@ echo "pytest rc=$rc"; tail -3 gpurun_out/prep/pytest.log
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prep/prof_m2 -o run -- \
-    python3 $R/bench.py --ne 1024 --nc 512 --batch 32 --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/prep/m2_stress.log 2>&1 || exit $?
+    python3 $R/bench.py --ne 1024 --nc 512 --batch 32 --steps 10 --warmup 2 --no-cpu --e2e 0 > $R/gpurun_out/prep/m2_stress.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prep/prof_glide -o run -- \
-    python3 $R/bench.py --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/prep/glide.log 2>&1 || exit $?
+    python3 $R/bench.py --steps 10 --warmup 2 --no-cpu --e2e 0 > $R/gpurun_out/prep/glide.log 2>&1 || exit $?
 grep -h prep $R/gpurun_out/prep/prof_m2/run_kernel_stats.csv $R/gpurun_out/prep/prof_glide/run_kernel_stats.csv

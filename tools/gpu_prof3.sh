@@ -6,5 +6,5 @@ bash $R/tools/profile.sh r03 || exit $?
 bash $R/tools/pmc_flops.sh || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof_m4 -o run -- \
-    python3 $R/bench.py --variant 4 --steps 50 --warmup 10 --no-cpu > $R/gpurun_out/prof_m4.log 2>&1 || exit $?
+    python3 $R/bench.py --variant 4 --steps 50 --warmup 10 --no-cpu --e2e 0 > $R/gpurun_out/prof_m4.log 2>&1 || exit $?
 echo done

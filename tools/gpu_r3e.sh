@@ -3,8 +3,8 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/e_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/e_tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python bench.py --no-cpu > gpurun_out/e_m2.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --no-cpu --variant 4 > gpurun_out/e_m4.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --no-cpu --e2e 0 > gpurun_out/e_m2.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --no-cpu --e2e 0 --variant 4 > gpurun_out/e_m4.log 2>&1 || exit $?
 python - <<'PY'
 import json
 for f in ("e_m2", "e_m4"):

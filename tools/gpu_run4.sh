@@ -12,4 +12,4 @@ step() {   # step <name> <timeout> <cmd...>
 }
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x
 step phases 300 python tools/mid_phases.py
-step bench 300 python bench.py --steps 50 --warmup 10 --no-cpu
+step bench 300 python bench.py --steps 50 --warmup 10 --no-cpu --e2e 0

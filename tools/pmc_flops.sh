@@ -9,5 +9,5 @@ C="SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_MFMA_MO
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 --pmc $C -f csv -d $OUT/cal -o run -- $R/tools/probe/flops_cal > $OUT/cal.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc $C -f csv -d $OUT/bench -o run -- \
-    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --no-graph ${BENCH_ARGS} > $OUT/bench.log 2>&1 || exit $?
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu --e2e 0 --no-graph ${BENCH_ARGS} > $OUT/bench.log 2>&1 || exit $?
 cd $R && python3 tools/pmc_table.py $OUT/cal && python3 tools/pmc_table.py $OUT/bench
