@@ -496,17 +496,25 @@ def remove_bundle(prefix):
 
 
 # ------------------------------------------------------------------ engine state <-> TF names
+@functools.lru_cache(maxsize=None)
+def _var_slices(variant):
+    """(TF name without ':0', offset, size, shape) of every variable of the flat vector."""
+    from . import layout
+    return tuple((name.split(":")[0], o, int(np.prod(shape)), tuple(shape))
+                 for name, (o, shape) in layout.offsets(variant).items())
+
+
 def state_tensors(flat, variant, adam_m=None, adam_v=None, beta_pow=None):
     """Flat engine vectors -> TF-named tensors (model variables, optional TF1 Adam slots)."""
-    from . import layout
+    flat = np.asarray(flat, np.float32)
+    if adam_m is not None:
+        adam_m, adam_v = np.asarray(adam_m, np.float32), np.asarray(adam_v, np.float32)
     out = {}
-    for name, (o, shape) in layout.offsets(variant).items():
-        n = int(np.prod(shape))
-        base = name.split(":")[0]
-        out[base] = np.asarray(flat[o:o + n], np.float32).reshape(shape)
+    for base, o, n, shape in _var_slices(variant):
+        out[base] = flat[o:o + n].reshape(shape)
         if adam_m is not None:
-            out[base + "/Adam"] = np.asarray(adam_m[o:o + n], np.float32).reshape(shape)
-            out[base + "/Adam_1"] = np.asarray(adam_v[o:o + n], np.float32).reshape(shape)
+            out[base + "/Adam"] = adam_m[o:o + n].reshape(shape)
+            out[base + "/Adam_1"] = adam_v[o:o + n].reshape(shape)
     if beta_pow is not None:
         out["beta1_power"] = np.asarray(beta_pow[0], np.float32).reshape(())
         out["beta2_power"] = np.asarray(beta_pow[1], np.float32).reshape(())
