@@ -2488,7 +2488,15 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   __shared__ float kz[1];                         // 0.f: stride-0 operand of padding tiles
   const float *U1e = Wl, *Q2 = Wl + 400;          // classifier rows 2..21 | EE second layer
   if (threadIdx.x == 0) kz[0] = 0.f;
-  const int b = blockIdx.y, t0 = blockIdx.x * TN, t = threadIdx.x, te = gridDim.x;
+  // XCD-grouped rows: the partial-gradient stores below are 4-byte values at a stride of
+  // the te*B rows, so a 64-byte line holds 16 neighbouring rows' values; dealing the rows
+  // to the 8 XCDs in contiguous ranges (block L runs on XCD L % 8) lets each line's
+  // partial writes merge in one L2 instead of reaching HBM from several
+  const int te = gridDim.x, nrow = te * gridDim.y, lin = blockIdx.y * te + blockIdx.x;
+  const int nx = nrow & ~7;
+  const int lrow = lin < nx ? (lin & 7) * (nx >> 3) + (lin >> 3) : lin;
+  const int b = lrow / te, tile = lrow - b * te;
+  const int t0 = tile * TN, t = threadIdx.x;
   const size_t base = ((size_t)b * Ne + t0) * H;
   stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
   stage_w(Wl + 400, W + o.EE_W2, 400);
@@ -2563,7 +2571,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
       }
     }
   }
-  const int row = b * te + blockIdx.x;
+  const int row = lrow;
   const Seg& s1 = sg.s[SG_ECW1E];
   const Seg& s2 = sg.s[SG_EEW2];
   const float Ne1 = (float)(Ne - 1);
