@@ -27,17 +27,83 @@ import torch  # noqa: E402
 METRIC = "training-step commits/sec, glide Ne=200 Nc=74 batch=100; 1/2/4/8 GPU"
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
 HBM_PEAK_GBS = 8000.0
+CLOCK_HZ = 2.4e9              # gfx950 peak engine clock (MI355X_MICROARCH.md)
 
 
-def _prof(name):
-    """The newest round's copy of a committed profile file (profiles/rNN/<name>)."""
+def find_profile(variant, path, ne, nc, batch):
+    """The newest committed rocprofv3 profile of this exact workload:
+    profiles/rNN/<config>/roofline.json (tools/roofline_profile.py) whose config matches
+    (variant, engine path, Ne, Nc, batch per GPU) on the default synthetic data."""
     pd = os.path.join(ROOT, "profiles")
-    rounds = sorted(d for d in os.listdir(pd) if d.startswith("r") and d[1:].isdigit()) \
-        if os.path.isdir(pd) else []
-    for d in reversed(rounds):
-        if os.path.exists(os.path.join(pd, d, name)):
-            return os.path.join(pd, d, name)
-    return os.path.join(pd, "r02", name)
+    rounds = sorted((d for d in os.listdir(pd) if d.startswith("r") and d[1:].isdigit()),
+                    reverse=True) if os.path.isdir(pd) else []
+    want = {"variant": variant, "path": path, "ne": ne, "nc": nc, "batch": batch}
+    for d in rounds:
+        for sub in sorted(os.listdir(os.path.join(pd, d))):
+            f = os.path.join(pd, d, sub, "roofline.json")
+            if os.path.isfile(f):
+                with open(f) as fh:
+                    pj = json.load(fh)
+                if {k: pj["config"].get(k) for k in want} == want:
+                    return f, pj
+    return None, None
+
+
+def build_roofline(dom, kern_ms, variant, path, ne, nc, batch, default_data):
+    """Roofline of the step's dominant kernel (the longest of the live per-kernel HIP-event
+    times) from the committed profile of the same workload: executed FP32 FLOPs per launch
+    (calibrated PMC counters) and HBM bytes per launch, over the LIVE average duration."""
+    f, pj = find_profile(variant, path, ne, nc, batch) if default_data else (None, None)
+    t = kern_ms[dom] * 1e-3
+    dense = flops_per_commit(ne, nc, variant) * batch
+    r = {"bound": None, "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": None, "traffic": None, "kernel": dom, "avg_launch_ms": round(kern_ms[dom], 5),
+         "algorithmic_bytes_per_launch": algorithmic_bytes_per_commit(ne, nc) * batch,
+         "compact_bytes_per_launch": compact_bytes_per_commit(ne, nc) * batch,
+         "dense_equivalent": {
+             "flops_per_step": dense,
+             "tflops": round(dense / (sum(kern_ms.values()) * 1e-3) / 1e12, 3),
+             "note": "SURVEY 8(d) per-commit figure (3 F_fwd: the TF graph's dense "
+                     "incidence-matrix work) over the whole fwd+bwd; the engine's sorted-x / "
+                     "per-node algebra (DESIGN.md 3) executes ~13x fewer operations, so this "
+                     "is work-equivalent throughput, not a hardware roofline (no frac)"},
+         "profile": None}
+    if pj is None:
+        r["profile"] = "no committed profile of this workload (tools/profile_config.sh)"
+        return r
+    kp = pj["kernels"].get(dom)
+    r["profile"] = os.path.relpath(f, ROOT)
+    if kp is None:
+        r["profile"] += ": kernel %s not in the profile" % dom
+        return r
+    fl = kp.get("executed_flops")
+    if fl:
+        r["achieved"] = round(fl / t / 1e12, 3)
+        r["frac"] = round(fl / t / 1e12 / FP32_PEAK_TFLOPS, 4)
+        r["flops_per_launch"] = fl
+    r["traffic"] = kp.get("hbm_bytes")
+    r["traffic_bounds"] = [kp.get("hbm_bytes_lower"), kp.get("hbm_bytes_upper")]
+    r["traffic_note"] = pj.get("traffic_note")
+    if r["traffic"]:
+        r["hbm_frac"] = round(r["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4)
+    vi = kp.get("valu_wave_insts")
+    if vi:           # a wave64 VALU instruction holds a SIMD for 4 cycles; 4 SIMDs per CU
+        r["executed"] = {"valu_wave_insts_per_launch": vi,
+                         "issue_frac_chip": round(vi / (t * CLOCK_HZ / 4 * 256 * 4), 4),
+                         "wait_any_frac": kp.get("wait_any_frac")}
+    issue = r.get("executed", {}).get("issue_frac_chip") or 0.0
+    r["bound"] = "valu-issue" if issue >= (r.get("hbm_frac") or 0.0) else "hbm"
+    # the whole step (every kernel of fwd+bwd) from the same profile
+    ks = [k for k in kern_ms if k in pj["kernels"] and pj["kernels"][k].get("executed_flops")]
+    if ks:
+        tot_t = sum(kern_ms.values()) * 1e-3
+        tot_f = sum(pj["kernels"][k]["executed_flops"] for k in ks)
+        tot_b = sum(pj["kernels"][k].get("hbm_bytes") or 0 for k in kern_ms if k in pj["kernels"])
+        r["step"] = {"kernels": len(kern_ms), "executed_flops": tot_f,
+                     "tflops": round(tot_f / tot_t / 1e12, 3),
+                     "frac": round(tot_f / tot_t / 1e12 / FP32_PEAK_TFLOPS, 4),
+                     "hbm_bytes": tot_b, "hbm_frac": round(tot_b / tot_t / 1e9 / HBM_PEAK_GBS, 4)}
+    return r
 
 
 def flops_per_commit(ne, nc, variant=2):
@@ -149,8 +215,9 @@ def e2e_train(B, ne, nc, v, epochs, dev):
             "commits_per_s": round(epochs * B / wall, 1),
             "ms_per_epoch": round(1e3 * wall / epochs, 3),
             "note": "graph2graph.train as main.py runs it: upload + hdg_prepare of the batch, "
-                    "then per epoch one training step, one device->host read of the epoch's "
-                    "losses / count, the result line + file and a TF-bundle checkpoint save"}
+                    "then per epoch one training step, the epoch's stats and state read to "
+                    "pinned host memory (epochs pipelined one deep), the result line + file "
+                    "and a TF-bundle checkpoint written by libhdgnn on the saver thread"}
 
 
 def main():
@@ -170,7 +237,6 @@ def main():
                     help="model_<variant>.py (the BASELINE metric is model_2)")
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "hbm_traffic.json"))
     ap.add_argument("--edensity", type=float, default=0.05,
                     help="synthetic entity-adjacency density (data-dependence runs)")
     ap.add_argument("--hdensity", type=float, default=0.10,
@@ -246,27 +312,29 @@ def main():
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
-    # per-kernel durations (HIP events on the launch stream), separate instrumented pass
-    ev = _lib.HipEvents(3)
-    # model_2 on the fused path: the step kernel and the reduction timed apart; model_4 on
-    # the fused path (entity-edge stage on general-path kernels around the step kernel) and
-    # the general path: the whole fwd+bwd
-    fused = eng.path == _lib.PATH_FUSED and v == 2
-    names = (["k_commit_step", "k_grad_reduce"] if fused else
-             ["hybrid_fwd_bwd" if eng.path == _lib.PATH_FUSED else "general_fwd_bwd", "none"])
-    acc = dict.fromkeys(names, 0.0)
-    nev = max(10, min(args.steps, 50))
+    # per-kernel durations: HIP events on the launch stream after every kernel launch of
+    # the step (hdg_fwd_bwd_kernel_events), eager launches, a separate instrumented pass
+    # with the training step's outputs (probs, as the training sess.run fetches; no logits)
     import ctypes
+    NEV = 40
+    ev = _lib.HipEvents(NEV)
+    kn = (ctypes.c_char_p * (NEV - 1))()
+    nk = ctypes.c_int32()
+    acc, order = {}, []
+    nev = max(10, min(args.steps, 50))
     tails = []                  # data parallel: the all-reduce + Adam tail after fwd_bwd
     for _ in range(nev):
         bstruct = db.struct()
-        _lib.check(eng.lib.hdg_fwd_bwd_events(ctypes.byref(eng.shape), ctypes.byref(bstruct),
-                                              ctypes.c_void_p(eng.params.data_ptr()),
-                                              ctypes.c_void_p(eng.grad_local.data_ptr()),
-                                              ctypes.byref(eng._out),
-                                              ctypes.c_void_p(eng.workspace.data_ptr()),
-                                              eng._stream(), ev.ev))
-        for i, n in enumerate(names):
+        _lib.check(eng.lib.hdg_fwd_bwd_kernel_events(
+            ctypes.byref(eng.shape), ctypes.byref(bstruct), ctypes.c_void_p(eng.params.data_ptr()),
+            ctypes.c_void_p(eng.grad_local.data_ptr()), ctypes.byref(eng._outputs(True, False)),
+            ctypes.c_void_p(eng.workspace.data_ptr()), eng._stream(), ev.ev, NEV, kn,
+            ctypes.byref(nk)))
+        for i in range(nk.value):
+            n = kn[i].decode()
+            if n not in acc:
+                acc[n] = 0.0
+                order.append(n)
             acc[n] += ev.elapsed_ms(i, i + 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -276,69 +344,15 @@ def main():
         e1.record()
         tails.append((e0, e1))
     torch.cuda.synchronize(dev)
-    kern_ms = {n: acc[n] / nev for n in names}
+    kern_ms = {n: acc[n] / nev for n in order}
     tail_ms = sum(a.elapsed_time(b) for a, b in tails) / nev
 
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
-    dom = names[0]
-    dense_launch = flops_per_commit(ne, nc, v) * B
-    dense_tflops = dense_launch / (kern_ms[dom] * 1e-3) / 1e12
-    # executed FP32 FLOPs of one launch (rocprofv3 PMC, calibrated: tools/flops_summary.py)
-    exec_flops, flops_src = None, None
-    fj = _prof("flops_pmc.json")
-    if fused and os.path.exists(fj):
-        with open(fj) as f:
-            pj = json.load(f)
-        if pj["config"] == {"ne": ne, "nc": nc, "batch": B} and v == 2:
-            ks = [k for k in pj["kernels"] if k.startswith(dom)]
-            if ks:
-                exec_flops = pj["kernels"][ks[0]]["executed_flops_per_launch"]
-                flops_src = (os.path.relpath(fj, ROOT) + ": 64 x SQ_INSTS_VALU_FLOPS_FP32 + 512 x "
-                             "SQ_INSTS_VALU_MFMA_MOPS_F32 per launch, counters calibrated "
-                             "on known instruction streams (tools/probe/flops_cal.hip)")
-    achieved = exec_flops / (kern_ms[dom] * 1e-3) / 1e12 if exec_flops else None
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if (tj.get("kernel") == dom and tj.get("batch") == B and tj.get("ne") == ne
-                and tj.get("nc") == nc and fused and default_data):
-            traffic = tj.get("bytes_per_launch")
-    executed = None              # executed-instruction view (SQ counters, tools/valu_issue.py)
-    vj = _prof("valu_issue.json")
-    if fused and (ne, nc, B) == (200, 74, 100) and default_data and os.path.exists(vj):
-        with open(vj) as f:
-            ev = json.load(f)
-        executed = {"valu_wave_insts_per_launch": ev.get("sq_insts_valu_per_launch"),
-                    "issue_frac_chip": round(ev.get("issue_frac_chip", 0.0), 4),
-                    "issue_frac_busy_cus": round(ev.get("issue_frac_busy_cus", 0.0), 4),
-                    "source": os.path.relpath(vj, ROOT) + " (rocprofv3 SQ_INSTS_VALU over the "
-                              "kernel's rocprof duration; 4 cycles per wave64 VALU op per SIMD)"}
-    # bound: VALU issue.  The kernel's work is FP32 on the vector ALUs (2/3 of its executed
-    # FLOPs) and MFMA; what binds it is instruction issue and latency, not the FP32 FLOP
-    # roof, so achieved/peak is the executed-FLOP fraction of the 157.3 TFLOP/s FP32 peak
-    # and executed.issue_frac_* is the issue-slot fraction next to it
-    roofline = {"bound": "valu-issue" if fused else "mfma",
-                "achieved": round(achieved, 3) if achieved else None,
-                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4) if achieved else None,
-                "traffic": traffic, "kernel": dom,
-                "flops_per_launch": exec_flops, "flops_source": flops_src,
-                "avg_launch_ms": round(kern_ms[dom], 5),
-                "algorithmic_bytes_per_launch": algorithmic_bytes_per_commit(ne, nc) * B,
-                "compact_bytes_per_launch": compact_bytes_per_commit(ne, nc) * B,
-                "hbm_frac": (round(traffic / (kern_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                             if traffic else None),
-                "dense_equivalent": {
-                    "flops_per_launch": dense_launch, "tflops": round(dense_tflops, 3),
-                    "note": "SURVEY 8(d) per-commit figure (3 F_fwd: the TF graph's dense "
-                            "incidence-matrix work) over the same launch time; the engine's "
-                            "sorted-x / per-node algebra (DESIGN.md 3) needs ~13x fewer "
-                            "operations, so this is work-equivalent throughput, not a "
-                            "hardware roofline (no frac)"},
-                "executed": executed}
+    path_name = {_lib.PATH_FUSED: "fused", _lib.PATH_GENERAL: "general"}[eng.path]
+    dom = max(kern_ms, key=kern_ms.get)          # the dominant kernel of the step
+    roofline = build_roofline(dom, kern_ms, v, path_name, ne, nc, B, default_data)
     e2e = None
     if world == 1 and args.e2e > 0:
         try:                     # a side measurement: never costs the bench line
@@ -362,8 +376,7 @@ def main():
             "config": {"workload": "model_%d (%s) train step: fwd+bwd+TF-Adam, %s" % (
                            v, {1: "HD-GNN/ES", 2: "HD-GNN/S", 3: "HD-GNN/E", 4: "HD-GNN"}[v],
                            "glide step=2" if (ne, nc) == (200, 74) else "Ne=%d Nc=%d" % (ne, nc)),
-                       "engine_path": {_lib.PATH_FUSED: "fused", _lib.PATH_GENERAL: "general"}[
-                           eng.path] + (" (entity-edge stage on general kernels)"
+                       "engine_path": path_name + (" (entity-edge stage on general kernels)"
                                         if eng.path == _lib.PATH_FUSED and v == 4 else ""),
                        "launch": "eager" if args.no_graph else
                                  "hipGraph replay, %d training steps per graph" % gsteps,
@@ -377,7 +390,8 @@ def main():
                            "k_dp_tail work); rccl: all_reduce + hdg_adam_tf"} if launched else None,
             "upload_prepare_ms": round(upload_ms, 3),
             "pcie_inclusive_commits_per_s": round(world * B / ((ms_per_step + upload_ms) * 1e-3), 1),
-            "kernels_ms": {k: round(v, 5) for k, v in kern_ms.items()}}
+            "kernels_ms": {k: round(t, 5) for k, t in kern_ms.items()},
+            "fwd_bwd_ms": round(sum(kern_ms.values()), 5)}
     if e2e:
         line["e2e"] = e2e
     print(json.dumps(line), flush=True)

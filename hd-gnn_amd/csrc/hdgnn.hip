@@ -22,6 +22,7 @@
 //   are prefix/suffix sums over the x-sorted order (O(Ne log nd) per hidden unit)
 //   plus sparse corrections for a = 1.  Hunk pairs run as dense register tiles.
 #include <hip/hip_runtime.h>
+#include <vector>
 
 #include <math.h>
 #include <stdarg.h>
@@ -3260,6 +3261,7 @@ int prep_tile(int ne, int nc) {
 namespace hdg {
 
 thread_local char g_err[512] = "";
+thread_local KTrace* g_ktrace = nullptr;
 
 int fail(int code, const char* fmt, ...) {
   va_list ap;
@@ -3479,7 +3481,7 @@ hipError_t launch_step(const hdg_shape* s, const hdg_batch* bt, const float* par
                      s->batch, (unsigned long long*)(ws + w.xch), o.status,
                      SPLIT ? debug_xfault() : 0u, hy.ins, hy.ncpart, hy.ncpt, hy.dnout,
                      (!TRAIN && o.ehr) ? 1 : 0);
-  return hipGetLastError();
+  return hdg::kmark("k_commit_step", st);
 }
 
 template <bool TRAIN, bool STAMPS = false>
@@ -3591,7 +3593,7 @@ int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, flo
     // the fused rows: [0, H1_W1) in place, [H1_W1, GRAD_LEN) past the entity-edge block
     hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
                        ws + w.part, R, 0, GRAD_LEN, m2::H1_W1, ins, grad);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(hdg::kmark("k_grad_reduce", st));
     if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st)) return rc;
   }
   HIP_TRY(mark(1));
@@ -3704,9 +3706,24 @@ int hdg_fwd_bwd_events(const hdg_shape* s, const hdg_batch* bt, const float* par
   HIP_TRY(mark(1));
   hipLaunchKernelGGL(k_grad_reduce, dim3((GRAD_LEN + RED_P - 1) / RED_P), dim3(1024), 0, st,
                      ws + w.part, part_rows(s, split), 0, GRAD_LEN, GRAD_LEN, 0, grad);
-  HIP_TRY(hipGetLastError());
+  HIP_TRY(hdg::kmark("k_grad_reduce", st));
   HIP_TRY(mark(2));
   return 0;
+}
+
+int hdg_fwd_bwd_kernel_events(const hdg_shape* s, const hdg_batch* bt, const float* params,
+                              float* grad, hdg_outputs* out, void* workspace, void* stream,
+                              void* const* events, int32_t n_events, const char** names,
+                              int32_t* n_kernels) {
+  if (!events || n_events < 2 || !names || !n_kernels)
+    return fail(HDG_EINVAL, "hdg_fwd_bwd_kernel_events: need >= 2 events, names, n_kernels");
+  hdg::KTrace t{events, (int)n_events, 0, names};
+  HIP_TRY(hipEventRecord((hipEvent_t)events[0], (hipStream_t)stream));
+  hdg::g_ktrace = &t;
+  const int rc = hdg_fwd_bwd_events(s, bt, params, grad, out, workspace, stream, nullptr);
+  hdg::g_ktrace = nullptr;
+  *n_kernels = t.n;
+  return rc;
 }
 
 int hdg_fwd_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, float* grad,
@@ -3807,20 +3824,21 @@ size_t hdg_dp_mailbox_bytes(void) { return dpk::BYTES; }
 // CRC-32C (Castagnoli, reflected 0x82F63B78), slicing by 8: the checksum of the TF V2
 // checkpoint bundle's records (hdgnn.tfckpt; LevelDB / TF masked CRCs)
 uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc) {
-  static uint32_t tab[8][256];
-  static bool init = false;                     // idempotent: same table for every caller
-  if (!__atomic_load_n(&init, __ATOMIC_ACQUIRE)) {
+  // slicing-by-8 tables, built once (a C++11 function-local static: thread-safe init)
+  struct Tab {
     uint32_t t[8][256];
-    for (uint32_t i = 0; i < 256; ++i) {
-      uint32_t c = i;
-      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
-      t[0][i] = c;
+    Tab() {
+      for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+        t[0][i] = c;
+      }
+      for (uint32_t i = 0; i < 256; ++i)
+        for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFFu];
     }
-    for (uint32_t i = 0; i < 256; ++i)
-      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFFu];
-    memcpy(tab, t, sizeof t);
-    __atomic_store_n(&init, true, __ATOMIC_RELEASE);
-  }
+  };
+  static const Tab T;
+  const auto& tab = T.t;
   const uint8_t* p = static_cast<const uint8_t*>(data);
   uint32_t c = crc ^ 0xFFFFFFFFu;
   for (; n >= 8; n -= 8, p += 8) {
@@ -3834,6 +3852,46 @@ uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc) {
   }
   for (; n; --n, ++p) c = tab[0][(c ^ *p) & 0xFFu] ^ (c >> 8);
   return c ^ 0xFFFFFFFFu;
+}
+
+static uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+static int write_file(const char* path, const void* p, size_t n) {
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(HDG_EINVAL, "cannot open %s for writing", path);
+  const size_t w = n ? fwrite(p, 1, n, f) : 0;
+  const int rc = fclose(f);
+  if (w != n || rc != 0) return fail(HDG_EINVAL, "short write to %s", path);
+  return 0;
+}
+
+int hdg_bundle_write(const char* data_path, const char* index_path, const float* state,
+                     const int32_t* gather, int64_t n_floats, uint8_t* index_img,
+                     int64_t index_len, const int64_t* entries, int32_t n_entries,
+                     const int64_t* blocks, int32_t n_blocks) {
+  if (!data_path || !index_path || !state || !gather || n_floats < 0 || !index_img ||
+      index_len < 48 || (n_entries && !entries) || (n_blocks && !blocks))
+    return fail(HDG_EINVAL, "hdg_bundle_write: bad arguments");
+  std::vector<float> blob((size_t)n_floats);
+  for (int64_t i = 0; i < n_floats; ++i) blob[i] = state[gather[i]];
+  const uint8_t* bytes = reinterpret_cast<const uint8_t*>(blob.data());
+  const int64_t nbytes = n_floats * 4;
+  for (int32_t e = 0; e < n_entries; ++e) {        // entry proto field 6: masked CRC of bytes
+    const int64_t off = entries[3 * e], size = entries[3 * e + 1], pos = entries[3 * e + 2];
+    if (off < 0 || size < 0 || off + size > nbytes || pos < 0 || pos + 4 > index_len)
+      return fail(HDG_EINVAL, "hdg_bundle_write: entry %d out of range", (int)e);
+    const uint32_t c = mask_crc(hdg_crc32c(bytes + off, (size_t)size, 0));
+    memcpy(index_img + pos, &c, 4);
+  }
+  for (int32_t b = 0; b < n_blocks; ++b) {         // block trailer: type byte + masked CRC
+    const int64_t off = blocks[2 * b], len = blocks[2 * b + 1];
+    if (off < 0 || len < 0 || off + len + 5 > index_len)
+      return fail(HDG_EINVAL, "hdg_bundle_write: block %d out of range", (int)b);
+    const uint32_t c = mask_crc(hdg_crc32c(index_img + off, (size_t)len + 1, 0));
+    memcpy(index_img + off + len + 1, &c, 4);
+  }
+  if (int rc = write_file(data_path, bytes, (size_t)nbytes)) return rc;
+  return write_file(index_path, index_img, (size_t)index_len);
 }
 
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle) {

@@ -134,6 +134,24 @@ hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride,
                             int o_kt, int o_ncst, hipStream_t st);
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Per-kernel timing hook (hdg_fwd_bwd_kernel_events): while a traced call runs, every
+// launch site of the step records one event after its launch, so events[k] .. events[k+1]
+// bracket the k-th kernel on the stream.  Thread-local and NULL outside a traced call.
+struct KTrace {
+  void* const* ev;
+  int cap, n;
+  const char** names;
+};
+extern thread_local KTrace* g_ktrace;
+// the launch's error, then (traced calls only) the event after it
+inline hipError_t kmark(const char* name, hipStream_t st) {
+  const hipError_t e = hipGetLastError();
+  KTrace* t = g_ktrace;
+  if (e != hipSuccess || !t || t->n + 1 >= t->cap) return e;
+  t->names[t->n++] = name;
+  return hipEventRecord((hipEvent_t)t->ev[t->n], st);
+}
+
 // ------------------------------------------------------------------------------
 // MFMA 16x16 fp32 tile (v_mfma_f32_16x16x4_f32) used by both paths
 // ------------------------------------------------------------------------------

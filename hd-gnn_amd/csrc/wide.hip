@@ -1603,6 +1603,42 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   }
 }
 
+// kw_hunk_mlpb's epilogue: the tile's D alpha / D beta rows out, the partial rows of dV1
+// (rows 0..3 / 4..7 from the pass's node vectors, 8, 9 from the row pass) and dc1.
+// res / yres: [TN][HP] LDS (padding nodes zeroed here), nt: [TN][4] LDS scratch.
+__device__ __forceinline__ void mlpb_epilogue(int z, int b, int t0, int tc, int Nc,
+                                              const float* __restrict__ nvec, float* res,
+                                              float* yres, float* nt, float* __restrict__ Dal,
+                                              float* __restrict__ Dbe, float* __restrict__ part,
+                                              const Segs& sg) {
+  float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H;
+  for (int e = threadIdx.x; e < TN * H; e += blockDim.x) {
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Nc;
+    if (!in) { res[n * HP + k] = 0.f; yres[n * HP + k] = 0.f; }
+    else dout[(t0 + n) * H + k] = res[n * HP + k];
+  }
+  for (int e = threadIdx.x; e < TN * 4; e += blockDim.x)
+    nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
+  __syncthreads();
+  const int row = (b * tc + blockIdx.x) * 2 + z;
+  const Seg& s = sg.s[SG_MLPB];
+  for (int e = threadIdx.x; e < 11 * H; e += blockDim.x) {   // rows 0..9 of V1, then c1
+    const int l = e / H, k = e - l * H;
+    float a = 0.f;
+    if (l < 8) {
+      const int m = l & 3;
+      if ((l >> 2) == z)
+        for (int n = 0; n < TN; ++n) a = fmaf(nt[n * 4 + m], res[n * HP + k], a);
+    } else if (z == 0) {
+      float sd = 0.f, sy = 0.f;
+      for (int n = 0; n < TN; ++n) { sd += res[n * HP + k]; sy += yres[n * HP + k]; }
+      a = l == 8 ? sd - sy : (l == 9 ? sy : sd);
+    }
+    put(part, s, e, row, a);
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // kw_hunk_mlpb  grid (tc, B, 2): hunk pair MLP backward (model_2.py:257-275)
 //   dz_pq = [alpha_p + beta_q + y delta > 0] (dG_p + dH_q)
@@ -1683,32 +1719,260 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
   }
   combine8(acc, buf, res);
   if (z == 0) combine8(ya, buf, yres);
-  float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H;
-  for (int e = threadIdx.x; e < TN * H; e += NTP) {
-    const int n = e / H, k = e - n * H;
-    const bool in = t0 + n < Nc;
-    if (!in) { res[n * HP + k] = 0.f; yres[n * HP + k] = 0.f; }
-    else dout[(t0 + n) * H + k] = res[n * HP + k];
+  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg);
+}
+
+// ---------------------------------------------------------------------------------
+// Sorted-threshold hunk pair sums (general path, Nc >= hunk_sorted_min()).  For hidden
+// unit k the y = 0 pre-activation of pair (p, q) is z0 = fl(alpha_p + beta_q), and
+// fl(a + b) > 0 exactly when b > -a, so {q : z0_pq > 0} is a suffix of the beta-sorted
+// order (and {p : z0_pq > 0} of the alpha-sorted order): one binary search per node and
+// unit plus f64 suffix sums replace the dense sweep (kw_hunk_fwd's relu sums,
+// kw_hunk_mlpb's mask sums).  The y = 1 pairs are corrected one by one over the set bits
+// of the node's label row (z1 = fl(z0 + delta), the dense kernels' expression), and the
+// self pair is removed.  O(Nc H (log Nc + deg_y)) per commit instead of O(Nc^2 H).
+//   side 0: beta sorted (the row pass: node p, swept q); side 1: alpha (the column pass)
+// Tables per (commit, side, unit), hsort_layout: sv f32 [NcP] values ascending, sp i32 [NcP]
+// node of each slot, sx f64 [NcP + 1] suffix sums of sv, sw f64 [NcP + 1] suffix sums of
+// the backward weights w[sp[r]] (side 0: dH, side 1: dG; kw_hunk_wsum).
+// ---------------------------------------------------------------------------------
+struct HSort {
+  size_t sv, sp, sx, sw;   // float offsets into the workspace
+  int NcP;
+};
+__host__ __device__ inline size_t hsort_tab(int b, int side, int k, int len) {
+  return (((size_t)b * 2 + side) * H + k) * (size_t)len;
+}
+
+// kw_hunk_sort  grid (H, B, 2), NT threads, dynamic LDS 8 * pow2(Nc) bytes: bitonic sort
+// of (value, node) keys (ties by node: a fixed order, so every table is deterministic),
+// then f64 suffix sums of the values
+__global__ __launch_bounds__(NT) void kw_hunk_sort(const float* __restrict__ alpha,
+                                                   const float* __restrict__ beta, int Nc,
+                                                   float* __restrict__ sv, int* __restrict__ sp,
+                                                   double* __restrict__ sx) {
+  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
+  __shared__ double cs[NW];
+  const int k = blockIdx.x, b = blockIdx.y, side = blockIdx.z, t = threadIdx.x;
+  const int NcP = (Nc + 3) & ~3;
+  int NP2 = 1;
+  while (NP2 < Nc) NP2 <<= 1;
+  float* kv = hs_lds;
+  int* ki = reinterpret_cast<int*>(hs_lds + NP2);
+  const float* src = (side ? alpha : beta) + (size_t)b * Nc * H;
+  for (int e = t; e < NP2; e += NT) {
+    kv[e] = e < Nc ? src[(size_t)e * H + k] : __builtin_inff();
+    ki[e] = e;
   }
-  for (int e = threadIdx.x; e < TN * 4; e += NTP)
-    nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
   __syncthreads();
-  const int row = (b * tc + blockIdx.x) * 2 + z;
-  const Seg& s = sg.s[SG_MLPB];
-  for (int e = threadIdx.x; e < 11 * H; e += NTP) {   // rows 0..9 of V1, then c1
-    const int l = e / H, k = e - l * H;
-    float a = 0.f;
-    if (l < 8) {
-      const int m = l & 3;
-      if ((l >> 2) == z)
-        for (int n = 0; n < TN; ++n) a = fmaf(nt[n * 4 + m], res[n * HP + k], a);
-    } else if (z == 0) {
-      float sd = 0.f, sy = 0.f;
-      for (int n = 0; n < TN; ++n) { sd += res[n * HP + k]; sy += yres[n * HP + k]; }
-      a = l == 8 ? sd - sy : (l == 9 ? sy : sd);
+  for (int len = 2; len <= NP2; len <<= 1) {
+    for (int st = len >> 1; st > 0; st >>= 1) {
+      for (int e = t; e < NP2 / 2; e += NT) {
+        const int lo = ((e / st) * 2 * st) + (e % st), hi = lo + st;
+        const bool up = (lo & len) == 0;
+        const float a = kv[lo], c = kv[hi];
+        const int ia = ki[lo], ic = ki[hi];
+        const bool gt = a > c || (a == c && ia > ic);
+        if (gt == up) {
+          kv[lo] = c; kv[hi] = a;
+          ki[lo] = ic; ki[hi] = ia;
+        }
+      }
+      __syncthreads();
     }
-    put(part, s, e, row, a);
   }
+  const size_t tb = hsort_tab(b, side, k, NcP), tx = hsort_tab(b, side, k, NcP + 1);
+  for (int e = t; e < Nc; e += NT) {
+    sv[tb + e] = kv[e];
+    sp[tb + e] = ki[e];
+  }
+  // suffix sums: thread t owns slots [t C, t C + C) in reverse order
+  const int C = (Nc + NT - 1) / NT;
+  const int r1 = Nc - t * C, r0 = r1 - C > 0 ? r1 - C : 0;   // slots [r0, r1), high first
+  double a = 0.0;
+  for (int r = r1 - 1; r >= r0; --r) a += (double)kv[r];
+  const int lane = t & 63, w = t >> 6;
+  double inc = a;
+#pragma unroll
+  for (int o2 = 1; o2 < 64; o2 <<= 1) {
+    const double u = __shfl_up(inc, o2);
+    if (lane >= o2) inc += u;
+  }
+  if (lane == 63) cs[w] = inc;
+  __syncthreads();
+  double base = 0.0;
+  for (int u = 0; u < w; ++u) base += cs[u];
+  double run = base + (inc - a);           // sum of the slots above this thread's chunk
+  if (t == 0) sx[tx + Nc] = 0.0;
+  for (int r = r1 - 1; r >= r0; --r) {
+    run += (double)kv[r];
+    sx[tx + r] = run;
+  }
+}
+
+// kw_hunk_wsum  grid (H, B, 2): sw[m] = sum_{r >= m} w[sp[r]][k], side 0: w = dH, 1: dG
+__global__ __launch_bounds__(NT) void kw_hunk_wsum(const int* __restrict__ sp,
+                                                   const float* __restrict__ dG,
+                                                   const float* __restrict__ dH, int Nc,
+                                                   double* __restrict__ sw) {
+  __shared__ double cs[NW];
+  const int k = blockIdx.x, b = blockIdx.y, side = blockIdx.z, t = threadIdx.x;
+  const int NcP = (Nc + 3) & ~3;
+  const float* wv = (side ? dG : dH) + (size_t)b * Nc * H;
+  const int* pm = sp + hsort_tab(b, side, k, NcP);
+  double* T = sw + hsort_tab(b, side, k, NcP + 1);
+  const int C = (Nc + NT - 1) / NT;
+  const int r1 = Nc - t * C, r0 = r1 - C > 0 ? r1 - C : 0;
+  double a = 0.0;
+  for (int r = r1 - 1; r >= r0; --r) a += (double)wv[(size_t)pm[r] * H + k];
+  const int lane = t & 63, w = t >> 6;
+  double inc = a;
+#pragma unroll
+  for (int o2 = 1; o2 < 64; o2 <<= 1) {
+    const double u = __shfl_up(inc, o2);
+    if (lane >= o2) inc += u;
+  }
+  if (lane == 63) cs[w] = inc;
+  __syncthreads();
+  double base = 0.0;
+  for (int u = 0; u < w; ++u) base += cs[u];
+  double run = base + (inc - a);
+  if (t == 0) T[Nc] = 0.0;
+  for (int r = r1 - 1; r >= r0; --r) {
+    run += (double)wv[(size_t)pm[r] * H + k];
+    T[r] = run;
+  }
+}
+
+// first slot m with sv[m] > thr (Nc if none): sv ascending
+__device__ __forceinline__ int upper_slot(const float* __restrict__ sv, int Nc, float thr) {
+  int m = 0;
+  for (int st = top_pow2(Nc); st > 0; st >>= 1)
+    if (m + st - 1 < Nc && !(sv[m + st - 1] > thr)) m += st;
+  return m;
+}
+
+// kw_hunk_fwd_s  grid (tc, B, 2), NT threads: kw_hunk_fwd's results (G / H, sigma / tau)
+// from the sorted tables.  Lane = node of the tile, wave w = units [5w, 5w + 5).
+__global__ __launch_bounds__(NT) void kw_hunk_fwd_s(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ sv, const double* __restrict__ sx,
+    float* __restrict__ G, float* __restrict__ Hh, float* __restrict__ sig,
+    float* __restrict__ tau) {
+#pragma clang fp contract(off)
+  __shared__ float res[TN * HP];
+  __shared__ float Ml[H * H];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5, NcP = (Nc + 3) & ~3;
+  stage_w(Ml, D + D_M, H * H);
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
+  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
+  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  float ow[KPW], dl[KPW], acc[KPW];
+  double dense[KPW];
+  const bool ys = bitf(brow, ncl) > 0.f;
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = w * KPW + kk;
+    ow[kk] = own[(size_t)ncl * H + k];
+    dl[kk] = D[D_DLT + k];
+    const int m = upper_slot(sv + hsort_tab(b, z, k, NcP), Nc, -ow[kk]);
+    dense[kk] = (double)(Nc - m) * (double)ow[kk] + sx[hsort_tab(b, z, k, NcP + 1) + m];
+    const float zs = ow[kk] + oth[(size_t)ncl * H + k];   // the self pair, as the walk
+    acc[kk] = -relu(ys ? zs + dl[kk] : zs);                // below and the dense part count it
+  }
+  for (int wi = 0; wi < WC; ++wi) {       // y = 1 pairs: relu(z1) replaces relu(z0)
+    uint32_t word = brow[wi];
+    while (word) {
+      const int q = wi * 32 + __builtin_ctz(word);
+      word &= word - 1u;
+#pragma unroll
+      for (int kk = 0; kk < KPW; ++kk) {
+        const float z0 = ow[kk] + oth[(size_t)q * H + w * KPW + kk];
+        acc[kk] += relu(z0 + dl[kk]) - relu(z0);
+      }
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) res[lane * HP + w * KPW + kk] = (float)dense[kk] + acc[kk];
+  __syncthreads();
+  float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
+  float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
+  const float* off = D + (z ? D_T0 : D_S0);
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float sacc = 0.f;
+    for (int l = 0; l < H; ++l) sacc = fmaf(res[n * HP + l], Ml[l * H + k], sacc);
+    gout[(t0 + n) * H + k] = res[n * HP + k];
+    sout[(t0 + n) * H + k] = sacc + off[k];
+  }
+}
+
+// kw_hunk_mlpb_s  grid (tc, B, 2), NT threads: kw_hunk_mlpb's results from the sorted
+// tables.  Row pass (z = 0, node p): D alpha_p = dG_p |S_p| + sum_{q in S_p} dH_q, S_p =
+// {q : beta_q > -alpha_p}; column pass (node q) with alpha's order and dG; then the y = 1
+// pairs' mask changes and ysum = sum y dz, and the self pair removed.
+__global__ __launch_bounds__(NT) void kw_hunk_mlpb_s(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
+    const float* __restrict__ nvec, const float* __restrict__ sv, const double* __restrict__ sw,
+    float* __restrict__ Dal, float* __restrict__ Dbe, float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float res[TN * HP], yres[TN * HP], nt[TN * 4];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5, NcP = (Nc + 3) & ~3;
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
+  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
+  const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
+  const float* woth = (z ? dG : dH) + (size_t)b * Nc * H;
+  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  float ow[KPW], wo[KPW], dl[KPW], acc[KPW], ya[KPW];
+  double dense[KPW];
+  const bool ys = bitf(brow, ncl) > 0.f;
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = w * KPW + kk;
+    ow[kk] = own[(size_t)ncl * H + k];
+    wo[kk] = wown[(size_t)ncl * H + k];
+    dl[kk] = D[D_DLT + k];
+    const int m = upper_slot(sv + hsort_tab(b, z, k, NcP), Nc, -ow[kk]);
+    dense[kk] = (double)(Nc - m) * (double)wo[kk] + sw[hsort_tab(b, z, k, NcP + 1) + m];
+    const float zs = ow[kk] + oth[(size_t)ncl * H + k];          // the self pair
+    const float gs = wo[kk] + woth[(size_t)ncl * H + k];
+    const bool ms = (ys ? zs + dl[kk] : zs) > 0.f;
+    acc[kk] = ms ? -gs : 0.f;
+    ya[kk] = (ms && ys) ? -gs : 0.f;
+  }
+  for (int wi = 0; wi < WC; ++wi) {       // y = 1 pairs: the mask of z1 replaces z0's
+    uint32_t word = brow[wi];
+    while (word) {
+      const int q = wi * 32 + __builtin_ctz(word);
+      word &= word - 1u;
+#pragma unroll
+      for (int kk = 0; kk < KPW; ++kk) {
+        const size_t e = (size_t)q * H + w * KPW + kk;
+        const float z0 = ow[kk] + oth[e];
+        const float g = wo[kk] + woth[e];
+        const float m1 = (z0 + dl[kk]) > 0.f ? g : 0.f;
+        acc[kk] += m1 - (z0 > 0.f ? g : 0.f);
+        ya[kk] += m1;
+      }
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    res[lane * HP + w * KPW + kk] = (float)dense[kk] + acc[kk];
+    yres[lane * HP + w * KPW + kk] = ya[kk];
+  }
+  __syncthreads();
+  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg);
 }
 
 // kw_dn  grid (tc, B): dn_c[m] = sum_k V1[m][k] Dalpha_c[k] + V1[4+m][k] Dbeta_c[k]
@@ -2918,10 +3182,19 @@ struct WideWork {
   size_t gam;                                     // [B][Nc][Nc]
   size_t D;                                       // derived weights
   size_t tab;                                     // f64 scan tables [2][B][H][2][Ne+1]
+  size_t hsv, hsp, hsx, hsw;                      // sorted hunk tables (hunk_sorted)
   size_t part;                                    // partial rows
   Segs segs;
   size_t total;
 };
+
+// the sorted-threshold form of the hunk relu / mask sums (kw_hunk_sort, _fwd_s, _wsum,
+// _mlpb_s) instead of the dense sweeps (kw_hunk_fwd, kw_hunk_mlpb)
+bool hunk_sorted(const hdg_shape* s) {
+  if (s->flags & HDG_FLAG_HUNK_DENSE) return false;
+  if (s->flags & HDG_FLAG_HUNK_SORTED) return true;
+  return s->nc >= HDG_HUNK_SORTED_MIN_NC && false;   // (enabled once parity-checked)
+}
 
 bool has_ent(int v) { return v == 2 || v == 4; }
 bool has_ee(int v) { return v == 4; }
@@ -2954,6 +3227,13 @@ WideWork wide_layout(const hdg_shape* s) {
   w.gam = take(B * Nc * Nc);
   w.D = take(D_WORDS);
   if (has_ent(v) || has_ee(v)) w.tab = take(2 * 2 * B * H * 2 * (Ne + 1));   // doubles
+  if (hunk_sorted(s)) {
+    const size_t NcP = (Nc + 3) & ~(size_t)3;
+    w.hsv = take(B * 2 * H * NcP);
+    w.hsp = take(B * 2 * H * NcP);
+    w.hsx = take(2 * B * 2 * H * (NcP + 1));                    // doubles
+    w.hsw = take(2 * B * 2 * H * (NcP + 1));
+  }
   const int te = (int)((Ne + TN - 1) / TN), tc = (int)((Nc + TN - 1) / TN);
   const int rc = (int)B * tc, re = (int)B * te;
   auto seg = [&](int id, int p0, int n, int rows) {
@@ -3022,7 +3302,7 @@ int launch_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, 
   else
     hipLaunchKernelGGL(kw_ee_fwd<false>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
                        bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_ee_fwd", st));
   return 0;
 }
 
@@ -3056,7 +3336,7 @@ int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
                      bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1),
                      ws + w.D, bpow, no);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_ent_fwd", st));
   unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
   return launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st);
 }
@@ -3076,18 +3356,18 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
                      aT, bt->hid, bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm),
                      F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_ee_clsb", st));
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
                      ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam),
                      F(w.phi), F(w.psi), part, w.segs);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_ee_nodeb", st));
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
                      F(w.psi), (double*)F(w.tab));
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_scan", st));
   hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NTP), sort_lds_bytes(Ne), st, bt->x,
                      bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
                      (const double*)F(w.tab), part, w.segs);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_first_bwd", st));
   // the entity-edge parameters [EE_W11, EC_B2 + 2): one contiguous block of the flat vector
   const int p0 = o.EE_W11, n = o.EC_B2 + 2 - o.EE_W11;
   if (adam) {
@@ -3101,7 +3381,7 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
     hipLaunchKernelGGL(kw_grad_reduce, dim3(n), dim3(64), 0, st, part, w.segs, p0, o.NP,
                        grad + p0);
   }
-  WTRY(hipGetLastError());
+  WTRY(kmark(adam ? "kw_reduce_adam" : "kw_grad_reduce", st));
   return 0;
 }
 
@@ -3125,17 +3405,17 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
   WTRY(launch_prep_maps(s, bt, GP.words, GP.ks, GP.kt, GP.ncst, st));
   hipLaunchKernelGGL(kw_prep_sort, dim3(s->batch), dim3(1024), (size_t)2 * s->ne * 4, st, bt->x,
                      (uint32_t*)bt->prep, s->ne, s->nc);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_prep_sort", st));
   uint32_t* aT = (uint32_t*)bt->prep + (size_t)s->batch * GP.words;
   uint32_t* yT = aT + (size_t)s->batch * s->ne * ((s->ne + 31) / 32);
   hipLaunchKernelGGL(kw_prep_T, dim3(8, s->batch), dim3(NT), 0, st, bt->abits, aT, s->ne);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_prep_T", st));
   hipLaunchKernelGGL(kw_prep_T, dim3(4, s->batch), dim3(NT), 0, st, bt->ybits, yT, s->nc);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_prep_T", st));
   if (has_ent(s->variant)) {   // the entity walks' neighbour lists
     hipLaunchKernelGGL(kw_prep_lists, dim3((s->ne + NW - 1) / NW, s->batch, 2), dim3(NT), 0, st,
                        bt->abits, aT, (uint32_t*)bt->prep, s->ne, s->nc);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_prep_lists", st));
   }
   return 0;
 }
@@ -3237,7 +3517,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   const float* bpow = train && adam ? adam->state->beta_pow : nullptr;
   if (!(ent || ee)) {
     hipLaunchKernelGGL(kw_derive, dim3(1), dim3(NT), 0, st, params, o, Nc, D, bpow);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_derive", st));
   }
   // ---- entity side ----
   if (ent || ee) {   // + kw_derive's work in one more block column, node_fwd_tile per tile
@@ -3246,7 +3526,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st,
                        bt->x, bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P),
                        F(w.R1), F(w.C1), D, bpow, no);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_ent_fwd", st));
   }
   unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
   if (ee) {
@@ -3256,20 +3536,33 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   hipLaunchKernelGGL(kw_cross_fwd, dim3((Nc + NW - 1) / NW, B), dim3(NT), 0, st, prep,
                      ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncpart, ee_fwd_tiles(Ne), F(w.nvec), F(w.alpha),
                      F(w.beta));
-  WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
-                     F(w.alpha), F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_cross_fwd", st));
+  const bool hs = hunk_sorted(s);
+  if (hs) {
+    int np2 = 1;
+    while (np2 < Nc) np2 <<= 1;
+    hipLaunchKernelGGL(kw_hunk_sort, dim3(H, B, 2), dim3(NT), (size_t)8 * np2, st, F(w.alpha),
+                       F(w.beta), Nc, F(w.hsv), (int*)F(w.hsp), (double*)F(w.hsx));
+    WTRY(kmark("kw_hunk_sort", st));
+    hipLaunchKernelGGL(kw_hunk_fwd_s, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+                       F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx), F(w.G),
+                       F(w.Hh), F(w.sig), F(w.tau));
+    WTRY(kmark("kw_hunk_fwd_s", st));
+  } else {
+    hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
+                       F(w.alpha), F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
+    WTRY(kmark("kw_hunk_fwd", st));
+  }
   float* probs = out ? out->probs : nullptr;
   float* logits = out ? out->logits : nullptr;
   if (!train) {
     hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D,
                        Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_hunk_cls", st));
     if (ce_sum) {
       hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, o.NP,
                          ce_sum);
-      WTRY(hipGetLastError());
+      WTRY(kmark("kw_grad_reduce", st));
     }
     if (out && out->ehr) {
       WTRY(launch_ehr(F(w.G), F(w.Hh), (size_t)Nc * H, B, Nc, params, v, out->ehr, st));
@@ -3278,45 +3571,55 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   }
   hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D, Nc,
                      F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_hunk_cls", st));
   hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o, D,
                      Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig), F(w.Dtau),
                      F(w.dG), F(w.dH), part, w.segs);
-  WTRY(hipGetLastError());
-  hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
-                     F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe), part,
-                     w.segs);
-  WTRY(hipGetLastError());
+  WTRY(kmark("kw_hunk_clsb", st));
+  if (hs) {
+    hipLaunchKernelGGL(kw_hunk_wsum, dim3(H, B, 2), dim3(NT), 0, st, (const int*)F(w.hsp),
+                       F(w.dG), F(w.dH), Nc, (double*)F(w.hsw));
+    WTRY(kmark("kw_hunk_wsum", st));
+    hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
+                       F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
+                       (const double*)F(w.hsw), F(w.Dal), F(w.Dbe), part, w.segs);
+    WTRY(kmark("kw_hunk_mlpb_s", st));
+  } else {
+    hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
+                       F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe),
+                       part, w.segs);
+    WTRY(kmark("kw_hunk_mlpb", st));
+  }
   if (ent || ee) {
     hipLaunchKernelGGL(kw_dn, dim3(tc, B), dim3(NT), 0, st, params, o, Nc, F(w.Dal), F(w.Dbe),
                        F(w.dn));
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_dn", st));
   }
   if (ent) {
     hipLaunchKernelGGL(kw_node_bwd, dim3(te, B), dim3(NT), 0, st, prep, bt->x, params, o, Ne, Nc,
                        F(w.dn), F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part, w.segs);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_node_bwd", st));
   }
   if (ee) {
     const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
     hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
                        aT, bt->hid, bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn),
                        F(w.drho), F(w.dgam), part, w.segs);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_ee_clsb", st));
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, D, Ne,
                        ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
                        F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_ee_nodeb", st));
   }
   if (ent || ee) {   // the first-layer backward of both stages: one scan, one launch
     const int mode0 = ent ? 0 : 1, stages = (ent && ee) ? 2 : 1;
     hipLaunchKernelGGL(kw_scan, dim3(H, B, stages), dim3(NT), 0, st, prep, params, o, Ne, Nc,
                        mode0, F(w.rhoE), F(w.psi), (double*)F(w.tab));
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_scan", st));
     hipLaunchKernelGGL(kw_first_bwd, dim3(te, B, stages), dim3(NTP), tlds, st, bt->x, bt->abits,
                        prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi), F(w.psi),
                        (const double*)F(w.tab), part, w.segs);
-    WTRY(hipGetLastError());
+    WTRY(kmark("kw_first_bwd", st));
   }
   if (adam) {
     hdg_state* S = adam->state;
@@ -3328,7 +3631,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_grad_reduce, dim3(o.NP + HDG_TRAILER), dim3(64), 0, st, part, w.segs,
                        0, o.NP, grad);
   }
-  WTRY(hipGetLastError());
+  WTRY(kmark(adam ? "kw_reduce_adam" : "kw_grad_reduce", st));
   return 0;
 }
 

@@ -67,7 +67,8 @@ EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count
            "hdg_debug_step_stamps", "hdg_prep_counts_layout", "hdg_dp_mailbox_bytes",
            "hdg_dp_mailbox_alloc", "hdg_dp_mailbox_open", "hdg_dp_mailbox_close",
            "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce",
-           "hdg_pack_classes", "hdg_crc32c"]
+           "hdg_pack_classes", "hdg_crc32c", "hdg_fwd_bwd_kernel_events",
+           "hdg_bundle_write"]
 
 _lib = None
 
@@ -100,6 +101,8 @@ def load(path=None):
     lib.hdg_pack_classes.argtypes = [vp, i32, i32, vp, vp]
     lib.hdg_fwd_bwd.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp]
     lib.hdg_fwd_bwd_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp, vp]
+    lib.hdg_fwd_bwd_kernel_events.argtypes = [P(Shape), P(Batch), vp, vp, P(Outputs), vp, vp,
+                                              vp, i32, P(ctypes.c_char_p), P(i32)]
     lib.hdg_debug_step_stamps.argtypes = [P(Shape), P(Batch), vp, vp, vp, vp]
     lib.hdg_adam_tf.argtypes = [P(Shape), P(State), vp, f32, vp, vp]
     lib.hdg_train_step.argtypes = [P(Shape), P(Batch), P(State), f32, P(Outputs), vp, vp, vp]
@@ -115,6 +118,8 @@ def load(path=None):
     lib.hdg_dp_allreduce.argtypes = [P(Dp), vp, vp, i32, vp, vp]
     lib.hdg_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
     lib.hdg_crc32c.restype = ctypes.c_uint32
+    lib.hdg_bundle_write.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, ctypes.c_int64, vp,
+                                     ctypes.c_int64, vp, i32, vp, i32]
     for name in EXPORTS:
         getattr(lib, name)
     _lib = lib

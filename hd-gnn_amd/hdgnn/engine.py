@@ -48,10 +48,13 @@ class Engine:
         dev = self.device
         f32 = torch.float32
         self.workspace = torch.zeros(wsb // 4, dtype=f32, device=dev)   # block-pair inboxes start at 0
-        self.params = torch.zeros(self.np, dtype=f32, device=dev)
-        self.m = torch.zeros(self.np, dtype=f32, device=dev)
-        self.v = torch.zeros(self.np, dtype=f32, device=dev)
-        self.beta_pow = torch.tensor([0.9, 0.999], dtype=f32, device=dev)
+        # the training state as one flat buffer [params | adam_m | adam_v | beta_pow]: one
+        # copy snapshots, restores or reads it (the checkpoint's host copy)
+        P = self.np
+        self.state = torch.zeros(3 * P + 2, dtype=f32, device=dev)
+        self.params, self.m, self.v, self.beta_pow = (self.state[:P], self.state[P:2 * P],
+                                                      self.state[2 * P:3 * P], self.state[3 * P:])
+        self.beta_pow.copy_(torch.tensor([0.9, 0.999]))
         self.grad = torch.zeros(self.glen, dtype=f32, device=dev)
         # ce, loss_map, loss_para, train_loss, count parts (3), fault count (hdg_outputs.stats)
         self.stats = torch.zeros(_lib.STATS_LEN, dtype=f32, device=dev)
@@ -138,12 +141,14 @@ class Engine:
                                                                        _lib.FLAG_NO_SPLIT)
 
     def snapshot(self):
-        """Device copies of the training state (parameters, Adam moments, beta powers)."""
-        return [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
+        """A device copy of the training state (parameters, Adam moments, beta powers)."""
+        return self.state.clone()
 
     def restore(self, snap):
-        for t, v in zip((self.params, self.m, self.v, self.beta_pow), snap):
-            t.copy_(v)
+        """Set the training state from a snapshot() (device) or a host copy of self.state."""
+        if isinstance(snap, np.ndarray):
+            snap = torch.from_numpy(np.ascontiguousarray(snap, np.float32))
+        self.state.copy_(snap)
 
     def split_fault_retry(self):
         """After a step whose block-pair exchange timed out (HDG_STATUS_XCH_TIMEOUT; its
@@ -163,7 +168,12 @@ class Engine:
     def train_step_checked(self, dbatch, outputs=True, logits=False, stats=None):
         """train_step that survives a split-mode pair timeout: on a faulted step (read from
         the gradient trailer, identical on every rank) the state is restored and the step
-        re-run with one block per commit.  Synchronises with the device once."""
+        re-run with one block per commit.
+
+        A per-step diagnostic / test helper, not a loop body: it snapshots the whole state
+        and synchronises with the device on every call.  Training loops use the epoch-buffer
+        pattern of graph2graph.train (every step's stats into its own device row, one read
+        per epoch, the retry decided from those rows)."""
         snap = self.snapshot() if self.split else None
         self.train_step(dbatch, outputs, logits, stats)
         fault = float(self.grad[self.np + _lib.TR_FAULT].item())
@@ -297,10 +307,9 @@ class Engine:
         """Capture `steps` consecutive train_step(dbatch) calls (fwd_bwd [+ RCCL all-reduce]
         + Adam each) into one HIP graph; replay() then runs that many training steps with a
         single launch (no per-step graph launch gap).  dbatch must stay alive."""
-        saved = [t.clone() for t in (self.params, self.m, self.v, self.beta_pow)]
+        saved = self.snapshot()
         self.train_step(dbatch, outputs, logits)  # warm: attributes set, RCCL comm built
-        for t, v in zip((self.params, self.m, self.v, self.beta_pow), saved):
-            t.copy_(v)                            # the warm-up step leaves no trace
+        self.restore(saved)                       # the warm-up step leaves no trace
         torch.cuda.synchronize(self.device)
         self._graph_batch = dbatch
         g = torch.cuda.CUDAGraph()

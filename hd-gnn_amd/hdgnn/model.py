@@ -34,6 +34,7 @@ from . import _lib, layout, metrics, tfckpt
 from .data import compact_from_read_data, onehot_relations
 
 HS = 20   # De_e = De_er = h_size compiled into the engine
+FAULT_POLL = 16   # train(): steps between fault polls inside a long epoch
 
 
 def shard_plan(n_commits, mini_batch, world=1, rank=0):
@@ -78,7 +79,8 @@ class Saver(object):
     Adam slots and beta powers so a restore resumes training.  save() keeps the newest
     max_to_keep bundles (TF's default 5) and rewrites the 'checkpoint' state file, as
     Saver.save does; restore() reads a TF-written bundle too (no Adam slots: the
-    optimizer state is then left as it is)."""
+    optimizer state is then left as it is).  The bundle bytes are assembled and written
+    by libhdgnn (tfckpt.BundleTemplate -> hdg_bundle_write) with the GIL released."""
 
     def __init__(self, model, max_to_keep=5):
         self._model = model
@@ -86,21 +88,25 @@ class Saver(object):
         self._last = []              # prefixes saved by this Saver, oldest first
         self._pool = None            # one writer thread: background saves stay in order
         self._pending = []
+        self._tmpl = None
 
     def _host_state(self):
-        """Parameters, Adam moments and beta powers in one device->host copy."""
+        """[params | adam_m | adam_v | beta_pow] in one device->host copy."""
         import torch
         eng = self._model.engine
-        n = eng.params.numel()
-        h = torch.cat([eng.params.detach(), eng.m, eng.v, eng.beta_pow]).cpu().numpy()
-        return h[:n].copy(), h[n:2 * n].copy(), h[2 * n:3 * n].copy(), h[3 * n:].copy()
+        st = getattr(eng, "state", None)
+        if st is None:
+            st = torch.cat([eng.params.detach(), eng.m, eng.v, eng.beta_pow])
+        return st.detach().cpu().numpy().copy()
 
-    def save(self, sess, save_path, global_step=None, background=False):
+    def save(self, sess, save_path, global_step=None, background=False, state=None):
         """background=True: the state is copied to the host now (the bundle holds exactly
         this step's values), the bundle is written by the writer thread while the caller's
-        next steps run; flush() waits for it and re-raises its error."""
+        next steps run; flush() waits for it and re-raises its error.  state: a host copy of
+        the flat training state the caller already holds (graph2graph.train reads it with
+        the epoch's statistics), instead of a fresh device read."""
         prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
-        state = self._host_state()
+        state = self._host_state() if state is None else np.array(state, np.float32)
         if not background:
             self.flush()
             return self._write(prefix, state)
@@ -117,15 +123,18 @@ class Saver(object):
             f.result()
 
     def _write(self, prefix, state):
-        params, m, v, bp = state
+        if self._tmpl is None:
+            self._tmpl = tfckpt.BundleTemplate(self._model.variant)
         d = os.path.dirname(prefix) or "."
-        os.makedirs(d, exist_ok=True)
-        tfckpt.write(prefix, tfckpt.state_tensors(params, self._model.variant, m, v, bp))
+        self._tmpl.write(prefix, state)
         if prefix in self._last:
             self._last.remove(prefix)
         self._last.append(prefix)
         while self.max_to_keep and len(self._last) > self.max_to_keep:
-            tfckpt.remove_bundle(self._last.pop(0))
+            old = self._last.pop(0)
+            for f in (old + ".index", old + ".data-00000-of-00001"):
+                if os.path.exists(f):
+                    os.remove(f)
         tfckpt.write_state_file(d, os.path.basename(prefix),
                                 [os.path.basename(q) for q in self._last
                                  if (os.path.dirname(q) or ".") == d])
@@ -271,10 +280,15 @@ class graph2graph(object):
 
     def train(self, args):
         """model_2.py:335-424.  Every step's pre-update losses and top_ACC count land in its
-        own row of an epoch buffer on the device (hdg_outputs.stats), read once per epoch:
-        no host synchronisation inside the epoch.  A split-mode exchange timeout (the
-        step's update skipped, the fault count in every rank's stats) re-runs the epoch
-        from its starting state with one block per commit (Engine.split_fault_retry)."""
+        own row of an epoch buffer on the device (hdg_outputs.stats); at the epoch's end that
+        buffer and the flat training state go to pinned host memory in two stream-ordered
+        copies.  Epochs are pipelined one deep: epoch i+1 is enqueued before the host waits
+        for epoch i, so epoch i's result line, result file and checkpoint (written by the
+        saver thread through libhdgnn) overlap epoch i+1 on the GPU.  A split-mode exchange
+        timeout (a step's update skipped, the fault count in every rank's stats) re-runs
+        epoch i from the host copy of the state before it, with one block per commit
+        (Engine.split_fault_retry); epochs of more than FAULT_POLL steps poll the fault
+        slots every FAULT_POLL steps and stop a faulted epoch early."""
         import torch
         self._initialize()
         _, _, train, _, maps = self._compact()
@@ -283,32 +297,70 @@ class graph2graph(object):
         counter = 1
         start_time1 = time.time()
         eng = self.engine
-        es = torch.zeros(max(nb, 1), _lib.STATS_LEN, dtype=torch.float32, device=eng.device)
+        S, dev = eng.state.numel(), eng.device
+        th_off = layout.offsets(self.variant)["map_conv/map_theta2:0"][0]
+        nr = max(nb, 1)
+        # device stats rows and pinned host slots per epoch parity; host state slots mod 3
+        # (a retry of epoch i needs the state after i-1 while i+1 is in flight)
+        es = [torch.zeros(nr, _lib.STATS_LEN, dtype=torch.float32, device=dev) for _ in range(2)]
+        hs = [torch.zeros(nr, _lib.STATS_LEN, dtype=torch.float32).pin_memory() for _ in range(2)]
+        hst = [torch.zeros(S, dtype=torch.float32).pin_memory() for _ in range(3)]
+        done = [torch.cuda.Event() for _ in range(2)]
+        hst[2].copy_(eng.state)                          # "after epoch -1": the initial state
+        outs = {}
+
+        def launch(i):
+            """Enqueue epoch i: its steps, then the host copies of its stats and end state."""
+            rows = es[i % 2]
+            for j, db in enumerate(batches):
+                eng.train_step(db, logits=self.fetch_logits, stats=rows[j])
+                if nb > FAULT_POLL and (j + 1) % FAULT_POLL == 0 and j + 1 < nb and \
+                        eng.split and eng.path == _lib.PATH_FUSED and \
+                        bool(rows[:j + 1, 7].any()):     # stop a faulted epoch early
+                    rows[j + 1:].zero_()
+                    rows[j + 1:, 7] = 1.0
+                    break
+            if nb:                                       # fresh tensors: stable attributes
+                outs[i] = (eng.probs.clone(), eng.logits.clone() if self.fetch_logits else None)
+            hs[i % 2].copy_(rows, non_blocking=True)
+            hst[i % 3].copy_(eng.state, non_blocking=True)
+            done[i % 2].record()
+
         self._barrier()
-        for i in range(self.epoch):
-            snap = eng.snapshot() if eng.split and eng.path == _lib.PATH_FUSED else None
-            while True:
-                for j, db in enumerate(batches):
-                    eng.train_step(db, logits=self.fetch_logits, stats=es[j])
-                host = es.cpu().numpy().astype(np.float64)    # the epoch's one synchronisation
-                if host[:nb, 7].any() and snap is not None and eng.split_fault_retry():
-                    eng.restore(snap)
+        if self.epoch > 0:
+            launch(0)
+        i = 0
+        while i < self.epoch:
+            if i + 1 < self.epoch and self.world == 1:
+                launch(i + 1)
+            done[i % 2].synchronize()
+            host = hs[i % 2].numpy().astype(np.float64)
+            if host[:nb, 7].any():                       # a split-mode exchange timed out
+                torch.cuda.synchronize(dev)              # epoch i+1 (if launched) drained
+                if eng.split and eng.path == _lib.PATH_FUSED and eng.split_fault_retry():
+                    eng.restore(hst[(i - 1) % 3].numpy())
+                    outs.pop(i + 1, None)
+                    launch(i)
                     continue
-                break
-            if host[:nb, 7].any() or int(eng.status.item()):
                 eng.check_status()
+                raise RuntimeError("libhdgnn: a training step faulted (stats %s)" % host[:nb])
+            if not np.isfinite(host[:nb, 0]).all():      # a NaN loss: a device fault (DP
+                eng.check_status()                       # timeout) raises, a diverged run
+                                                         # prints nan as the reference would
             tr_loss_Hedge = float(host[:nb, 0].sum())
             tr_loss_map = float(host[:nb, 1].sum())
             correct = sum(int(round(r[4])) + (int(round(r[5])) << 16) + (int(round(r[6])) << 32)
                           for r in host[:nb])
+            state = hst[i % 3].numpy()
             if nb:
                 self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[nb - 1, 0]),
                                                                       float(host[nb - 1, 1]),
                                                                       float(host[nb - 1, 2]))
-                self.C_edge_output2 = eng.probs            # device (B, 2, Ncr), last step
-                self.C_edge_output2_logits = eng.logits if self.fetch_logits else None
+                self.C_edge_output2, self.C_edge_output2_logits = outs.pop(i)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
-            theta = self.theta.reshape([2])
+            # theta (model_2.py:369-371, 392): map_theta2 in the state after epoch i, as
+            # self.theta reads it at this point
+            theta = state[th_off:th_off + 2].astype(np.float32)
             resultString = "Epoch " + str(i + 1) + \
                            " acc: " + str(acc_top)[0:6] + \
                            " Hedge loss: " + str(tr_loss_Hedge / nb if nb else 0.0)[0:6] + \
@@ -322,18 +374,47 @@ class graph2graph(object):
                     f.write(resultString)
                 print(resultString)
             counter += 1
-            self.save(args.checkpoint_dir, counter, background=True)
+            self.save(args.checkpoint_dir, counter, background=True, state=state)
             self._barrier()
+            if self.world > 1 and i + 1 < self.epoch:   # DP: ranks launch in step after the barrier
+                launch(i + 1)
+            i += 1
         self.saver.flush()          # every epoch's bundle on disk before train() returns
         end_time1 = time.time()
         if self.rank == 0:
             print('test time:' + str(end_time1 - start_time1))
 
+    # sess.run's fetched C_edge_output2 / C_edge_output2_logits.  Training keeps the last
+    # step's device output as a fresh tensor per epoch (later steps never change it) and
+    # hands out a host numpy copy on first access, as sess.run returns one.
+    def _fetched(self, key):
+        f = self.__dict__.setdefault("_fetch", {})
+        v = f.get(key)
+        if v is not None and not isinstance(v, np.ndarray):
+            v = f[key] = v.detach().cpu().numpy()
+        return v
+
+    @property
+    def C_edge_output2(self):
+        return self._fetched("probs")
+
+    @C_edge_output2.setter
+    def C_edge_output2(self, v):
+        self.__dict__.setdefault("_fetch", {})["probs"] = v
+
+    @property
+    def C_edge_output2_logits(self):
+        return self._fetched("logits")
+
+    @C_edge_output2_logits.setter
+    def C_edge_output2_logits(self, v):
+        self.__dict__.setdefault("_fetch", {})["logits"] = v
+
     # ------------------------------------------------------------------ checkpoints
     def _model_dir(self, checkpoint_dir):
         return os.path.join(checkpoint_dir, "%s/model_%d/%s" % (self.Repo, self.variant, self.Step))
 
-    def save(self, checkpoint_dir, step, background=False):
+    def save(self, checkpoint_dir, step, background=False, state=None):
         """saver.save(sess, <dir>/g2g.model, global_step=step) (model_2.py:427-437): a TF V2
         bundle g2g.model-<step>.index / .data-00000-of-00001 under the TF variable names
         (hdgnn.tfckpt), plus TF1 Adam's slots and beta powers so training can resume, and
@@ -344,7 +425,7 @@ class graph2graph(object):
         if self.rank != 0:
             return
         self.saver.save(self.sess, os.path.join(self._model_dir(checkpoint_dir), "g2g.model"),
-                        global_step=step, background=background)
+                        global_step=step, background=background, state=state)
 
     def load(self, checkpoint_dir):
         """get_checkpoint_state + saver.restore (model_2.py:439-451).  Reads TF V2 bundles
@@ -395,7 +476,7 @@ class graph2graph(object):
         for db in self._device_batches(test, maps):
             probs, logits, ce_sum = eng.forward(db)
             p = probs.cpu().numpy()
-            self.C_edge_output2_logits = logits
+            self.C_edge_output2_logits = logits.clone()     # not overwritten by later batches
             self.loss_E_HR = self._allsum(float(eng.ehr.item()))
             eng.check_status()
             ce = self._allsum(float(ce_sum.item())) / (self.mini_batch_num * self.Ncr)

@@ -339,7 +339,8 @@ def read_table(data, verify=True):
     return out
 
 
-def _block_bytes(entries, restart_interval=16):
+def _block_bytes(entries, restart_interval=16, vpos=None):
+    """One block's contents; vpos (a list) receives each entry's value offset in it."""
     buf, restarts, prev = bytearray(), [], b""
     for n, (k, v) in enumerate(entries):
         if n % restart_interval == 0:
@@ -351,7 +352,10 @@ def _block_bytes(entries, restart_interval=16):
             while shared < m and prev[shared] == k[shared]:
                 shared += 1
         buf += _put_varint(shared) + _put_varint(len(k) - shared) + _put_varint(len(v))
-        buf += k[shared:] + v
+        buf += k[shared:]
+        if vpos is not None:
+            vpos.append(len(buf))
+        buf += v
         prev = k
     if not restarts:
         restarts = [0]
@@ -361,35 +365,46 @@ def _block_bytes(entries, restart_interval=16):
     return bytes(buf)
 
 
-def write_table(entries, block_size=4096):
-    """Sorted (key, value) pairs -> SSTable image (uncompressed blocks, no filter)."""
+def write_table(entries, block_size=4096, layout=None):
+    """Sorted (key, value) pairs -> SSTable image (uncompressed blocks, no filter).
+    layout (a dict) receives "values": each entry's absolute value offset in the image and
+    "blocks": (offset, length) of every block, in the order their checksums depend on."""
     keys = [k for k, _ in entries]
     if keys != sorted(keys) or len(set(keys)) != len(keys):
         raise CheckpointError("table keys must be unique and sorted")
     out = bytearray()
     index = []
+    values, blocks = [], []
 
-    def emit(contents):
+    def emit(contents, vpos=None):
         off = len(out)
         out.extend(contents)
         tail = b"\x00"
         out.extend(tail + struct.pack("<I", mask_crc(crc32c(contents + tail))))
+        values.extend(off + p for p in (vpos or ()))
+        blocks.append((off, len(contents)))
         return _put_varint(off) + _put_varint(len(contents))
+
+    def data_block(cur):
+        vpos = []
+        return emit(_block_bytes(cur, vpos=vpos), vpos)
 
     cur, size = [], 0
     for k, v in entries:
         cur.append((k, v))
         size += len(k) + len(v) + 8
         if size >= block_size:
-            index.append((cur[-1][0], emit(_block_bytes(cur))))
+            index.append((cur[-1][0], data_block(cur)))
             cur, size = [], 0
     if cur:
-        index.append((cur[-1][0], emit(_block_bytes(cur))))
+        index.append((cur[-1][0], data_block(cur)))
     meta = emit(_block_bytes([]))
     idx = emit(_block_bytes(index, restart_interval=1))
     foot = meta + idx
     foot += b"\x00" * (40 - len(foot)) + struct.pack("<Q", MAGIC)
     out.extend(foot)
+    if layout is not None:
+        layout["values"], layout["blocks"] = values, blocks
     return bytes(out)
 
 
@@ -459,6 +474,64 @@ def write(prefix, tensors):
         f.write(bytes(blob))
     with open(prefix + ".index", "wb") as f:
         f.write(write_table(entries))
+
+
+class BundleTemplate(object):
+    """The byte layout of one model variant's training checkpoint (model variables, TF1 Adam
+    slots, beta powers: every tensor float32, fixed shapes), built once.  write() fills it
+    from the flat engine state [params | adam_m | adam_v | beta_pow] in libhdgnn's
+    hdg_bundle_write: the tensor bytes gathered in name order, each entry's CRC and each
+    index block's trailer CRC patched into the index image, both files written -- native
+    code that runs with the GIL released (ctypes), so the saver thread does not stall the
+    training loop.  Same bytes as write(prefix, state_tensors(...)) (tests/test_tfckpt.py)."""
+
+    def __init__(self, variant, slots=True):
+        sl = _var_slices(variant)
+        P = sum(n for _, _, n, _ in sl)
+        spans = {}
+        for base, o, n, shape in sl:
+            spans[base] = (o, n, shape)
+            if slots:
+                spans[base + "/Adam"] = (P + o, n, shape)
+                spans[base + "/Adam_1"] = (2 * P + o, n, shape)
+        if slots:
+            spans["beta1_power"] = (3 * P, 1, ())
+            spans["beta2_power"] = (3 * P + 1, 1, ())
+        self.n_state = 3 * P + 2 if slots else P
+        names = sorted(spans, key=lambda n: n.encode("utf-8"))
+        gather, entries, offs = [], [(b"", encode_header(1))], []
+        nbytes = 0
+        for n in names:
+            o, cnt, shape = spans[n]
+            gather.extend(range(o, o + cnt))
+            entries.append((n.encode("utf-8"), encode_entry(1, shape, 0, nbytes, 4 * cnt, 0)))
+            offs.append((nbytes, 4 * cnt))
+            nbytes += 4 * cnt
+        lay = {}
+        img = write_table(entries, layout=lay)
+        # entry e's CRC is the last 4 bytes of its value (entry proto field 6, fixed32)
+        ent = [(off, size, vp + len(entries[i + 1][1]) - 4)
+               for i, ((off, size), vp) in enumerate(zip(offs, lay["values"][1:]))]
+        self.gather = np.asarray(gather, np.int32)
+        self.entries = np.asarray(ent, np.int64).reshape(-1, 3)
+        self.blocks = np.asarray(lay["blocks"], np.int64).reshape(-1, 2)
+        self.image = np.frombuffer(img, np.uint8).copy()
+
+    def write(self, prefix, state):
+        from . import _lib
+        state = np.ascontiguousarray(state, np.float32)
+        if state.size != self.n_state:
+            raise CheckpointError("state has %d floats, the template %d" % (state.size, self.n_state))
+        d = os.path.dirname(prefix)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        img = self.image.copy()
+        lib = _lib.load()
+        _lib.check(lib.hdg_bundle_write(
+            _shard_name(prefix, 0, 1).encode(), (prefix + ".index").encode(),
+            state.ctypes.data, self.gather.ctypes.data, self.gather.size, img.ctypes.data,
+            img.size, self.entries.ctypes.data, len(self.entries), self.blocks.ctypes.data,
+            len(self.blocks)))
 
 
 def latest(checkpoint_dir):

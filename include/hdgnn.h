@@ -57,6 +57,14 @@ typedef struct hdg_shape {
  * caller retries with after HDG_STATUS_XCH_TIMEOUT.  Same results up to fp32
  * re-association of the block-pair sums.                                              */
 #define HDG_FLAG_NO_SPLIT 1
+/* General path, hunk pair sums of the first hunk MLP layer (forward relu sums, backward mask
+ * sums): by default from per-unit sorted thresholds (a binary search per node and unit plus
+ * the label pairs one by one) when nc >= 256, a dense sweep of the pair grid below; these
+ * flags force one form (same results up to fp32 re-association; the layout of
+ * hdg_workspace_bytes follows the choice, so keep the flags fixed for a workspace).      */
+#define HDG_FLAG_HUNK_DENSE 2
+#define HDG_FLAG_HUNK_SORTED 4
+#define HDG_HUNK_SORTED_MIN_NC 256
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
  * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge
@@ -178,6 +186,17 @@ int hdg_fwd_bwd_events(const hdg_shape* shape, const hdg_batch* batch, const flo
                        float* grad, hdg_outputs* out, void* workspace, void* stream,
                        void* const* events);
 
+/* hdg_fwd_bwd with per-kernel timing of every engine path (bench.py's roofline): events
+ * [n_events] hipEvent_t; events[0] is recorded on `stream` before the first launch and
+ * events[k + 1] right after the k-th kernel launch, whose name goes to names[k] (static
+ * strings).  *n_kernels = the kernels bracketed (at most n_events - 1; later launches run
+ * untimed).  Replaces nothing in the reference (its only clock is time.time(),
+ * model_2.py:358, 423-424).                                                          */
+int hdg_fwd_bwd_kernel_events(const hdg_shape* shape, const hdg_batch* batch,
+                              const float* params, float* grad, hdg_outputs* out,
+                              void* workspace, void* stream, void* const* events,
+                              int32_t n_events, const char** names, int32_t* n_kernels);
+
 /* Diagnostic: run k_commit_step alone with s_memrealtime (100 MHz) stamps at every
  * phase barrier, stamps[2B][32] (device; row = the block's partial-gradient row, 2b + h
  * in split mode).  Overwrites the workspace.                                        */
@@ -238,6 +257,19 @@ size_t hdg_dp_mailbox_bytes(void);
 /* Host utility: CRC-32C (Castagnoli) of n bytes, continuing from crc (0 to start) -- the
  * record checksum of the TF V2 checkpoint bundles graph2graph.saver writes.          */
 uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc);
+/* Host utility: write one TF V2 checkpoint bundle of float32 tensors from a prebuilt
+ * template (hdgnn.tfckpt.BundleTemplate; replaces the Python encoder of saver.save,
+ * model_2.py:427-437, so the caller's thread runs it without holding the GIL):
+ *   data file  = state[gather[i]] for i < n_floats (the tensors' bytes, sorted by name)
+ *   index file = index_img with each entry's masked CRC-32C of its bytes written at
+ *                entries[3e + 2] (the tensor spans [entries[3e], +entries[3e + 1]) bytes of
+ *                the data file), then each block's trailer CRC (blocks[2b] offset,
+ *                blocks[2b + 1] length; type byte at offset + length) -- index_img is
+ *                modified in place.  0, or HDG_EINVAL (message in hdg_last_error).     */
+int hdg_bundle_write(const char* data_path, const char* index_path, const float* state,
+                     const int32_t* gather, int64_t n_floats, uint8_t* index_img,
+                     int64_t index_len, const int64_t* entries, int32_t n_entries,
+                     const int64_t* blocks, int32_t n_blocks);
 /* allocate + zero this rank's mailbox on the current device; handle: 64 bytes out */
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle);
 /* map a peer's mailbox (its handle) into this process; close / free undo the calls */

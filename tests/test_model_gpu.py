@@ -56,8 +56,26 @@ def test_graph2graph_train_and_test(v, golden_dir, tmp_path, monkeypatch):
             from oracle import layout as olayout
             keys = [k for k, _, _ in olayout.keyed_specs(v)]
             theta = opt.step(theta, np.concatenate([g[k].reshape(-1) for k in keys]))
+            last = (P, sh)
         epoch_theta.append(theta.copy())
     np.testing.assert_allclose(m.engine.get_params(), theta, rtol=0, atol=5e-6)
+
+    # C_edge_output2 = the last step's sess.run fetch (model_2.py:369-371): a host array of
+    # the pre-update probabilities that later steps do not change
+    fetched = m.C_edge_output2
+    assert isinstance(fetched, np.ndarray) and fetched.shape == (mb, 2, nc * (nc - 1))
+    P, sh = last
+    o = model_ref.forward(model_ref.to_torch_params(P, requires_grad=False),
+                          sh.x.astype(np.float64), sh.a, sh.y, sh.hid, sh.nlen, variant=v)
+    np.testing.assert_allclose(fetched, o["probs"].detach().numpy().transpose(0, 2, 1), atol=1e-5)
+    keep = fetched.copy()
+    snap = m.engine.snapshot()
+    db = m._device_batches(train, maps)[0]
+    m.engine.train_step(db)                         # a later step overwrites engine.probs
+    torch.cuda.synchronize()
+    assert not torch.equal(m.engine.probs.cpu(), torch.from_numpy(keep))
+    np.testing.assert_array_equal(m.C_edge_output2, keep)
+    m.engine.restore(snap)                          # the checks below read the trained state
 
     res = tmp_path / "outputSelf" / "tiny" / ("model_%d" % v) / "2" / "result_2.npy"
     lines = res.read_text().splitlines()

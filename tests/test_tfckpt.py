@@ -214,3 +214,25 @@ def test_background_saver_keeps_order_and_state(tmp_path):
             np.testing.assert_array_equal(fl, want[step][0])
             assert np.all(m == want[step][1])
             np.testing.assert_array_equal(bp, np.float32([0.9, 0.999]))
+
+
+def test_native_bundle_template_bytes_equal_python_writer(tmp_path):
+    """tfckpt.BundleTemplate (libhdgnn hdg_bundle_write: the saver thread's GIL-free path)
+    writes the same .index / .data bytes as the Python encoder, for every variant, and the
+    bundle reads back to the state it was given."""
+    for v in (1, 2, 3, 4):
+        P = layout.n_params(v)
+        st = np.random.default_rng(v).standard_normal(3 * P + 2).astype(np.float32)
+        t = tfckpt.BundleTemplate(v)
+        for rep in range(2):                 # the template is reused across saves
+            st = st + np.float32(rep)
+            t.write(str(tmp_path / ("n%d" % v)), st)
+            tfckpt.write(str(tmp_path / ("p%d" % v)),
+                         tfckpt.state_tensors(st[:P], v, st[P:2 * P], st[2 * P:3 * P], st[3 * P:]))
+            for ext in (".index", ".data-00000-of-00001"):
+                assert (tmp_path / ("n%d%s" % (v, ext))).read_bytes() == \
+                    (tmp_path / ("p%d%s" % (v, ext))).read_bytes()
+            fl, m, vv, bp = tfckpt.engine_state(tfckpt.read(str(tmp_path / ("n%d" % v))), v)
+            np.testing.assert_array_equal(np.concatenate([fl, m, vv, bp]), st)
+    with pytest.raises(tfckpt.CheckpointError):
+        tfckpt.BundleTemplate(2).write(str(tmp_path / "bad"), np.zeros(5, np.float32))
