@@ -237,6 +237,9 @@ def main():
                     help="model_<variant>.py (the BASELINE metric is model_2)")
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
+    ap.add_argument("--hunk", default="auto", choices=("auto", "dense", "sorted"),
+                    help="general path's hunk relu / mask sums: the default crossover "
+                         "(include/hdgnn.h HDG_HUNK_SORTED_MIN_NC), or forced dense / sorted")
     ap.add_argument("--edensity", type=float, default=0.05,
                     help="synthetic entity-adjacency density (data-dependence runs)")
     ap.add_argument("--hdensity", type=float, default=0.10,
@@ -269,8 +272,10 @@ def main():
     knobs = {"edensity": args.edensity, "hdensity": args.hdensity, "xkind": args.xkind}
     default_data = knobs == {"edensity": 0.05, "hdensity": 0.10, "xkind": "int10"}
     cb = synth_commits(B, ne, nc, seed_for(1, rank), **knobs)
+    hflags = {"auto": 0, "dense": _lib.FLAG_HUNK_DENSE, "sorted": _lib.FLAG_HUNK_SORTED}[args.hunk]
     eng = Engine(ne, nc, B, variant=v, device=dev, batch_global=B * world, path=args.path,
-                 process_group=torch.distributed.group.WORLD if launched else None)
+                 process_group=torch.distributed.group.WORLD if launched else None,
+                 flags=hflags)
     eng.set_params(layout.init_flat(0, v))
     eng.upload(cb)                               # warm the upload / prepare path once
     torch.cuda.synchronize(dev)
@@ -382,6 +387,7 @@ def main():
                                  "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world,
+                       **({} if args.hunk == "auto" else {"hunk_sums": args.hunk}),
                        **({} if default_data else {"data_knobs": knobs})},
             "roofline": roofline, "cpu_baseline": cpu,
             "dp": {"allreduce": eng.allreduce_kind, "selftest": eng.allreduce_selftest,

@@ -100,6 +100,9 @@ __device__ __forceinline__ void row16_sum5(float* v) {
 #undef HDG_DPP_STEP4
 #undef HDG_DPP_STEP3
 #undef HDG_DPP_STEP
+#ifndef HDG_HOIST   // pair tiles: the columns' B (and MODE 1 wc) operands held in registers
+#define HDG_HOIST 1  // for the whole sweep instead of re-read from LDS every 16-row trip
+#endif
 #ifndef HDG_XROW
 #define HDG_XROW 1
 #endif
@@ -361,6 +364,27 @@ __device__ __forceinline__ void pair_tile(
     dk2[p] = *reinterpret_cast<const p2*>(dl + kpb + 2 * p);
   }
 
+  // loop-invariant column operands (the trip loop's stores to Rout may alias A in general,
+  // so the compiler does not hoist these LDS reads itself; B / wc are not written in the loop)
+  // HDG_HOIST bits: 1 MODE 0's B (M5), 2 MODE 1's wc, 4 MODE 2's B (M8), 8 MODE 1's B (M10)
+  constexpr bool HB = (MODE == 0 && (HDG_HOIST & 1)) || (MODE == 2 && (HDG_HOIST & 4)) ||
+                      (MODE == 1 && (HDG_HOIST & 8));
+  constexpr bool HW = (HDG_HOIST & 2) && MODE == 1;
+  p2 bcol[HB ? SMAX : 1][KP > 0 ? KP : 1], wcol[HW ? SMAX : 1][KP > 0 ? KP : 1];
+  float bcolt[HB ? SMAX : 1], wcolt[HW ? SMAX : 1];
+  if constexpr (HB || HW) {
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) {
+      const int j = tj + 16 * c;
+#pragma unroll
+      for (int p = 0; p < KP; ++p) {
+        if constexpr (HB) bcol[c][p] = *reinterpret_cast<const p2*>(Bv + j * LD + kpb + 2 * p);
+        if constexpr (HW) wcol[c][p] = *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
+      }
+      if constexpr (HB) bcolt[c] = KT ? Bv[j * LD + ktl] : 0.f;
+      if constexpr (HW) wcolt[c] = KT ? wc[j * LD + ktl] : 0.f;
+    }
+  }
   for (int s = 0; s < S; ++s) {
     if (wrow + 16 * s >= nown) continue;    // wave-uniform: no row of this wave in the trip
     const int r = ti + 16 * s;
@@ -409,7 +433,9 @@ __device__ __forceinline__ void pair_tile(
       const float* Bj = Bv + j * LD;
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
-        const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
+        p2 bb;
+        if constexpr (HB) bb = bcol[c][p];
+        else bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
         if constexpr (MODE == 0) {
           // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
@@ -420,7 +446,8 @@ __device__ __forceinline__ void pair_tile(
         } else {
           p2 w;
           if constexpr (MODE == 1) {
-            w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
+            if constexpr (HW) w = rw2[p] + wcol[c][p];
+            else w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
           } else {
             w = (p2){g, g};
           }
@@ -431,12 +458,12 @@ __device__ __forceinline__ void pair_tile(
         }
       }
       if constexpr (KT) {
-        const float z = at + fmaf(af, dkt, Bj[ktl]);
+        const float z = at + fmaf(af, dkt, HB ? bcolt[c] : Bj[ktl]);
         float e;
         if constexpr (MODE == 0) {
           e = reluf(z);
         } else {
-          const float w = (MODE == 1) ? (rwt + wc[j * LD + ktl]) : g;
+          const float w = (MODE == 1) ? (rwt + (HW ? wcolt[c] : wc[j * LD + ktl])) : g;
           e = (z > 0.f) ? w : 0.f;
           yacct = fmaf(af, e, yacct);
         }

@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hdgnn.h"
@@ -338,6 +339,18 @@ __host__ __device__ inline ListLayout list_layout(int B, int Ne, int Nc) {
   L.ids = L.cnt + ((2 * (size_t)B * Ne + 3) & ~(size_t)3);
   L.end = L.ids + (size_t)B * Ne * list_stride(Ne);     // 2 sides x LS/2 words
   return L;
+}
+
+// label id lists (kw_prep_lists on y, the sorted hunk passes' walks): counts u32 [2][B][Nc]
+// (side 0: row p of y, 1: column q), ids u16 [2][B][Nc][LSc] ascending, padded to a
+// multiple of 4 with the sentinel Nc; after the entity lists (model_2 / model_4) or yT
+__host__ __device__ inline ListLayout ylist_layout(int B, int Ne, int Nc, bool ent) {
+  const ListLayout L = list_layout(B, Ne, Nc);
+  ListLayout Y;
+  Y.cnt = ((ent ? L.end : L.cnt) + 3) & ~(size_t)3;
+  Y.ids = Y.cnt + ((2 * (size_t)B * Nc + 3) & ~(size_t)3);
+  Y.end = Y.ids + (size_t)B * Nc * list_stride(Nc);
+  return Y;
 }
 
 // per-block partial gradient rows: segment s holds n consecutive parameters starting at
@@ -1610,7 +1623,7 @@ __device__ __forceinline__ void mlpb_epilogue(int z, int b, int t0, int tc, int 
                                               const float* __restrict__ nvec, float* res,
                                               float* yres, float* nt, float* __restrict__ Dal,
                                               float* __restrict__ Dbe, float* __restrict__ part,
-                                              const Segs& sg) {
+                                              const Segs& sg, int tile) {
   float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H;
   for (int e = threadIdx.x; e < TN * H; e += blockDim.x) {
     const int n = e / H, k = e - n * H;
@@ -1621,7 +1634,7 @@ __device__ __forceinline__ void mlpb_epilogue(int z, int b, int t0, int tc, int 
   for (int e = threadIdx.x; e < TN * 4; e += blockDim.x)
     nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
   __syncthreads();
-  const int row = (b * tc + blockIdx.x) * 2 + z;
+  const int row = (b * tc + tile) * 2 + z;
   const Seg& s = sg.s[SG_MLPB];
   for (int e = threadIdx.x; e < 11 * H; e += blockDim.x) {   // rows 0..9 of V1, then c1
     const int l = e / H, k = e - l * H;
@@ -1719,7 +1732,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
   }
   combine8(acc, buf, res);
   if (z == 0) combine8(ya, buf, yres);
-  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg);
+  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1745,103 +1758,243 @@ __host__ __device__ inline size_t hsort_tab(int b, int side, int k, int len) {
 }
 
 // kw_hunk_sort  grid (H, B, 2), NT threads, dynamic LDS 8 * pow2(Nc) bytes: bitonic sort
-// of (value, node) keys (ties by node: a fixed order, so every table is deterministic),
-// then f64 suffix sums of the values
+// of 64-bit keys (order-preserving bits of the value, node index below: ties by node, so
+// every table is deterministic), then f64 suffix sums of the values
+__device__ __forceinline__ uint32_t fkey(float v) {   // monotone float -> u32 (no NaN here)
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// inclusive f64 sum over the block's threads in thread order (NT threads): each thread
+// gets the sum of the chunks of the threads before it ("above" its own slots)
+__device__ __forceinline__ double block_excl(double a, double* cs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double inc = a;
+#pragma unroll
+  for (int o2 = 1; o2 < 64; o2 <<= 1) {
+    const double u = __shfl_up(inc, o2);
+    if (lane >= o2) inc += u;
+  }
+  if (lane == 63) cs[w] = inc;
+  __syncthreads();
+  double base = 0.0;
+  for (int u = 0; u < w; ++u) base += cs[u];
+  return base + (inc - a);
+}
+
+// One wave per table: the Nc keys (padded to NP2 = 64 E with max keys) held E per lane,
+// element e = 64 i + lane in register i.  Bitonic network: partners at distance >= 64 are
+// registers of the same lane, below 64 lanes of the same register (shuffles).
+// the value of lane ^ ST (ST < 64) without the LDS crossbar where the VALU can: permlane
+// swaps for 32 / 16, DPP for 8 (row_ror:8 = lane ^ 8 in a 16-lane row), 2, 1 (quad_perm);
+// ds_swizzle (xor mode) for 4
+template <int ST>
+__device__ __forceinline__ uint32_t xlane(uint32_t v, int lane) {
+  if constexpr (ST == 32 || ST == 16) {
+    float x = __uint_as_float(v), y = x;
+    if constexpr (ST == 32) {
+      swap32(x, y);
+      return __float_as_uint((lane & 32) ? x : y);
+    } else {
+      swap16(x, y);
+      return __float_as_uint((lane & 16) ? x : y);
+    }
+  } else if constexpr (ST == 8) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (ST == 4) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1F);
+  } else if constexpr (ST == 2) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  } else {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  }
+}
+template <int ST>
+__device__ __forceinline__ unsigned long long xlane64(unsigned long long v, int lane) {
+  const uint32_t lo = xlane<ST>((uint32_t)v, lane), hi = xlane<ST>((uint32_t)(v >> 32), lane);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int ST, int LEN, int E>
+__device__ __forceinline__ void bitonic_xstage(unsigned long long (&k)[E], int lane) {
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = 64 * i + lane;
+    const bool up = (e & LEN) == 0;
+    const unsigned long long o = xlane64<ST>(k[i], lane);
+    const bool lower = (lane & ST) == 0;          // this lane holds the lower slot
+    const bool keep_min = lower == up;
+    const bool lt = k[i] < o;
+    k[i] = (lt == keep_min) ? k[i] : o;
+  }
+}
+
+template <int LEN, int E>
+__device__ __forceinline__ void bitonic_xstages(unsigned long long (&k)[E], int lane) {
+  // the cross-lane distances of one merge level, highest first
+  if constexpr (LEN > 32) bitonic_xstage<32, LEN, E>(k, lane);
+  if constexpr (LEN > 16) bitonic_xstage<16, LEN, E>(k, lane);
+  if constexpr (LEN > 8) bitonic_xstage<8, LEN, E>(k, lane);
+  if constexpr (LEN > 4) bitonic_xstage<4, LEN, E>(k, lane);
+  if constexpr (LEN > 2) bitonic_xstage<2, LEN, E>(k, lane);
+  bitonic_xstage<1, LEN, E>(k, lane);
+}
+
+template <int LEN, int E>
+__device__ __forceinline__ void bitonic_level(unsigned long long (&k)[E], int lane) {
+  // register distances (>= 64) first, then the lane distances
+#pragma unroll
+  for (int st = LEN >> 1; st >= 64; st >>= 1) {
+    const int rs = st >> 6;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (i & rs) continue;
+      const int e = 64 * i + lane;
+      const bool up = (e & LEN) == 0;
+      const unsigned long long a = k[i], c = k[i + rs];
+      const bool sw = (a > c) == up;
+      k[i] = sw ? c : a;
+      k[i + rs] = sw ? a : c;
+    }
+  }
+  bitonic_xstages<LEN, E>(k, lane);
+}
+
+template <int LEN, int E>
+__device__ __forceinline__ void bitonic_from(unsigned long long (&k)[E], int lane) {
+  bitonic_level<LEN, E>(k, lane);
+  if constexpr (LEN < 64 * E) bitonic_from<2 * LEN, E>(k, lane);
+}
+
+template <int E>
+__device__ __forceinline__ void wave_bitonic(unsigned long long (&k)[E], int lane) {
+  bitonic_from<2, E>(k, lane);
+}
+
+template <int E>
+__device__ __forceinline__ void wave_bitonic_shfl(unsigned long long (&k)[E], int lane) {
+  constexpr int N = 64 * E;
+#pragma unroll
+  for (int len = 2; len <= N; len <<= 1) {
+#pragma unroll
+    for (int st = len >> 1; st > 0; st >>= 1) {
+      if (st >= 64) {
+        const int rs = st >> 6;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          if (i & rs) continue;
+          const int e = 64 * i + lane;
+          const bool up = (e & len) == 0;
+          const unsigned long long a = k[i], c = k[i + rs];
+          const bool sw = (a > c) == up;
+          k[i] = sw ? c : a;
+          k[i + rs] = sw ? a : c;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          const int e = 64 * i + lane;
+          const bool up = (e & len) == 0;
+          const unsigned long long o = __shfl_xor(k[i], st);
+          const bool lower = (lane & st) == 0;       // this lane holds the lower slot
+          const unsigned long long mn = k[i] < o ? k[i] : o, mx = k[i] < o ? o : k[i];
+          k[i] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+}
+
+// suffix sums over the wave's strided elements (e = 64 i + lane): out(e, sum_{r >= e} v_r),
+// register i from the top with the higher registers' total carried in
+template <int E, class V, class O>
+__device__ __forceinline__ void wave_suffix(int lane, int n, V val, O out) {
+  double carry = 0.0;
+#pragma unroll
+  for (int i = E - 1; i >= 0; --i) {
+    const int e = 64 * i + lane;
+    double v = e < n ? val(i) : 0.0;
+#pragma unroll
+    for (int o2 = 1; o2 < 64; o2 <<= 1) {
+      const double u = __shfl_down(v, o2);
+      if (lane + o2 < 64) v += u;
+    }
+    v += carry;
+    if (e < n) out(e, v);
+    carry = __shfl(v, 0);
+  }
+}
+
+template <int E>
 __global__ __launch_bounds__(NT) void kw_hunk_sort(const float* __restrict__ alpha,
                                                    const float* __restrict__ beta, int Nc,
                                                    float* __restrict__ sv, int* __restrict__ sp,
                                                    double* __restrict__ sx) {
-  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
-  __shared__ double cs[NW];
-  const int k = blockIdx.x, b = blockIdx.y, side = blockIdx.z, t = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * NW + uni(threadIdx.x >> 6), b = blockIdx.y, side = blockIdx.z;
+  if (k >= H) return;                             // wave-uniform, no barriers
   const int NcP = (Nc + 3) & ~3;
-  int NP2 = 1;
-  while (NP2 < Nc) NP2 <<= 1;
-  float* kv = hs_lds;
-  int* ki = reinterpret_cast<int*>(hs_lds + NP2);
-  const float* src = (side ? alpha : beta) + (size_t)b * Nc * H;
-  for (int e = t; e < NP2; e += NT) {
-    kv[e] = e < Nc ? src[(size_t)e * H + k] : __builtin_inff();
-    ki[e] = e;
+  const float* src = (side ? alpha : beta) + (size_t)b * Nc * H + k;
+  unsigned long long key[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = 64 * i + lane;
+    const uint32_t kv = e < Nc ? fkey(src[(size_t)(e < Nc ? e : 0) * H]) : 0xffffffffu;
+    key[i] = ((unsigned long long)kv << 32) | (uint32_t)e;
   }
-  __syncthreads();
-  for (int len = 2; len <= NP2; len <<= 1) {
-    for (int st = len >> 1; st > 0; st >>= 1) {
-      for (int e = t; e < NP2 / 2; e += NT) {
-        const int lo = ((e / st) * 2 * st) + (e % st), hi = lo + st;
-        const bool up = (lo & len) == 0;
-        const float a = kv[lo], c = kv[hi];
-        const int ia = ki[lo], ic = ki[hi];
-        const bool gt = a > c || (a == c && ia > ic);
-        if (gt == up) {
-          kv[lo] = c; kv[hi] = a;
-          ki[lo] = ic; ki[hi] = ia;
-        }
-      }
-      __syncthreads();
+  wave_bitonic<E>(key, lane);
+  const size_t tb = hsort_tab(b, side, k, NcP), tx = hsort_tab(b, side, k, NcP + 1);
+  float val[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = 64 * i + lane;
+    val[i] = fkey_inv((uint32_t)(key[i] >> 32));
+    if (e < Nc) {
+      sv[tb + e] = val[i];
+      sp[tb + e] = (int)(key[i] & 0xffffffffu);
     }
   }
-  const size_t tb = hsort_tab(b, side, k, NcP), tx = hsort_tab(b, side, k, NcP + 1);
-  for (int e = t; e < Nc; e += NT) {
-    sv[tb + e] = kv[e];
-    sp[tb + e] = ki[e];
-  }
-  // suffix sums: thread t owns slots [t C, t C + C) in reverse order
-  const int C = (Nc + NT - 1) / NT;
-  const int r1 = Nc - t * C, r0 = r1 - C > 0 ? r1 - C : 0;   // slots [r0, r1), high first
-  double a = 0.0;
-  for (int r = r1 - 1; r >= r0; --r) a += (double)kv[r];
-  const int lane = t & 63, w = t >> 6;
-  double inc = a;
-#pragma unroll
-  for (int o2 = 1; o2 < 64; o2 <<= 1) {
-    const double u = __shfl_up(inc, o2);
-    if (lane >= o2) inc += u;
-  }
-  if (lane == 63) cs[w] = inc;
-  __syncthreads();
-  double base = 0.0;
-  for (int u = 0; u < w; ++u) base += cs[u];
-  double run = base + (inc - a);           // sum of the slots above this thread's chunk
-  if (t == 0) sx[tx + Nc] = 0.0;
-  for (int r = r1 - 1; r >= r0; --r) {
-    run += (double)kv[r];
-    sx[tx + r] = run;
-  }
+  if (lane == 0) sx[tx + Nc] = 0.0;
+  wave_suffix<E>(lane, Nc, [&](int i) { return (double)val[i]; },
+                 [&](int e, double v) { sx[tx + e] = v; });
 }
 
-// kw_hunk_wsum  grid (H, B, 2): sw[m] = sum_{r >= m} w[sp[r]][k], side 0: w = dH, 1: dG
+// kw_hunk_wsum  grid (H / 4, B, 2), one wave per table: sw[m] = sum_{r >= m} w[sp[r]][k],
+// side 0: w = dH, 1: dG
+template <int E>
 __global__ __launch_bounds__(NT) void kw_hunk_wsum(const int* __restrict__ sp,
                                                    const float* __restrict__ dG,
                                                    const float* __restrict__ dH, int Nc,
                                                    double* __restrict__ sw) {
-  __shared__ double cs[NW];
-  const int k = blockIdx.x, b = blockIdx.y, side = blockIdx.z, t = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * NW + uni(threadIdx.x >> 6), b = blockIdx.y, side = blockIdx.z;
+  if (k >= H) return;
   const int NcP = (Nc + 3) & ~3;
-  const float* wv = (side ? dG : dH) + (size_t)b * Nc * H;
+  const float* wv = (side ? dG : dH) + (size_t)b * Nc * H + k;
   const int* pm = sp + hsort_tab(b, side, k, NcP);
   double* T = sw + hsort_tab(b, side, k, NcP + 1);
-  const int C = (Nc + NT - 1) / NT;
-  const int r1 = Nc - t * C, r0 = r1 - C > 0 ? r1 - C : 0;
-  double a = 0.0;
-  for (int r = r1 - 1; r >= r0; --r) a += (double)wv[(size_t)pm[r] * H + k];
-  const int lane = t & 63, w = t >> 6;
-  double inc = a;
+  float v[E];
+  int id[E];
 #pragma unroll
-  for (int o2 = 1; o2 < 64; o2 <<= 1) {
-    const double u = __shfl_up(inc, o2);
-    if (lane >= o2) inc += u;
+  for (int i = 0; i < E; ++i) {
+    const int e = 64 * i + lane;
+    id[i] = pm[e < Nc ? e : 0];
   }
-  if (lane == 63) cs[w] = inc;
-  __syncthreads();
-  double base = 0.0;
-  for (int u = 0; u < w; ++u) base += cs[u];
-  double run = base + (inc - a);
-  if (t == 0) T[Nc] = 0.0;
-  for (int r = r1 - 1; r >= r0; --r) {
-    run += (double)wv[(size_t)pm[r] * H + k];
-    T[r] = run;
-  }
+#pragma unroll
+  for (int i = 0; i < E; ++i) v[i] = wv[(size_t)id[i] * H];
+  if (lane == 0) T[Nc] = 0.0;
+  wave_suffix<E>(lane, Nc, [&](int i) { return (double)v[i]; },
+                 [&](int e, double x) { T[e] = x; });
+}
+
+// E = elements per lane of the one-wave sort: pow2(Nc) / 64, at least 2
+inline int hsort_e(int Nc) {
+  int e = 2;
+  while (64 * e < Nc) e <<= 1;
+  return e;
 }
 
 // first slot m with sv[m] > thr (Nc if none): sv ascending
@@ -1852,57 +2005,163 @@ __device__ __forceinline__ int upper_slot(const float* __restrict__ sv, int Nc, 
   return m;
 }
 
-// kw_hunk_fwd_s  grid (tc, B, 2), NT threads: kw_hunk_fwd's results (G / H, sigma / tau)
-// from the sorted tables.  Lane = node of the tile, wave w = units [5w, 5w + 5).
-__global__ __launch_bounds__(NT) void kw_hunk_fwd_s(
-    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
-    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
-    const float* __restrict__ beta, const float* __restrict__ sv, const double* __restrict__ sx,
-    float* __restrict__ G, float* __restrict__ Hh, float* __restrict__ sig,
-    float* __restrict__ tau) {
-#pragma clang fp contract(off)
-  __shared__ float res[TN * HP];
-  __shared__ float Ml[H * H];
-  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
-  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
-  const int WC = (Nc + 31) >> 5, NcP = (Nc + 3) & ~3;
-  stage_w(Ml, D + D_M, H * H);
-  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
-  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
-  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
-  float ow[KPW], dl[KPW], acc[KPW];
-  double dense[KPW];
-  const bool ys = bitf(brow, ncl) > 0.f;
+// The sorted passes run 8 waves over 128 nodes (two 64-node halves); wave w takes half
+// w >> 2 and hidden units [5 (w & 3), +5).  With STAGE (Nc <= HS_STAGE_MAX) the block stages
+// the sorted values of all 20 units and the swept side's node vectors (and weights) in LDS
+// (16-byte copies, every load of a thread issued before its first LDS store): the binary
+// searches and the label walks then wait on LDS, not on one dependent L2 round trip per step
+// / pair.  The walks read the node's label id list (ylist_layout) four ids per 8-byte load.
+constexpr int HSN = 128;                  // nodes per block
+constexpr int HS_STAGE_MAX = 512;
+__host__ __device__ inline size_t hs_lds_bytes(int Nc, int nvec) {   // nvec: 1 (fwd) / 2 (mlpb)
+  const size_t NcP = (Nc + 3) & ~3;
+  return ((size_t)H * NcP + (size_t)H * Nc * nvec) * 4;
+}
+
+struct HsView {
+  const float* sv;      // [H][svs]: the sorted values (LDS or the global tables)
+  int svs;
+  const float* oth;     // [Nc][H]
+  const float* woth;    // [Nc][H] (mlpb)
+};
+
+// copy n16 16-byte words src -> dst with every load of the thread in flight first
+template <int U>
+__device__ __forceinline__ void copy16(float4* __restrict__ dst, const float4* __restrict__ src,
+                                       int n16) {
+  for (int e0 = threadIdx.x; e0 < n16; e0 += U * blockDim.x) {
+    float4 v[U];
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    const int k = w * KPW + kk;
-    ow[kk] = own[(size_t)ncl * H + k];
-    dl[kk] = D[D_DLT + k];
-    const int m = upper_slot(sv + hsort_tab(b, z, k, NcP), Nc, -ow[kk]);
-    dense[kk] = (double)(Nc - m) * (double)ow[kk] + sx[hsort_tab(b, z, k, NcP + 1) + m];
-    const float zs = ow[kk] + oth[(size_t)ncl * H + k];   // the self pair, as the walk
-    acc[kk] = -relu(ys ? zs + dl[kk] : zs);                // below and the dense part count it
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x;
+      v[u] = src[e < n16 ? e : e0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x;
+      if (e < n16) dst[e] = v[u];
+    }
   }
-  for (int wi = 0; wi < WC; ++wi) {       // y = 1 pairs: relu(z1) replaces relu(z0)
-    uint32_t word = brow[wi];
-    while (word) {
-      const int q = wi * 32 + __builtin_ctz(word);
-      word &= word - 1u;
+}
+
+template <bool STAGE>
+__device__ __forceinline__ HsView hs_stage(int z, int b, int Nc, const float* sv_g,
+                                           const float* oth_g, const float* woth_g, void* lds) {
+  const int NcP = (Nc + 3) & ~3;
+  HsView v;
+  const float* svb = sv_g + hsort_tab(b, z, 0, NcP);       // the 20 tables, contiguous
+  if constexpr (STAGE) {
+    float* svl = reinterpret_cast<float*>(lds);
+    float* ol = svl + (size_t)H * NcP;
+    float* wl = ol + (size_t)H * Nc;
+    copy16<6>(reinterpret_cast<float4*>(svl), reinterpret_cast<const float4*>(svb), H * NcP / 4);
+    copy16<6>(reinterpret_cast<float4*>(ol), reinterpret_cast<const float4*>(oth_g), H * Nc / 4);
+    if (woth_g)
+      copy16<6>(reinterpret_cast<float4*>(wl), reinterpret_cast<const float4*>(woth_g),
+                H * Nc / 4);
+    __syncthreads();
+    v.sv = svl;
+    v.oth = ol;
+    v.woth = wl;
+  } else {
+    v.sv = svb;
+    v.oth = oth_g;
+    v.woth = woth_g;
+  }
+  v.svs = NcP;
+  return v;
+}
+
+// node r's label ids (ylist_layout): f(id, valid) for each, the sentinel padding invalid;
+// LB groups of four ids loaded before any is used
+template <int LB = 2, class F>
+__device__ __forceinline__ void for_ylist(const uint32_t* __restrict__ prep, const ListLayout& Y,
+                                          size_t r, int Nc, F f) {
+  const int ng = ((int)prep[Y.cnt + r] + 3) >> 2;
+  const uint2* ids = reinterpret_cast<const uint2*>(
+      reinterpret_cast<const uint16_t*>(prep + Y.ids) + r * list_stride(Nc));
+  for (int g0 = 0; g0 < ng; g0 += LB) {
+    uint2 q[LB];
 #pragma unroll
-      for (int kk = 0; kk < KPW; ++kk) {
-        const float z0 = ow[kk] + oth[(size_t)q * H + w * KPW + kk];
-        acc[kk] += relu(z0 + dl[kk]) - relu(z0);
+    for (int u = 0; u < LB; ++u) q[u] = ids[g0 + u < ng ? g0 + u : g0];
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      if (g0 + u < ng) {
+        const int i0 = (int)(q[u].x & 0xffffu), i1 = (int)(q[u].x >> 16);
+        const int i2 = (int)(q[u].y & 0xffffu), i3 = (int)(q[u].y >> 16);
+        f(i0 < Nc ? i0 : Nc - 1, i0 < Nc);
+        f(i1 < Nc ? i1 : Nc - 1, i1 < Nc);
+        f(i2 < Nc ? i2 : Nc - 1, i2 < Nc);
+        f(i3 < Nc ? i3 : Nc - 1, i3 < Nc);
       }
     }
   }
+}
+
+// kw_hunk_fwd_s  grid (ceil(Nc / 128), B, 2), NTP threads: kw_hunk_fwd's results (G / H,
+// sigma / tau) from the sorted tables
+template <bool STAGE>
+__global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ sv, const double* __restrict__ sx,
+    const uint32_t* __restrict__ prep, ListLayout Y, float* __restrict__ G,
+    float* __restrict__ Hh, float* __restrict__ sig, float* __restrict__ tau) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
+  __shared__ float res[HSN * HP];
+  __shared__ float Ml[H * H];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * HSN, B = gridDim.y;
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
+  const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  stage_w(Ml, D + D_M, H * H);
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
+  const HsView V = hs_stage<STAGE>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
+                                   nullptr, hs_lds);
+  float ow[KPW], dl[KPW], acc[KPW];
+  int m[KPW];
+  const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) res[lane * HP + w * KPW + kk] = (float)dense[kk] + acc[kk];
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    ow[kk] = own[(size_t)ncl * H + k];
+    dl[kk] = D[D_DLT + k];
+    m[kk] = 0;
+  }
+  // the five binary searches interleaved (independent LDS chains)
+  for (int st = top_pow2(Nc); st > 0; st >>= 1) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int c = m[kk] + st - 1;
+      if (c < Nc && !(V.sv[(g * KPW + kk) * V.svs + c] > -ow[kk])) m[kk] += st;
+    }
+  }
+  double dense[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    dense[kk] = (double)(Nc - m[kk]) * (double)ow[kk] + sx[hsort_tab(b, z, k, ((Nc + 3) & ~3) + 1) + m[kk]];
+    const float zs = ow[kk] + V.oth[(size_t)ncl * H + k];   // the self pair, as the walk
+    acc[kk] = -relu(ys ? zs + dl[kk] : zs);                  // and the dense part count it
+  }
+  // y = 1 pairs: relu(z1) replaces relu(z0) (the sentinel ids: a zero term)
+  for_ylist(prep, Y, ((size_t)z * B + b) * Nc + ncl, Nc, [&](int q, bool ok) {
+    const float* oq = V.oth + (size_t)q * H + g * KPW;
+    const float vm = ok ? 1.f : 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = ow[kk] + oq[kk];
+      acc[kk] += vm * (relu(z0 + dl[kk]) - relu(z0));
+    }
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) res[nl * HP + g * KPW + kk] = (float)dense[kk] + acc[kk];
   __syncthreads();
   float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
   float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
   const float* off = D + (z ? D_T0 : D_S0);
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
+  for (int e = threadIdx.x; e < HSN * H; e += NTP) {
     const int n = e / H, k = e - n * H;
     if (t0 + n >= Nc) continue;
     float sacc = 0.f;
@@ -1912,67 +2171,85 @@ __global__ __launch_bounds__(NT) void kw_hunk_fwd_s(
   }
 }
 
-// kw_hunk_mlpb_s  grid (tc, B, 2), NT threads: kw_hunk_mlpb's results from the sorted
-// tables.  Row pass (z = 0, node p): D alpha_p = dG_p |S_p| + sum_{q in S_p} dH_q, S_p =
-// {q : beta_q > -alpha_p}; column pass (node q) with alpha's order and dG; then the y = 1
-// pairs' mask changes and ysum = sum y dz, and the self pair removed.
-__global__ __launch_bounds__(NT) void kw_hunk_mlpb_s(
+// kw_hunk_mlpb_s  grid (ceil(Nc / 128), B, 2), NTP threads: kw_hunk_mlpb's results from the
+// sorted tables.  Row pass (z = 0, node p): D alpha_p = dG_p |S_p| + sum_{q in S_p} dH_q with
+// S_p = {q : beta_q > -alpha_p}; the column pass (node q) with alpha's order and dG; then
+// the y = 1 pairs' mask changes, ysum = sum y dz, and the self pair removed.  The epilogue
+// (partial gradient rows) per 64-node half, as kw_hunk_mlpb's tiles write them.
+template <bool STAGE>
+__global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
     const float* __restrict__ nvec, const float* __restrict__ sv, const double* __restrict__ sw,
-    float* __restrict__ Dal, float* __restrict__ Dbe, float* __restrict__ part, Segs sg) {
+    const uint32_t* __restrict__ prep, ListLayout Y, float* __restrict__ Dal,
+    float* __restrict__ Dbe, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ float res[TN * HP], yres[TN * HP], nt[TN * 4];
-  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
-  const int nd = t0 + lane, ncl = nd < Nc ? nd : Nc - 1;
-  const int WC = (Nc + 31) >> 5, NcP = (Nc + 3) & ~3;
+  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
+  __shared__ float res[HSN * HP], yres[HSN * HP], nt[TN * 4];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * HSN, B = gridDim.y;
+  const int tc = (Nc + TN - 1) / TN;
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
+  const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
-  const float* oth = (z ? alpha : beta) + (size_t)b * Nc * H;
   const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
-  const float* woth = (z ? dG : dH) + (size_t)b * Nc * H;
-  const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
+  const HsView V = hs_stage<STAGE>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
+                                   (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
+  const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
   float ow[KPW], wo[KPW], dl[KPW], acc[KPW], ya[KPW];
-  double dense[KPW];
-  const bool ys = bitf(brow, ncl) > 0.f;
+  int m[KPW];
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
-    const int k = w * KPW + kk;
+    const int k = g * KPW + kk;
     ow[kk] = own[(size_t)ncl * H + k];
     wo[kk] = wown[(size_t)ncl * H + k];
     dl[kk] = D[D_DLT + k];
-    const int m = upper_slot(sv + hsort_tab(b, z, k, NcP), Nc, -ow[kk]);
-    dense[kk] = (double)(Nc - m) * (double)wo[kk] + sw[hsort_tab(b, z, k, NcP + 1) + m];
-    const float zs = ow[kk] + oth[(size_t)ncl * H + k];          // the self pair
-    const float gs = wo[kk] + woth[(size_t)ncl * H + k];
+    m[kk] = 0;
+  }
+  for (int st = top_pow2(Nc); st > 0; st >>= 1) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int c = m[kk] + st - 1;
+      if (c < Nc && !(V.sv[(g * KPW + kk) * V.svs + c] > -ow[kk])) m[kk] += st;
+    }
+  }
+  double dense[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    dense[kk] = (double)(Nc - m[kk]) * (double)wo[kk] + sw[hsort_tab(b, z, k, ((Nc + 3) & ~3) + 1) + m[kk]];
+    const float zs = ow[kk] + V.oth[(size_t)ncl * H + k];       // the self pair
+    const float gs = wo[kk] + V.woth[(size_t)ncl * H + k];
     const bool ms = (ys ? zs + dl[kk] : zs) > 0.f;
     acc[kk] = ms ? -gs : 0.f;
     ya[kk] = (ms && ys) ? -gs : 0.f;
   }
-  for (int wi = 0; wi < WC; ++wi) {       // y = 1 pairs: the mask of z1 replaces z0's
-    uint32_t word = brow[wi];
-    while (word) {
-      const int q = wi * 32 + __builtin_ctz(word);
-      word &= word - 1u;
+  // y = 1 pairs: the mask of z1 replaces z0's (the sentinel ids: weight 0)
+  for_ylist(prep, Y, ((size_t)z * B + b) * Nc + ncl, Nc, [&](int q, bool ok) {
+    const size_t e = (size_t)q * H + g * KPW;
 #pragma unroll
-      for (int kk = 0; kk < KPW; ++kk) {
-        const size_t e = (size_t)q * H + w * KPW + kk;
-        const float z0 = ow[kk] + oth[e];
-        const float g = wo[kk] + woth[e];
-        const float m1 = (z0 + dl[kk]) > 0.f ? g : 0.f;
-        acc[kk] += m1 - (z0 > 0.f ? g : 0.f);
-        ya[kk] += m1;
-      }
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = ow[kk] + V.oth[e + kk];
+      const float gq = ok ? wo[kk] + V.woth[e + kk] : 0.f;
+      const float m1 = (z0 + dl[kk]) > 0.f ? gq : 0.f;
+      acc[kk] += m1 - (z0 > 0.f ? gq : 0.f);
+      ya[kk] += m1;
     }
-  }
+  });
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
-    res[lane * HP + w * KPW + kk] = (float)dense[kk] + acc[kk];
-    yres[lane * HP + w * KPW + kk] = ya[kk];
+    res[nl * HP + g * KPW + kk] = (float)dense[kk] + acc[kk];
+    yres[nl * HP + g * KPW + kk] = ya[kk];
   }
   __syncthreads();
-  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg);
+  for (int half = 0; half < 2; ++half) {        // kw_hunk_mlpb's rows, one per 64-node tile
+    const int tile = blockIdx.x * 2 + half;
+    if (tile >= tc) break;                       // block-uniform
+    mlpb_epilogue(z, b, tile * TN, tc, Nc, nvec, res + half * TN * HP, yres + half * TN * HP,
+                  nt, Dal, Dbe, part, sg, tile);
+    __syncthreads();
+  }
 }
 
 // kw_dn  grid (tc, B): dn_c[m] = sum_k V1[m][k] Dalpha_c[k] + V1[4+m][k] Dbeta_c[k]
@@ -3138,14 +3415,15 @@ __global__ __launch_bounds__(NT) void kw_prep_T(const uint32_t* __restrict__ in,
 // kw_prep_lists  grid (ceil(Ne/4), B, 2), one wave per node and side: the set bits j != i of
 // the node's a row (side 0) / aT row (side 1) as ascending u16 ids (list_layout); the wave
 // scans the words' popcounts for each lane's write offset, then pads to 4 with Ne
+// (the same kernel builds the hunk label lists: n = Nc, bits = ybits / yT, L = ylist_layout)
 __global__ __launch_bounds__(NT) void kw_prep_lists(const uint32_t* __restrict__ abits,
                                                     const uint32_t* __restrict__ aT,
-                                                    uint32_t* __restrict__ prep, int Ne, int Nc) {
+                                                    uint32_t* __restrict__ prep, int Ne,
+                                                    ListLayout L) {
   const int lane = threadIdx.x & 63, i = blockIdx.x * NW + (threadIdx.x >> 6);
   const int b = blockIdx.y, side = blockIdx.z, B = gridDim.y;
   if (i >= Ne) return;
   const int WE = (Ne + 31) >> 5, LS = list_stride(Ne);
-  const ListLayout L = list_layout(B, Ne, Nc);
   const size_t r = ((size_t)side * B + b) * Ne + i;
   const uint32_t* row = (side ? aT : abits) + ((size_t)b * Ne + i) * WE;
   uint16_t* out = reinterpret_cast<uint16_t*>(prep + L.ids) + r * LS;
@@ -3193,8 +3471,12 @@ struct WideWork {
 bool hunk_sorted(const hdg_shape* s) {
   if (s->flags & HDG_FLAG_HUNK_DENSE) return false;
   if (s->flags & HDG_FLAG_HUNK_SORTED) return true;
-  return s->nc >= HDG_HUNK_SORTED_MIN_NC && false;   // (enabled once parity-checked)
+  return s->nc >= HDG_HUNK_SORTED_MIN_NC;
 }
+
+// the hunk label id lists (the sorted passes' walks) are part of every general-path
+// batch, whatever the flags: a batch's prep layout depends on its shape's path only
+bool hunk_lists(const hdg_shape* s) { return hdg_resolve_path(s) == HDG_PATH_GENERAL; }
 
 bool has_ent(int v) { return v == 2 || v == 4; }
 bool has_ee(int v) { return v == 4; }
@@ -3285,6 +3567,12 @@ int set_wide_attrs() {
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_clsb,      // 41 KiB static + 32 KiB at Ne 4096
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_fwd_s<true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hs_lds_bytes(HS_STAGE_MAX, 1)));
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_mlpb_s<true>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hs_lds_bytes(HS_STAGE_MAX, 2)));
     attr_set = true;
   }
   return 0;
@@ -3352,17 +3640,18 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const uint32_t* aT = prep + (size_t)B * gen_prep(Ne, Nc).words;
   const int te = (Ne + TN - 1) / TN;
   float* part = ws;
+  if (int rc = set_wide_attrs()) return rc;
   const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
   hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
                      aT, bt->hid, bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm),
                      F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
   WTRY(kmark("kw_ee_clsb", st));
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
-                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho), F(w.dgam),
-                     F(w.phi), F(w.psi), part, w.segs);
+                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
+                     F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
   WTRY(kmark("kw_ee_nodeb", st));
-  hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1, nullptr,
-                     F(w.psi), (double*)F(w.tab));
+  hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
+                     nullptr, F(w.psi), (double*)F(w.tab));
   WTRY(kmark("kw_scan", st));
   hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NTP), sort_lds_bytes(Ne), st, bt->x,
                      bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
@@ -3396,6 +3685,7 @@ void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, i
 
 size_t wide_prep_bytes(const hdg_shape* s) {
   const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
+  if (hunk_lists(s)) return ylist_layout(s->batch, s->ne, s->nc, has_ent(s->variant)).end * 4;
   if (has_ent(s->variant)) return list_layout(s->batch, s->ne, s->nc).end * 4;
   return (B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
 }
@@ -3414,7 +3704,14 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
   WTRY(kmark("kw_prep_T", st));
   if (has_ent(s->variant)) {   // the entity walks' neighbour lists
     hipLaunchKernelGGL(kw_prep_lists, dim3((s->ne + NW - 1) / NW, s->batch, 2), dim3(NT), 0, st,
-                       bt->abits, aT, (uint32_t*)bt->prep, s->ne, s->nc);
+                       bt->abits, aT, (uint32_t*)bt->prep, s->ne,
+                       list_layout(s->batch, s->ne, s->nc));
+    WTRY(kmark("kw_prep_lists", st));
+  }
+  if (hunk_lists(s)) {         // the sorted hunk passes' label lists
+    hipLaunchKernelGGL(kw_prep_lists, dim3((s->nc + NW - 1) / NW, s->batch, 2), dim3(NT), 0, st,
+                       bt->ybits, yT, (uint32_t*)bt->prep, s->nc,
+                       ylist_layout(s->batch, s->ne, s->nc, has_ent(s->variant)));
     WTRY(kmark("kw_prep_lists", st));
   }
   return 0;
@@ -3538,15 +3835,30 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                      F(w.beta));
   WTRY(kmark("kw_cross_fwd", st));
   const bool hs = hunk_sorted(s);
+  const ListLayout YL = ylist_layout(B, Ne, Nc, ent);
   if (hs) {
-    int np2 = 1;
-    while (np2 < Nc) np2 <<= 1;
-    hipLaunchKernelGGL(kw_hunk_sort, dim3(H, B, 2), dim3(NT), (size_t)8 * np2, st, F(w.alpha),
-                       F(w.beta), Nc, F(w.hsv), (int*)F(w.hsp), (double*)F(w.hsx));
+    const dim3 gw((H + NW - 1) / NW, B, 2);
+#define HDG_SORT(E_)                                                                            \
+  hipLaunchKernelGGL(kw_hunk_sort<E_>, gw, dim3(NT), 0, st, F(w.alpha), F(w.beta), Nc, F(w.hsv), \
+                     (int*)F(w.hsp), (double*)F(w.hsx))
+    switch (hsort_e(Nc)) {
+      case 2: HDG_SORT(2); break;
+      case 4: HDG_SORT(4); break;
+      case 8: HDG_SORT(8); break;
+      case 16: HDG_SORT(16); break;
+      default: HDG_SORT(32); break;
+    }
+#undef HDG_SORT
     WTRY(kmark("kw_hunk_sort", st));
-    hipLaunchKernelGGL(kw_hunk_fwd_s, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
-                       F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx), F(w.G),
-                       F(w.Hh), F(w.sig), F(w.tau));
+    const dim3 gs((Nc + HSN - 1) / HSN, B, 2);
+    if (Nc <= HS_STAGE_MAX)
+      hipLaunchKernelGGL(kw_hunk_fwd_s<true>, gs, dim3(NTP), hs_lds_bytes(Nc, 1), st, bt->ybits,
+                         yT, D, Nc, F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx),
+                         prep, YL, F(w.G), F(w.Hh), F(w.sig), F(w.tau));
+    else
+      hipLaunchKernelGGL(kw_hunk_fwd_s<false>, gs, dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
+                         F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx), prep, YL,
+                         F(w.G), F(w.Hh), F(w.sig), F(w.tau));
     WTRY(kmark("kw_hunk_fwd_s", st));
   } else {
     hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
@@ -3577,12 +3889,28 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                      F(w.dG), F(w.dH), part, w.segs);
   WTRY(kmark("kw_hunk_clsb", st));
   if (hs) {
-    hipLaunchKernelGGL(kw_hunk_wsum, dim3(H, B, 2), dim3(NT), 0, st, (const int*)F(w.hsp),
-                       F(w.dG), F(w.dH), Nc, (double*)F(w.hsw));
+    const dim3 gw((H + NW - 1) / NW, B, 2);
+#define HDG_WSUM(E_)                                                                        \
+  hipLaunchKernelGGL(kw_hunk_wsum<E_>, gw, dim3(NT), 0, st, (const int*)F(w.hsp), F(w.dG), \
+                     F(w.dH), Nc, (double*)F(w.hsw))
+    switch (hsort_e(Nc)) {
+      case 2: HDG_WSUM(2); break;
+      case 4: HDG_WSUM(4); break;
+      case 8: HDG_WSUM(8); break;
+      case 16: HDG_WSUM(16); break;
+      default: HDG_WSUM(32); break;
+    }
+#undef HDG_WSUM
     WTRY(kmark("kw_hunk_wsum", st));
-    hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3(tc, B, 2), dim3(NT), 0, st, bt->ybits, yT, D, Nc,
-                       F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
-                       (const double*)F(w.hsw), F(w.Dal), F(w.Dbe), part, w.segs);
+    const dim3 gs((Nc + HSN - 1) / HSN, B, 2);
+    if (Nc <= HS_STAGE_MAX)
+      hipLaunchKernelGGL(kw_hunk_mlpb_s<true>, gs, dim3(NTP), hs_lds_bytes(Nc, 2), st, bt->ybits,
+                         yT, D, Nc, F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
+                         (const double*)F(w.hsw), prep, YL, F(w.Dal), F(w.Dbe), part, w.segs);
+    else
+      hipLaunchKernelGGL(kw_hunk_mlpb_s<false>, gs, dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
+                         F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
+                         (const double*)F(w.hsw), prep, YL, F(w.Dal), F(w.Dbe), part, w.segs);
     WTRY(kmark("kw_hunk_mlpb_s", st));
   } else {
     hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,

@@ -110,7 +110,7 @@ class DeviceBatch:
         import torch
         from . import _lib
         self.x, self.abits, self.ybits, self.hid, self.nlen = x, abits, ybits, hid, nlen
-        self.B, self.Ne, self.Nc = x.shape[0], Ne, Nc
+        self.B, self.Ne, self.Nc, self.variant = x.shape[0], Ne, Nc, variant
         lib = _lib.load()
         shape = _lib.Shape(self.B, Ne, Nc, variant, self.B, path)
         self.path = lib.hdg_resolve_path(ctypes.byref(shape))   # prep layout is per path

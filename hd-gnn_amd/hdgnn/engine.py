@@ -21,10 +21,11 @@ from .layout import n_params
 
 class Engine:
     def __init__(self, ne, nc, batch, variant=2, device="cuda", batch_global=None, lr=3e-4,
-                 process_group=None, path=_lib.PATH_AUTO, allreduce=None):
+                 process_group=None, path=_lib.PATH_AUTO, allreduce=None, flags=0):
         """variant: model_<variant>.py (1 HD-GNN/ES, 2 HD-GNN/S, 3 HD-GNN/E, 4 HD-GNN).
         path: PATH_AUTO (fused kernel when it applies, else the general path),
-        PATH_FUSED or PATH_GENERAL (include/hdgnn.h)."""
+        PATH_FUSED or PATH_GENERAL (include/hdgnn.h).  flags: HDG_FLAG_* bits
+        (FLAG_HUNK_DENSE / FLAG_HUNK_SORTED force the general path's hunk-sum form)."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -35,7 +36,7 @@ class Engine:
         self.batch_global = batch_global or batch
         self.lr = lr
         self.pg = process_group
-        self.shape = _lib.Shape(batch, ne, nc, variant, self.batch_global, path)
+        self.shape = _lib.Shape(batch, ne, nc, variant, self.batch_global, path, flags)
         self.path = self.lib.hdg_resolve_path(ctypes.byref(self.shape))
         if self.path < 0:
             raise ValueError(self.lib.hdg_last_error().decode())
@@ -115,9 +116,10 @@ class Engine:
 
     def _check(self, dbatch):
         assert dbatch.B == self.batch and dbatch.Ne == self.ne and dbatch.Nc == self.nc
-        if dbatch.path != self.path:
-            raise ValueError("batch prepared for path %d, engine runs path %d (use "
-                             "Engine.upload)" % (dbatch.path, self.path))
+        if dbatch.path != self.path or getattr(dbatch, "variant", self.variant) != self.variant:
+            raise ValueError("batch prepared for model_%s path %d, engine runs model_%d path %d "
+                             "(use Engine.upload)" % (getattr(dbatch, "variant", "?"), dbatch.path,
+                                                      self.variant, self.path))
 
     def _outputs(self, outputs, logits, stats=None):
         if not outputs:

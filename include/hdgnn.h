@@ -58,13 +58,13 @@ typedef struct hdg_shape {
  * re-association of the block-pair sums.                                              */
 #define HDG_FLAG_NO_SPLIT 1
 /* General path, hunk pair sums of the first hunk MLP layer (forward relu sums, backward mask
- * sums): by default from per-unit sorted thresholds (a binary search per node and unit plus
- * the label pairs one by one) when nc >= 256, a dense sweep of the pair grid below; these
+ * sums): a dense sweep of the pair grid, or per-unit sorted thresholds (a binary search per
+ * node and unit plus the label pairs one by one) from nc >= HDG_HUNK_SORTED_MIN_NC; these
  * flags force one form (same results up to fp32 re-association; the layout of
  * hdg_workspace_bytes follows the choice, so keep the flags fixed for a workspace).      */
 #define HDG_FLAG_HUNK_DENSE 2
 #define HDG_FLAG_HUNK_SORTED 4
-#define HDG_HUNK_SORTED_MIN_NC 256
+#define HDG_HUNK_SORTED_MIN_NC 0x7fffffff   /* default: dense (the measured crossover) */
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
  * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge
@@ -155,7 +155,9 @@ int         hdg_grad_len(int32_t variant);
  * run at the same time: plain launches do not guarantee it, so a pair that cannot meet
  * is detected (HDG_STATUS_XCH_TIMEOUT) instead of producing silent garbage.          */
 size_t      hdg_workspace_bytes(const hdg_shape* shape);
-/* bytes of batch->prep for this shape (0 on a shape error) */
+/* bytes of batch->prep for this shape (0 on a shape error).  It depends on the path the
+ * shape resolves to (fused, fused + entity-edge, general), never on the flags: prepare a
+ * batch with a shape that resolves to the same path as the steps that read it.      */
 size_t      hdg_prep_bytes(const hdg_shape* shape);
 /* Where hdg_prepare puts the cross-graph count tables of commit b inside batch->prep
  * (4-byte words from prep + b * stride_words): K_s at ks, K_t at kt (u16 [Nc][Ne]),

@@ -27,9 +27,9 @@ def _keys(v):
     return [k for k, _, _ in olayout.keyed_specs(v)]
 
 
-def _engine(B, ne, nc, v, path=GEN):
+def _engine(B, ne, nc, v, path=GEN, flags=0):
     from hdgnn.engine import Engine
-    return Engine(ne, nc, B, variant=v, path=path)
+    return Engine(ne, nc, B, variant=v, path=path, flags=flags)
 
 
 def _oracle(flat, cb, v):
@@ -77,10 +77,10 @@ def _grad_close(g_eng, g_ref, v):
     assert not bad, "gradient mismatch:\n  " + "\n  ".join(bad)
 
 
-def _run_and_check(cb, v, seed, path=GEN):
+def _run_and_check(cb, v, seed, path=GEN, flags=0):
     B, ne, nc = cb.B, cb.Ne, cb.Nc
     flat = layout.init_flat(seed, v)
-    eng = _engine(B, ne, nc, v, path)
+    eng = _engine(B, ne, nc, v, path, flags)
     eng.set_params(flat)
     db = eng.upload(cb)
     eng.fwd_bwd(db)
@@ -301,3 +301,67 @@ def test_max_classes_matches_oracle(v):
     """The general path's class limit Nc = 2048 (hunk pair passes over 2048 x 2047
     relations, 64-word y rows, u16 count tables)."""
     _run_and_check(synth_commits(1, 40, 2048, 4), v, 4)
+
+
+SORTED, DENSE = _lib.FLAG_HUNK_SORTED, _lib.FLAG_HUNK_DENSE
+
+
+@pytest.mark.parametrize("v", [1, 2, 4])
+@pytest.mark.parametrize("B,ne,nc,seed", SHAPES + [(1, 90, 300, 10)])
+def test_hunk_sorted_matches_oracle(v, B, ne, nc, seed):
+    """The sorted-threshold hunk sums (kw_hunk_sort / _fwd_s / _wsum / _mlpb_s), forced on
+    below their default crossover, against the oracle at every tile boundary."""
+    _run_and_check(synth_commits(B, ne, nc, seed), v, seed, GEN, SORTED)
+
+
+@pytest.mark.parametrize("case", ["empty_adjacency", "full_adjacency", "float_attributes",
+                                  "all_lines_one_hunk"])
+def test_hunk_sorted_edge_cases(case):
+    """No label pairs, every pair labelled (the correction walk over all Nc - 1 bits, ties
+    of equal alpha / beta values across nodes), real-valued attributes."""
+    _run_and_check(EDGE[case](synth_commits(2, 70, 13, 7)), 2, 7, GEN, SORTED)
+    _run_and_check(EDGE[case](synth_commits(1, 40, 300, 7)), 2, 7, GEN, SORTED)
+
+
+@pytest.mark.parametrize("nc", [300, 512, 1024])
+def test_hunk_sorted_equals_dense(nc):
+    """The two forms of the general path agree far inside the oracle tolerance (the
+    default switches at HUNK_SORTED_MIN_NC)."""
+    B, ne, v = 1, 64, 2
+    cb = synth_commits(B, ne, nc, 21)
+    flat = layout.init_flat(4, v)
+    outs = []
+    for fl in (DENSE, SORTED):
+        eng = _engine(B, ne, nc, v, GEN, fl)
+        eng.set_params(flat)
+        eng.fwd_bwd(eng.upload(cb))
+        torch.cuda.synchronize()
+        outs.append((eng.logits.cpu().numpy().astype(np.float64),
+                     eng.grad.cpu().numpy().astype(np.float64)))
+    (l1, g1), (l2, g2) = outs
+    scale = np.maximum(1.0, np.abs(l1).max())
+    assert np.abs(l1 - l2).max() <= 2e-6 * scale
+    np_ = layout.n_params(v)
+    for name, (o, shape) in layout.offsets(v).items():
+        n = int(np.prod(shape))
+        a, r = g2[o:o + n], g1[o:o + n]
+        assert np.abs(a - r).max() <= 1e-5 * max(np.abs(r).max(), 1e-12), name
+    assert _lib.trailer_count(g1[np_:]) == _lib.trailer_count(g2[np_:])
+
+
+def test_hunk_sorted_deterministic_and_garbage_free():
+    B, ne, nc, v = 2, 60, 290, 2
+    cb = synth_commits(B, ne, nc, 8)
+    flat = layout.init_flat(5, v)
+    ref = _engine(B, ne, nc, v, GEN, SORTED)
+    ref.set_params(flat)
+    db = ref.upload(cb)
+    ref.fwd_bwd(db)
+    g1, p1 = ref.grad.clone(), ref.probs.clone()
+    dirty = _engine(B, ne, nc, v, GEN, SORTED)
+    dirty.set_params(flat)
+    dirty.workspace.fill_(float("nan"))
+    dirty.grad.fill_(float("inf"))
+    dirty.fwd_bwd(dirty.upload(cb))
+    torch.cuda.synchronize()
+    assert torch.equal(g1, dirty.grad) and torch.equal(p1, dirty.probs)

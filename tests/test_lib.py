@@ -61,8 +61,10 @@ def test_host_only_entry_points():
     assert lib.hdg_resolve_path(ctypes.byref(m4)) == _lib.PATH_FUSED
     m4g = _lib.Shape(100, 200, 74, 4, 100, _lib.PATH_GENERAL)
     m2 = _lib.Shape(100, 200, 74, 2, 100, 0)
-    assert lib.hdg_prep_bytes(ctypes.byref(m4)) == (lib.hdg_prep_bytes(ctypes.byref(m2)) +
-                                                     lib.hdg_prep_bytes(ctypes.byref(m4g)))
+    # (the general path's own batches also carry the hunk label lists of its sorted passes,
+    # which the hybrid's entity-edge half does not need)
+    assert (lib.hdg_prep_bytes(ctypes.byref(m2)) < lib.hdg_prep_bytes(ctypes.byref(m4))
+            <= lib.hdg_prep_bytes(ctypes.byref(m2)) + lib.hdg_prep_bytes(ctypes.byref(m4g)))
     assert lib.hdg_workspace_bytes(ctypes.byref(m4)) > lib.hdg_workspace_bytes(ctypes.byref(m4g))
     forced = _lib.Shape(4, 200, 74, 2, 4, _lib.PATH_GENERAL)
     assert lib.hdg_resolve_path(ctypes.byref(forced)) == _lib.PATH_GENERAL
