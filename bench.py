@@ -237,7 +237,7 @@ def main():
                     help="model_<variant>.py (the BASELINE metric is model_2)")
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
-    ap.add_argument("--hunk", default="auto", choices=("auto", "dense", "sorted"),
+    ap.add_argument("--hunk", default="auto", choices=("auto", "dense", "sorted", "tiled"),
                     help="general path's hunk relu / mask sums: the default crossover "
                          "(include/hdgnn.h HDG_HUNK_SORTED_MIN_NC), or forced dense / sorted")
     ap.add_argument("--edensity", type=float, default=0.05,
@@ -272,7 +272,8 @@ def main():
     knobs = {"edensity": args.edensity, "hdensity": args.hdensity, "xkind": args.xkind}
     default_data = knobs == {"edensity": 0.05, "hdensity": 0.10, "xkind": "int10"}
     cb = synth_commits(B, ne, nc, seed_for(1, rank), **knobs)
-    hflags = {"auto": 0, "dense": _lib.FLAG_HUNK_DENSE, "sorted": _lib.FLAG_HUNK_SORTED}[args.hunk]
+    hflags = {"auto": 0, "dense": _lib.FLAG_HUNK_DENSE, "sorted": _lib.FLAG_HUNK_SORTED,
+              "tiled": _lib.FLAG_HUNK_TILED}[args.hunk]
     eng = Engine(ne, nc, B, variant=v, device=dev, batch_global=B * world, path=args.path,
                  process_group=torch.distributed.group.WORLD if launched else None,
                  flags=hflags)

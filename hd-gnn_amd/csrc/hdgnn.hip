@@ -323,9 +323,14 @@ __device__ __forceinline__ void pair_tile(
     const float* __restrict__ wr, const float* __restrict__ wc,
     const float* __restrict__ gam, const int gld, float* Rout, float* Cout,
     float* __restrict__ ysum, float* __restrict__ cred, const int rmul = 1, const int radd = 0,
-    FIX fix = FIX{}) {
+    FIX fix = FIX{}, const int ncol = -1, const int wstride = -1, const int doff = 0) {
   typedef float p2 __attribute__((ext_vector_type(2)));
   constexpr int NP16 = 16 * SMAX;
+  // a rectangular block of the pair grid (the general path's tiled passes): N rows, NCOL
+  // columns, the rows' bit words at stride WS (W of them from the block's first column on),
+  // global column = global row + doff on the diagonal; the fused kernel's square grid by
+  // default
+  const int NCOL = ncol < 0 ? N : ncol, WS = wstride < 0 ? W : wstride;
   constexpr int NW = (SMAX + 1) / 2;
   constexpr int KP = KK / 2, KT = KK & 1;      // packed fp32 pairs (v_pk_*) + odd tail
   // SIMD balance: waves 4g + w of a block share one SIMD for every group g (workgroup waves
@@ -416,7 +421,7 @@ __device__ __forceinline__ void pair_tile(
     const uint32_t bmask = iv ? 0xFFFFFFFFu : 0u;
 #pragma unroll
     for (int q = 0; q < NW; ++q)        // clamped load, masked value
-      wrow[q] = bits[ib * W + (q < W ? q : 0)] & (q < W ? bmask : 0u);
+      wrow[q] = bits[ib * WS + (q < W ? q : 0)] & (q < W ? bmask : 0u);
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
@@ -426,9 +431,9 @@ __device__ __forceinline__ void pair_tile(
       if constexpr (MODE == 2 && GFULL) {   // rows past the sweep read the first swept row
         g = gam[(iv ? i : radd) * gld + j];  // (A = -inf zeroes their terms)
       } else if constexpr (MODE == 2) {      // clamped load, selected (not multiplied:
-        const int ic = iv ? i : N - 1, jc = j < N ? j : N - 1;   // garbage * 0 can be NaN)
+        const int ic = iv ? i : N - 1, jc = j < NCOL ? j : NCOL - 1;   // garbage * 0 can be NaN)
         const float gl = gam[ic * gld + jc];
-        g = (iv && j < N && j != i) ? gl : 0.f;
+        g = (iv && j < NCOL && j + doff != i) ? gl : 0.f;
       }
       const float* Bj = Bv + j * LD;
 #pragma unroll
@@ -529,7 +534,7 @@ __device__ __forceinline__ void pair_tile(
     wave_sums(yacc, lane, [&](int k, float x) { credy[wv * KK + k] = x; });
   }
   __syncthreads();
-  close_columns<NP16 * KK, KK>(cred, N, t, kof, fix,
+  close_columns<NP16 * KK, KK>(cred, NCOL, t, kof, fix,
                                [&](int j, int kk, float v) { Cout[j * LD + kk] = v; });
   if constexpr (MODE != 0) {
     if (t < KK) ysum[kof(t)] = credy[t] + credy[KK + t] + credy[2 * KK + t] + credy[3 * KK + t];
@@ -3282,6 +3287,96 @@ int prep_tile(int ne, int nc) {
   while (ti > 1 && prep_lds_words(ne, nc, ti) > 38 * 1024) ti >>= 1;
   return ti;
 }
+
+// ------------------------------------------------------------------------------
+// kh_tile<MODE>  grid (ceil(Nc / HTC), ceil(Nc / HTR), B), 1024 threads = 4 groups of 256
+// (one per five hidden units): the general path's hunk pair sums on one HTR-row x
+// HTC-column block of the commit's pair grid with the fused kernel's pair tiles -- row sums
+// and column sums from ONE sweep (the two-pass kernels sweep every pair twice, once per
+// side), block partials reduced in a fixed order by kw_hunk_fin*:
+//   MODE 0  relu(z), z = alpha_p + beta_q + y delta           (kw_hunk_fwd's G / H)
+//   MODE 1  [z > 0] (dG_p + dH_q)                            (kw_hunk_mlpb's D alpha / D beta)
+//   MODE 2  [kappa > 0] gamma_pq, kappa = sigma_p + tau_q + y eps   (kw_hunk_clsb's sums)
+// Rpart [B][CC][Nc][20] row sums over the block's columns, Cpart [B][RC][Nc][20] column sums
+// over its rows, ysp [B][RC][CC][20] sum y e (MODE 1, 2).  The diagonal pair is inside the
+// sweep for MODE 0 / 1 (removed by kw_hunk_fin0 / fin1); gamma's diagonal is 0.
+// ------------------------------------------------------------------------------
+constexpr int HTR = 256, HTC = 64, HT_SMAX = HTC / 16;
+
+template <int MODE>
+__global__ __launch_bounds__(NT_MID) void kh_tile(hdg::HTileArgs a) {
+  constexpr int CRW = tile_cred_words<HT_SMAX, KK_MID>();
+  __shared__ __attribute__((aligned(16))) float Al[HTR * HS];
+  __shared__ __attribute__((aligned(16))) float Bl[HTC * HS];
+  __shared__ __attribute__((aligned(16))) float Wr[MODE == 1 ? HTR * HS : 4];
+  __shared__ __attribute__((aligned(16))) float Wc[MODE == 1 ? HTC * HS : 4];
+  __shared__ float cred[NG_MID * CRW];
+  const int cc = blockIdx.x, rc = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int Nc = a.Nc, CC = gridDim.x, RC = gridDim.y, WC = (Nc + 31) >> 5;
+  const int j0 = cc * HTC, r0 = rc * HTR;
+  const int nr = Nc - r0 < HTR ? Nc - r0 : HTR, ncol = Nc - j0 < HTC ? Nc - j0 : HTC;
+  const size_t cb = (size_t)b * Nc * HS;
+  {   // 16-byte copies, every load of a thread issued before its stores
+    const float4* ra = reinterpret_cast<const float4*>(a.rows + cb + (size_t)r0 * HS);
+    const float4* ca = reinterpret_cast<const float4*>(a.cols + cb + (size_t)j0 * HS);
+    const int nra = nr * HS / 4, nca = HTC * HS / 4, ncv = ncol * HS / 4;
+    const float4 pad = make_float4(PADNEG, PADNEG, PADNEG, PADNEG), zero4 = {0.f, 0.f, 0.f, 0.f};
+    float4 v0 = t < nra ? ra[t] : pad, v1 = t + NT_MID < nra ? ra[t + NT_MID] : pad;
+    float4 w0 = zero4, w1 = zero4, u = pad, uw = zero4;
+    if constexpr (MODE == 1) {
+      const float4* rw = reinterpret_cast<const float4*>(a.wrow + cb + (size_t)r0 * HS);
+      w0 = t < nra ? rw[t] : zero4;
+      w1 = t + NT_MID < nra ? rw[t + NT_MID] : zero4;
+    }
+    if (t < nca) {
+      u = t < ncv ? ca[t] : pad;
+      if constexpr (MODE == 1)
+        uw = t < ncv ? reinterpret_cast<const float4*>(a.wcol + cb + (size_t)j0 * HS)[t] : zero4;
+    }
+    float4* A4 = reinterpret_cast<float4*>(Al);
+    if (t < HTR * HS / 4) A4[t] = v0;
+    if (t + NT_MID < HTR * HS / 4) A4[t + NT_MID] = v1;
+    if constexpr (MODE == 1) {
+      float4* W4 = reinterpret_cast<float4*>(Wr);
+      if (t < HTR * HS / 4) W4[t] = w0;
+      if (t + NT_MID < HTR * HS / 4) W4[t + NT_MID] = w1;
+    }
+    if (t < nca) {
+      reinterpret_cast<float4*>(Bl)[t] = u;
+      if constexpr (MODE == 1) reinterpret_cast<float4*>(Wc)[t] = uw;
+    }
+  }
+  __syncthreads();
+  const int g = t >> 8, tg = t & 255;
+  const uint32_t* bits = a.ybits + ((size_t)b * Nc + r0) * WC + (j0 >> 5);
+  float* Rout = a.rpart + (((size_t)b * CC + cc) * Nc + r0) * HS;
+  float* Cout = a.cpart + (((size_t)b * RC + rc) * Nc + j0) * HS;
+  float* ysum = a.ysp + (((size_t)b * RC + rc) * CC + cc) * HS;
+  const float* gam = MODE == 2 ? a.gam + ((size_t)b * Nc + r0) * Nc + j0 : nullptr;
+  pair_tile<KK_MID, HT_SMAX, MODE, HS, 0, false>(
+      nr, tg, Al, Bl, g * KK_MID, a.dl, bits, WC - (j0 >> 5), Wr, Wc, gam, Nc, Rout, Cout, ysum,
+      cred + g * CRW, 1, 0, NoFix{}, ncol, WC, j0 - r0);
+}
+
+}  // namespace
+
+namespace hdg {
+
+hipError_t launch_hunk_tile(int mode, const HTileArgs& a, int B, hipStream_t st) {
+  const dim3 grid((a.Nc + HTC - 1) / HTC, (a.Nc + HTR - 1) / HTR, B);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(kh_tile<0>, grid, dim3(NT_MID), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(kh_tile<1>, grid, dim3(NT_MID), 0, st, a); break;
+    default: hipLaunchKernelGGL(kh_tile<2>, grid, dim3(NT_MID), 0, st, a); break;
+  }
+  return kmark(mode == 0 ? "kh_tile<0>" : (mode == 1 ? "kh_tile<1>" : "kh_tile<2>"), st);
+}
+int hunk_tile_cols() { return HTC; }
+int hunk_tile_rows() { return HTR; }
+
+}  // namespace hdg
+
+namespace {
 
 }  // namespace
 

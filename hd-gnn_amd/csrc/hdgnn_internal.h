@@ -129,6 +129,23 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
 hipError_t launch_ehr(const float* G, const float* Hh, size_t cs, int B, int Nc,
                       const float* params, int variant, float* out, hipStream_t st);
 
+// the general path's one-sweep hunk pair sums (kh_tile<MODE>, hdgnn.hip: the fused kernel's
+// pair tiles on HTR x HTC blocks of the pair grid); mode 0 relu sums, 1 MLP mask sums,
+// 2 classifier mask sums (see hdgnn.hip).  All pointers are per batch (commit b at b * Nc *
+// 20 floats, gam at b * Nc * Nc); rpart / cpart / ysp the block partials.
+struct HTileArgs {
+  int Nc;
+  const float *rows, *cols;       // alpha / beta (modes 0, 1), sigma / tau (mode 2)
+  const float *wrow, *wcol;       // dG / dH (mode 1)
+  const float* gam;               // [B][Nc][Nc] (mode 2)
+  const float* dl;                // delta (D + D_DLT) / eps (D + D_EPS): 20 floats
+  const uint32_t* ybits;          // [B][Nc][ceil(Nc/32)]
+  float *rpart, *cpart, *ysp;
+};
+hipError_t launch_hunk_tile(int mode, const HTileArgs& a, int B, hipStream_t st);
+int hunk_tile_cols();             // HTC: columns per block
+int hunk_tile_rows();             // HTR: rows per block
+
 // fused path pieces the general path reuses (hdgnn.hip)
 hipError_t launch_prep_maps(const hdg_shape* s, const hdg_batch* bt, int stride, int o_ks,
                             int o_kt, int o_ncst, hipStream_t st);

@@ -1449,6 +1449,98 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   }
 }
 
+// kw_hunk_clsb's epilogue (also kw_hunk_fin2's): from the tile's per-node sums res (and
+// the y-weighted sums yres, row pass), D = c (.) sums out, dG = D M^T (dH), and the partial
+// rows of dU1 / dd1 / dV2 / dc2 through X = sum_n G_n (x) D_n (model_2.py:265-275, 304-321).
+// LDS: res, yres, Gt [TN][HP]; X [H][H]; sumD, ysum [H]; Wl the staged M | V2 | c2 | U1e.
+__device__ __forceinline__ void clsb_epilogue(
+    const int z, const int b, const int t0, const int tc, const int Nc, const float* __restrict__ W,
+    const Off& o, const float* __restrict__ D, const float* __restrict__ G,
+    const float* __restrict__ Hh, float* __restrict__ Dsig, float* __restrict__ Dtau,
+    float* __restrict__ dG, float* __restrict__ dH, float* __restrict__ part, const Segs& sg,
+    float* res, float* yres, float* Gt, float* X, float* sumD, float* ysum, const float* Wl,
+    const float* kzh, const int tile) {
+  const float *Ml = Wl, *V2 = Wl + H * H, *c2 = Wl + 2 * H * H, *U1e = Wl + 2 * H * H + H;
+  (void)W;
+  const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
+  float* dout = (z ? Dtau : Dsig) + (size_t)b * Nc * H;
+  float* gout = (z ? dH : dG) + (size_t)b * Nc * H;
+  for (int e = threadIdx.x; e < TN * H; e += blockDim.x) {   // D = c (.) sums; padding rows -> 0
+    const int n = e / H, k = e - n * H;
+    const bool in = t0 + n < Nc;
+    const float d = in ? res[n * HP + k] * D[D_CV + k] : 0.f;
+    res[n * HP + k] = d;
+    Gt[n * HP + k] = in ? gsrc[(t0 + n) * H + k] : 0.f;
+    if (z == 0 && !in) yres[n * HP + k] = 0.f;
+    if (in) dout[(t0 + n) * H + k] = d;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < TN * H; e += blockDim.x) {   // dG_n[l] = sum_k M[l][k] D_n[k]
+    const int n = e / H, l = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float sacc = 0.f;
+    for (int k = 0; k < H; ++k) sacc = fmaf(Ml[l * H + k], res[n * HP + k], sacc);
+    gout[(t0 + n) * H + l] = sacc;
+  }
+  if (threadIdx.x < 256) {   // X_blk = sum_n G_n (x) D_n: 2 x 2 16x16 MFMA tiles, K = 64 nodes
+    const int lane = threadIdx.x & 63, tq = threadIdx.x >> 6;   // wave-uniform
+    const int rl = (tq >> 1) * 16 + (lane & 15), kc = (tq & 1) * 16 + (lane & 15);
+    const bool rv = rl < H, cv = kc < H;
+    const f4v c = mfma_tile16_p(rv ? Gt + rl : kzh, rv ? HP : 0, cv ? res + kc : kzh,
+                                cv ? HP : 0, TN, lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = (tq >> 1) * 16 + 4 * (lane >> 4) + j;
+        if (rr < H) X[rr * H + kc] = c[j];
+      }
+  }
+  if (threadIdx.x < H) {
+    const int k = threadIdx.x;
+    float sd = 0.f, y = 0.f;
+    for (int n = 0; n < TN; ++n) {
+      sd += res[n * HP + k];
+      if (z == 0) y += yres[n * HP + k];
+    }
+    sumD[k] = sd;
+    ysum[k] = y;
+  }
+  __syncthreads();
+  const int row = (b * tc + tile) * 2 + z;
+  const float Nc1 = (float)(Nc - 1);
+  const Seg& s2 = sg.s[SG_CLSB_H2];
+  const Seg& s1 = sg.s[SG_CLSB_H1];
+  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += blockDim.x) {
+    if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
+      const int m = e / H, k = e - m * H;
+      float a = Nc1 * c2[m] * sumD[k];
+      for (int l = 0; l < H; ++l) a = fmaf(V2[l * H + m], X[l * H + k], a);
+      put(part, s2, (2 + m) * H + k, row, a);
+    } else if (e < 2 * H * H) {   // dV2[l][m] = sum_k X[l][k] U1e[m][k]
+      const int f = e - H * H, l = f / H, m = f - l * H;
+      float a = 0.f;
+      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], U1e[m * H + k], a);
+      put(part, s1, f, row, a);
+    } else if (e < 2 * H * H + H) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
+      const int m = e - 2 * H * H;
+      float a = 0.f;
+      for (int k = 0; k < H; ++k) a = fmaf(U1e[m * H + k], sumD[k], a);
+      put(part, s1, H * H + m, row, Nc1 * a);
+    } else {                      // dU1[0], dU1[1], dd1 (row pass only)
+      const int f = e - 2 * H * H - H;   // 0 .. 2H-1
+      const int k = f % H;
+      const float dd1 = z == 0 ? sumD[k] : 0.f;
+      const float dy1 = z == 0 ? D[D_CV + k] * ysum[k] : 0.f;
+      if (f < H) {
+        put(part, s2, k, row, dd1 - dy1);
+        put(part, s2, H + k, row, dy1);
+      } else {
+        put(part, s2, 22 * H + k, row, dd1);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // kw_hunk_clsb  grid (tc, B, 2): classifier backward (model_2.py:304-321)
 //   e_pqk = [kappa_pqk > 0] gamma_pq;  row pass: Dsig_p = c (.) sum_q e_pq, ysum = sum y e
@@ -1537,83 +1629,8 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   __syncthreads();                       // every wave is done with os_ / gt (= buf)
   combine8(acc, buf, res);
   if (z == 0) combine8(ya, buf, yres);
-  const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
-  float* dout = (z ? Dtau : Dsig) + (size_t)b * Nc * H;
-  float* gout = (z ? dH : dG) + (size_t)b * Nc * H;
-  for (int e = threadIdx.x; e < TN * H; e += NTP) {   // D = c (.) sums; padding rows -> 0
-    const int n = e / H, k = e - n * H;
-    const bool in = t0 + n < Nc;
-    const float d = in ? res[n * HP + k] * D[D_CV + k] : 0.f;
-    res[n * HP + k] = d;
-    Gt[n * HP + k] = in ? gsrc[(t0 + n) * H + k] : 0.f;
-    if (z == 0 && !in) yres[n * HP + k] = 0.f;
-    if (in) dout[(t0 + n) * H + k] = d;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < TN * H; e += NTP) {   // dG_n[l] = sum_k M[l][k] D_n[k]
-    const int n = e / H, l = e - n * H;
-    if (t0 + n >= Nc) continue;
-    float sacc = 0.f;
-    for (int k = 0; k < H; ++k) sacc = fmaf(Ml[l * H + k], res[n * HP + k], sacc);
-    gout[(t0 + n) * H + l] = sacc;
-  }
-  if (threadIdx.x < 256) {   // X_blk = sum_n G_n (x) D_n: 2 x 2 16x16 MFMA tiles, K = 64 nodes
-    const int lane = threadIdx.x & 63, tile = threadIdx.x >> 6;   // wave-uniform
-    const int rl = (tile >> 1) * 16 + (lane & 15), kc = (tile & 1) * 16 + (lane & 15);
-    const bool rv = rl < H, cv = kc < H;
-    const f4v c = mfma_tile16_p(rv ? Gt + rl : kzh, rv ? HP : 0, cv ? res + kc : kzh,
-                                cv ? HP : 0, TN, lane);
-    if (cv)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int rr = (tile >> 1) * 16 + 4 * (lane >> 4) + j;
-        if (rr < H) X[rr * H + kc] = c[j];
-      }
-  }
-  if (threadIdx.x < H) {
-    const int k = threadIdx.x;
-    float sd = 0.f, y = 0.f;
-    for (int n = 0; n < TN; ++n) {
-      sd += res[n * HP + k];
-      if (z == 0) y += yres[n * HP + k];
-    }
-    sumD[k] = sd;
-    ysum[k] = y;
-  }
-  __syncthreads();
-  const int row = (b * tc + blockIdx.x) * 2 + z;
-  const float Nc1 = (float)(Nc - 1);
-  const Seg& s2 = sg.s[SG_CLSB_H2];
-  const Seg& s1 = sg.s[SG_CLSB_H1];
-  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += NTP) {
-    if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
-      const int m = e / H, k = e - m * H;
-      float a = Nc1 * c2[m] * sumD[k];
-      for (int l = 0; l < H; ++l) a = fmaf(V2[l * H + m], X[l * H + k], a);
-      put(part, s2, (2 + m) * H + k, row, a);
-    } else if (e < 2 * H * H) {   // dV2[l][m] = sum_k X[l][k] U1e[m][k]
-      const int f = e - H * H, l = f / H, m = f - l * H;
-      float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], U1e[m * H + k], a);
-      put(part, s1, f, row, a);
-    } else if (e < 2 * H * H + H) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
-      const int m = e - 2 * H * H;
-      float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(U1e[m * H + k], sumD[k], a);
-      put(part, s1, H * H + m, row, Nc1 * a);
-    } else {                      // dU1[0], dU1[1], dd1 (row pass only)
-      const int f = e - 2 * H * H - H;   // 0 .. 2H-1
-      const int k = f % H;
-      const float dd1 = z == 0 ? sumD[k] : 0.f;
-      const float dy1 = z == 0 ? D[D_CV + k] * ysum[k] : 0.f;
-      if (f < H) {
-        put(part, s2, k, row, dd1 - dy1);
-        put(part, s2, H + k, row, dy1);
-      } else {
-        put(part, s2, 22 * H + k, row, dd1);
-      }
-    }
-  }
+  clsb_epilogue(z, b, t0, tc, Nc, W, o, D, G, Hh, Dsig, Dtau, dG, dH, part, sg, res, yres, Gt, X,
+                sumD, ysum, Wl, kzh, blockIdx.x);
 }
 
 // kw_hunk_mlpb's epilogue: the tile's D alpha / D beta rows out, the partial rows of dV1
@@ -2250,6 +2267,133 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
                   nt, Dal, Dbe, part, sg, tile);
     __syncthreads();
   }
+}
+
+// ---------------------------------------------------------------------------------
+// kw_hunk_fin0/1/2: the one-sweep tiles' (kh_tile<MODE>, hdgnn.hip) block partials summed in
+// a fixed order per node -- row sums over the column blocks, column sums over the row
+// blocks -- the diagonal pair removed (modes 0, 1), then the epilogue of the two-pass kernel
+// the mode replaces (kw_hunk_fwd / kw_hunk_mlpb / kw_hunk_clsb), unchanged.  The sum y e
+// totals (modes 1, 2) go into the row pass's first tile (its epilogue only ever sums them).
+// ---------------------------------------------------------------------------------
+struct HTileSums {
+  const float *rpart, *cpart, *ysp;
+  int CC, RC;
+};
+// row (z = 0) / column (z = 1) sum of node nd, unit k, commit b
+__device__ __forceinline__ float htile_sum(const HTileSums& hs, int z, int b, int Nc, int nd,
+                                           int k) {
+  const int n = z ? hs.RC : hs.CC;
+  const float* p = (z ? hs.cpart : hs.rpart) + ((size_t)b * n * Nc + nd) * H + k;
+  const size_t st = (size_t)Nc * H;
+  float v[8];
+  float a = 0.f;
+  for (int q0 = 0; q0 < n; q0 += 8) {                 // eight partials' loads in flight
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = q0 + u < n ? p[(q0 + u) * st] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
+  }
+  return a;
+}
+__device__ __forceinline__ float htile_ysum(const HTileSums& hs, int b, int k) {
+  const float* p = hs.ysp + (size_t)b * hs.RC * hs.CC * H + k;
+  float a = 0.f;
+  for (int q = 0; q < hs.RC * hs.CC; ++q) a += p[(size_t)q * H];
+  return a;
+}
+
+// kw_hunk_fin0  grid (tc, B, 2): G / H (z = 0 / 1) and sigma / tau
+__global__ __launch_bounds__(NTP) void kw_hunk_fin0(HTileSums hs, const float* __restrict__ D,
+                                                    int Nc, const float* __restrict__ alpha,
+                                                    const float* __restrict__ beta,
+                                                    float* __restrict__ G, float* __restrict__ Hh,
+                                                    float* __restrict__ sig,
+                                                    float* __restrict__ tau) {
+#pragma clang fp contract(off)
+  __shared__ float res[TN * HP];
+  __shared__ float Ml[H * H];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
+  stage_w(Ml, D + D_M, H * H);
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H, nd = t0 + n;
+    float v = 0.f;
+    if (nd < Nc) {
+      const size_t q = ((size_t)b * Nc + nd) * H + k;
+      const float zs = alpha[q] + (0.f * D[D_DLT + k] + beta[q]);   // the tile's z, y = 0
+      v = htile_sum(hs, z, b, Nc, nd, k) - zs * (zs > 0.f ? 1.f : 0.f);
+    }
+    res[n * HP + k] = v;
+  }
+  __syncthreads();
+  float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
+  float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
+  const float* off = D + (z ? D_T0 : D_S0);
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float sacc = 0.f;
+    for (int l = 0; l < H; ++l) sacc = fmaf(res[n * HP + l], Ml[l * H + k], sacc);
+    gout[(t0 + n) * H + k] = res[n * HP + k];
+    sout[(t0 + n) * H + k] = sacc + off[k];
+  }
+}
+
+// kw_hunk_fin1  grid (tc, B, 2): D alpha / D beta and kw_hunk_mlpb's partial rows
+__global__ __launch_bounds__(NTP) void kw_hunk_fin1(HTileSums hs, const float* __restrict__ D,
+                                                    int Nc, const float* __restrict__ alpha,
+                                                    const float* __restrict__ beta,
+                                                    const float* __restrict__ dG,
+                                                    const float* __restrict__ dH,
+                                                    const float* __restrict__ nvec,
+                                                    float* __restrict__ Dal, float* __restrict__ Dbe,
+                                                    float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float res[TN * HP], yres[TN * HP], nt[TN * 4];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H, nd = t0 + n;
+    float v = 0.f;
+    if (nd < Nc) {
+      const size_t q = ((size_t)b * Nc + nd) * H + k;
+      const float zs = alpha[q] + (0.f * D[D_DLT + k] + beta[q]);
+      const float gs = dG[q] + dH[q];
+      v = htile_sum(hs, z, b, Nc, nd, k) - (zs > 0.f ? 1.f : 0.f) * gs;
+    }
+    res[n * HP + k] = v;
+    yres[n * HP + k] = (z == 0 && blockIdx.x == 0 && n == 0) ? htile_ysum(hs, b, k) : 0.f;
+  }
+  __syncthreads();
+  mlpb_epilogue(z, b, t0, tc, Nc, nvec, res, yres, nt, Dal, Dbe, part, sg, blockIdx.x);
+}
+
+// kw_hunk_fin2  grid (tc, B, 2): the classifier backward's sums, then kw_hunk_clsb's epilogue
+__global__ __launch_bounds__(NTP) void kw_hunk_fin2(HTileSums hs, const float* __restrict__ W,
+                                                    Off o, const float* __restrict__ D, int Nc,
+                                                    const float* __restrict__ G,
+                                                    const float* __restrict__ Hh,
+                                                    float* __restrict__ Dsig,
+                                                    float* __restrict__ Dtau, float* __restrict__ dG,
+                                                    float* __restrict__ dH, float* __restrict__ part,
+                                                    Segs sg) {
+#pragma clang fp contract(off)
+  __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
+  __shared__ float X[H * H], sumD[H], ysum[H];
+  __shared__ float Wl[3 * H * H + H];
+  __shared__ float kzh[1];
+  if (threadIdx.x == 0) kzh[0] = 0.f;
+  stage_w(Wl, D + D_M, H * H);
+  stage_w(Wl + H * H, W + o.H1_W2, H * H + H);
+  stage_w(Wl + 2 * H * H + H, W + o.H2_W1 + 2 * H, H * H);
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
+  for (int e = threadIdx.x; e < TN * H; e += NTP) {
+    const int n = e / H, k = e - n * H, nd = t0 + n;
+    res[n * HP + k] = nd < Nc ? htile_sum(hs, z, b, Nc, nd, k) : 0.f;
+    yres[n * HP + k] = (z == 0 && blockIdx.x == 0 && n == 0) ? htile_ysum(hs, b, k) : 0.f;
+  }
+  __syncthreads();
+  clsb_epilogue(z, b, t0, tc, Nc, W, o, D, G, Hh, Dsig, Dtau, dG, dH, part, sg, res, yres, Gt, X,
+                sumD, ysum, Wl, kzh, blockIdx.x);
 }
 
 // kw_dn  grid (tc, B): dn_c[m] = sum_k V1[m][k] Dalpha_c[k] + V1[4+m][k] Dbeta_c[k]
@@ -3461,6 +3605,7 @@ struct WideWork {
   size_t D;                                       // derived weights
   size_t tab;                                     // f64 scan tables [2][B][H][2][Ne+1]
   size_t hsv, hsp, hsx, hsw;                      // sorted hunk tables (hunk_sorted)
+  size_t htr, htc, hty;                           // one-sweep tile partials (hunk_tiled)
   size_t part;                                    // partial rows
   Segs segs;
   size_t total;
@@ -3469,9 +3614,15 @@ struct WideWork {
 // the sorted-threshold form of the hunk relu / mask sums (kw_hunk_sort, _fwd_s, _wsum,
 // _mlpb_s) instead of the dense sweeps (kw_hunk_fwd, kw_hunk_mlpb)
 bool hunk_sorted(const hdg_shape* s) {
-  if (s->flags & HDG_FLAG_HUNK_DENSE) return false;
+  if (s->flags & (HDG_FLAG_HUNK_DENSE | HDG_FLAG_HUNK_TILED)) return false;
   if (s->flags & HDG_FLAG_HUNK_SORTED) return true;
   return s->nc >= HDG_HUNK_SORTED_MIN_NC;
+}
+// the one-sweep tiles (kh_tile + kw_hunk_fin*) for all three hunk pair passes
+bool hunk_tiled(const hdg_shape* s) {
+  if (s->flags & (HDG_FLAG_HUNK_DENSE | HDG_FLAG_HUNK_SORTED)) return false;
+  if (s->flags & HDG_FLAG_HUNK_TILED) return true;
+  return s->nc >= HDG_HUNK_TILED_MIN_NC && !hunk_sorted(s);
 }
 
 // the hunk label id lists (the sorted passes' walks) are part of every general-path
@@ -3509,6 +3660,13 @@ WideWork wide_layout(const hdg_shape* s) {
   w.gam = take(B * Nc * Nc);
   w.D = take(D_WORDS);
   if (has_ent(v) || has_ee(v)) w.tab = take(2 * 2 * B * H * 2 * (Ne + 1));   // doubles
+  if (hunk_tiled(s)) {
+    const size_t CC = (Nc + hunk_tile_cols() - 1) / hunk_tile_cols();
+    const size_t RC = (Nc + hunk_tile_rows() - 1) / hunk_tile_rows();
+    w.htr = take(B * CC * Nc * H);
+    w.htc = take(B * RC * Nc * H);
+    w.hty = take(B * RC * CC * H);
+  }
   if (hunk_sorted(s)) {
     const size_t NcP = (Nc + 3) & ~(size_t)3;
     w.hsv = take(B * 2 * H * NcP);
@@ -3834,8 +3992,10 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                      ent ? F(w.xp) : bt->x, params, o, Ne, Nc, ncpart, ee_fwd_tiles(Ne), F(w.nvec), F(w.alpha),
                      F(w.beta));
   WTRY(kmark("kw_cross_fwd", st));
-  const bool hs = hunk_sorted(s);
+  const bool hs = hunk_sorted(s), ht = hunk_tiled(s);
   const ListLayout YL = ylist_layout(B, Ne, Nc, ent);
+  const HTileSums hts{F(w.htr), F(w.htc), F(w.hty), (Nc + hunk_tile_cols() - 1) / hunk_tile_cols(),
+                      (Nc + hunk_tile_rows() - 1) / hunk_tile_rows()};
   if (hs) {
     const dim3 gw((H + NW - 1) / NW, B, 2);
 #define HDG_SORT(E_)                                                                            \
@@ -3860,6 +4020,13 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                          F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx), prep, YL,
                          F(w.G), F(w.Hh), F(w.sig), F(w.tau));
     WTRY(kmark("kw_hunk_fwd_s", st));
+  } else if (ht) {
+    HTileArgs ha{Nc, F(w.alpha), F(w.beta), nullptr, nullptr, nullptr, D + D_DLT, bt->ybits,
+                 F(w.htr), F(w.htc), F(w.hty)};
+    WTRY(launch_hunk_tile(0, ha, B, st));
+    hipLaunchKernelGGL(kw_hunk_fin0, dim3(tc, B, 2), dim3(NTP), 0, st, hts, D, Nc, F(w.alpha),
+                       F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
+    WTRY(kmark("kw_hunk_fin0", st));
   } else {
     hipLaunchKernelGGL(kw_hunk_fwd, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
                        F(w.alpha), F(w.beta), F(w.G), F(w.Hh), F(w.sig), F(w.tau));
@@ -3884,10 +4051,19 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D, Nc,
                      F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
   WTRY(kmark("kw_hunk_cls", st));
-  hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o, D,
-                     Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig), F(w.Dtau),
-                     F(w.dG), F(w.dH), part, w.segs);
-  WTRY(kmark("kw_hunk_clsb", st));
+  if (ht) {
+    HTileArgs ha{Nc, F(w.sig), F(w.tau), nullptr, nullptr, F(w.gam), D + D_EPS, bt->ybits,
+                 F(w.htr), F(w.htc), F(w.hty)};
+    WTRY(launch_hunk_tile(2, ha, B, st));
+    hipLaunchKernelGGL(kw_hunk_fin2, dim3(tc, B, 2), dim3(NTP), 0, st, hts, params, o, D, Nc,
+                       F(w.G), F(w.Hh), F(w.Dsig), F(w.Dtau), F(w.dG), F(w.dH), part, w.segs);
+    WTRY(kmark("kw_hunk_fin2", st));
+  } else {
+    hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o,
+                       D, Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig),
+                       F(w.Dtau), F(w.dG), F(w.dH), part, w.segs);
+    WTRY(kmark("kw_hunk_clsb", st));
+  }
   if (hs) {
     const dim3 gw((H + NW - 1) / NW, B, 2);
 #define HDG_WSUM(E_)                                                                        \
@@ -3912,6 +4088,13 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                          F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
                          (const double*)F(w.hsw), prep, YL, F(w.Dal), F(w.Dbe), part, w.segs);
     WTRY(kmark("kw_hunk_mlpb_s", st));
+  } else if (ht) {
+    HTileArgs ha{Nc, F(w.alpha), F(w.beta), F(w.dG), F(w.dH), nullptr, D + D_DLT, bt->ybits,
+                 F(w.htr), F(w.htc), F(w.hty)};
+    WTRY(launch_hunk_tile(1, ha, B, st));
+    hipLaunchKernelGGL(kw_hunk_fin1, dim3(tc, B, 2), dim3(NTP), 0, st, hts, D, Nc, F(w.alpha),
+                       F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe), part, w.segs);
+    WTRY(kmark("kw_hunk_fin1", st));
   } else {
     hipLaunchKernelGGL(kw_hunk_mlpb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
                        F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.Dal), F(w.Dbe),

@@ -87,8 +87,14 @@ class CommitBatch:
         Nc = self.y.shape[1]
         assert self.a.shape == (B, Ne, Ne) and self.y.shape == (B, Nc, Nc)
         assert self.hid.shape == (B, Ne) and self.nlen.shape == (B,)
-        for m in (self.a, self.y):         # classes in {0, 1}: two reductions, no np.isin
-            if m.size and (m.max() > 1 or (m.dtype.kind != "u" and m.min() < 0)):
+        for m in (self.a, self.y):         # classes in {0, 1}
+            if not m.size:
+                continue
+            if m.dtype.kind in "uib":      # integer grids: two reductions, no np.isin
+                bad = m.max() > 1 or (m.dtype.kind == "i" and m.min() < 0)
+            else:                          # float grids: exact membership (0.5, NaN fail)
+                bad = not ((m == 0) | (m == 1)).all()
+            if bad:
                 raise ValueError("edge classes must be 0/1")
         if np.any(self.hid < -1) or np.any(self.hid >= Nc):
             raise ValueError("hid entries must be in [-1, Nc)")

@@ -64,7 +64,12 @@ typedef struct hdg_shape {
  * hdg_workspace_bytes follows the choice, so keep the flags fixed for a workspace).      */
 #define HDG_FLAG_HUNK_DENSE 2
 #define HDG_FLAG_HUNK_SORTED 4
-#define HDG_HUNK_SORTED_MIN_NC 0x7fffffff   /* default: dense (the measured crossover) */
+/* HDG_FLAG_HUNK_TILED: the hunk pair passes (relu sums, MLP and classifier mask sums) as
+ * one sweep over blocks of the pair grid giving row and column sums together (the fused
+ * kernel's pair tiles), instead of a row pass and a column pass over every pair.        */
+#define HDG_FLAG_HUNK_TILED 8
+#define HDG_HUNK_SORTED_MIN_NC 0x7fffffff   /* default: never (the measured crossover) */
+#define HDG_HUNK_TILED_MIN_NC 0x7fffffff    /* default: not yet (measured crossover) */
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
  * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge

@@ -87,6 +87,25 @@ def test_synth_shapes_and_ranges():
     assert np.all(cb.nlen <= 200) and np.all(cb.nlen >= 100)
 
 
+@pytest.mark.parametrize("bad", [0.5, np.nan, 2.0, -1.0])
+def test_validate_float_grids_exact_membership(bad):
+    """Float class grids must hold exactly 0/1: a value the u8 upload would truncate to
+    class 0 (0.5, NaN) is rejected, not silently reclassified."""
+    cb = synth_commits(2, 20, 9, 1)
+    for name in ("a", "y"):
+        f = data.CommitBatch(cb.x, cb.a.astype(np.float32), cb.y.astype(np.float32),
+                             cb.hid, cb.nlen)
+        f.validate()                                   # exact 0/1 floats pass
+        getattr(f, name)[1, 3, 4] = bad
+        with pytest.raises(ValueError):
+            f.validate()
+    i = data.CommitBatch(cb.x, cb.a.astype(np.int8), cb.y, cb.hid, cb.nlen)
+    i.validate()
+    i.a[0, 1, 2] = -1
+    with pytest.raises(ValueError):
+        i.validate()
+
+
 def test_layouts_agree():
     assert layout.n_params(2) == olayout.n_params(2) == 2127
     eng = [(n.split(":")[0], s) for n, s in layout.specs(2)]

@@ -303,35 +303,41 @@ def test_max_classes_matches_oracle(v):
     _run_and_check(synth_commits(1, 40, 2048, 4), v, 4)
 
 
-SORTED, DENSE = _lib.FLAG_HUNK_SORTED, _lib.FLAG_HUNK_DENSE
+SORTED, DENSE, TILED = _lib.FLAG_HUNK_SORTED, _lib.FLAG_HUNK_DENSE, _lib.FLAG_HUNK_TILED
+FORMS = pytest.mark.parametrize("form", [SORTED, TILED], ids=["sorted", "tiled"])
 
 
+@FORMS
 @pytest.mark.parametrize("v", [1, 2, 4])
-@pytest.mark.parametrize("B,ne,nc,seed", SHAPES + [(1, 90, 300, 10)])
-def test_hunk_sorted_matches_oracle(v, B, ne, nc, seed):
-    """The sorted-threshold hunk sums (kw_hunk_sort / _fwd_s / _wsum / _mlpb_s), forced on
-    below their default crossover, against the oracle at every tile boundary."""
-    _run_and_check(synth_commits(B, ne, nc, seed), v, seed, GEN, SORTED)
+@pytest.mark.parametrize("B,ne,nc,seed", SHAPES + [(1, 90, 300, 10), (1, 40, 257, 11)])
+def test_hunk_forms_match_oracle(form, v, B, ne, nc, seed):
+    """The general path's other two forms of the hunk pair sums against the oracle at every
+    tile boundary: sorted thresholds (kw_hunk_sort / _fwd_s / _wsum / _mlpb_s) and the
+    one-sweep tiles (kh_tile<0..2> + kw_hunk_fin*: 64-column x 256-row blocks, so Nc = 65,
+    257, 300 cross both block edges)."""
+    _run_and_check(synth_commits(B, ne, nc, seed), v, seed, GEN, form)
 
 
+@FORMS
 @pytest.mark.parametrize("case", ["empty_adjacency", "full_adjacency", "float_attributes",
                                   "all_lines_one_hunk"])
-def test_hunk_sorted_edge_cases(case):
+def test_hunk_forms_edge_cases(form, case):
     """No label pairs, every pair labelled (the correction walk over all Nc - 1 bits, ties
     of equal alpha / beta values across nodes), real-valued attributes."""
-    _run_and_check(EDGE[case](synth_commits(2, 70, 13, 7)), 2, 7, GEN, SORTED)
-    _run_and_check(EDGE[case](synth_commits(1, 40, 300, 7)), 2, 7, GEN, SORTED)
+    _run_and_check(EDGE[case](synth_commits(2, 70, 13, 7)), 2, 7, GEN, form)
+    _run_and_check(EDGE[case](synth_commits(1, 40, 300, 7)), 2, 7, GEN, form)
 
 
+@FORMS
 @pytest.mark.parametrize("nc", [300, 512, 1024])
-def test_hunk_sorted_equals_dense(nc):
-    """The two forms of the general path agree far inside the oracle tolerance (the
-    default switches at HUNK_SORTED_MIN_NC)."""
+def test_hunk_forms_equal_dense(form, nc):
+    """The forms of the general path agree far inside the oracle tolerance (the default
+    picks one by Nc, include/hdgnn.h)."""
     B, ne, v = 1, 64, 2
     cb = synth_commits(B, ne, nc, 21)
     flat = layout.init_flat(4, v)
     outs = []
-    for fl in (DENSE, SORTED):
+    for fl in (DENSE, form):
         eng = _engine(B, ne, nc, v, GEN, fl)
         eng.set_params(flat)
         eng.fwd_bwd(eng.upload(cb))
@@ -349,16 +355,19 @@ def test_hunk_sorted_equals_dense(nc):
     assert _lib.trailer_count(g1[np_:]) == _lib.trailer_count(g2[np_:])
 
 
-def test_hunk_sorted_deterministic_and_garbage_free():
+@FORMS
+def test_hunk_forms_deterministic_and_garbage_free(form):
     B, ne, nc, v = 2, 60, 290, 2
     cb = synth_commits(B, ne, nc, 8)
     flat = layout.init_flat(5, v)
-    ref = _engine(B, ne, nc, v, GEN, SORTED)
+    ref = _engine(B, ne, nc, v, GEN, form)
     ref.set_params(flat)
     db = ref.upload(cb)
     ref.fwd_bwd(db)
     g1, p1 = ref.grad.clone(), ref.probs.clone()
-    dirty = _engine(B, ne, nc, v, GEN, SORTED)
+    ref.fwd_bwd(db)
+    assert torch.equal(g1, ref.grad) and torch.equal(p1, ref.probs)
+    dirty = _engine(B, ne, nc, v, GEN, form)
     dirty.set_params(flat)
     dirty.workspace.fill_(float("nan"))
     dirty.grad.fill_(float("inf"))
