@@ -30,10 +30,11 @@ HBM_PEAK_GBS = 8000.0
 CLOCK_HZ = 2.4e9              # gfx950 peak engine clock (MI355X_MICROARCH.md)
 
 
-def find_profile(variant, path, ne, nc, batch):
+def find_profile(variant, path, ne, nc, batch, hunk="auto"):
     """The newest committed rocprofv3 profile of this exact workload:
     profiles/rNN/<config>/roofline.json (tools/roofline_profile.py) whose config matches
-    (variant, engine path, Ne, Nc, batch per GPU) on the default synthetic data."""
+    (variant, engine path, Ne, Nc, batch per GPU, hunk pair-pass form) on the default
+    synthetic data."""
     pd = os.path.join(ROOT, "profiles")
     rounds = sorted((d for d in os.listdir(pd) if d.startswith("r") and d[1:].isdigit()),
                     reverse=True) if os.path.isdir(pd) else []
@@ -44,16 +45,17 @@ def find_profile(variant, path, ne, nc, batch):
             if os.path.isfile(f):
                 with open(f) as fh:
                     pj = json.load(fh)
-                if {k: pj["config"].get(k) for k in want} == want:
+                if ({k: pj["config"].get(k) for k in want} == want
+                        and pj["config"].get("hunk", "auto") == hunk):
                     return f, pj
     return None, None
 
 
-def build_roofline(dom, kern_ms, variant, path, ne, nc, batch, default_data):
+def build_roofline(dom, kern_ms, variant, path, ne, nc, batch, default_data, hunk="auto"):
     """Roofline of the step's dominant kernel (the longest of the live per-kernel HIP-event
     times) from the committed profile of the same workload: executed FP32 FLOPs per launch
     (calibrated PMC counters) and HBM bytes per launch, over the LIVE average duration."""
-    f, pj = find_profile(variant, path, ne, nc, batch) if default_data else (None, None)
+    f, pj = find_profile(variant, path, ne, nc, batch, hunk) if default_data else (None, None)
     t = kern_ms[dom] * 1e-3
     dense = flops_per_commit(ne, nc, variant) * batch
     r = {"bound": None, "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -358,7 +360,7 @@ def main():
         return
     path_name = {_lib.PATH_FUSED: "fused", _lib.PATH_GENERAL: "general"}[eng.path]
     dom = max(kern_ms, key=kern_ms.get)          # the dominant kernel of the step
-    roofline = build_roofline(dom, kern_ms, v, path_name, ne, nc, B, default_data)
+    roofline = build_roofline(dom, kern_ms, v, path_name, ne, nc, B, default_data, args.hunk)
     e2e = None
     if world == 1 and args.e2e > 0:
         try:                     # a side measurement: never costs the bench line

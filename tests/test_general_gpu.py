@@ -2,10 +2,13 @@
 
 Variants: 1 model_1 HD-GNN/ES (hunk stage on B_1), 2 model_2 HD-GNN/S,
 3 model_3 HD-GNN/E (entity-edge stage computed, unused), 4 model_4 HD-GNN (entity-edge
-probabilities replace E_edge in B_2).  Same tolerances as tests/test_gpu_parity.py:
-logits 1e-4 |ref| + 1e-5 max(1, max|ref|); probs = softmax(logits) to 1e-6; CE rel 1e-5;
-gradients rtol 1e-3 + 1e-4 max|ref| per variable (achieved <= 2.5e-5 max|ref|, at the
-4096-node shape; <= 3.5e-6 at glide); weights after TF-Adam atol 2e-6.
+probabilities replace E_edge in B_2).  Tolerances, set at about 4x the worst error any
+case here reached (profiles/r03/parity_summary.txt):
+  logits  3e-5 |ref| + 3e-6 max(1, max|ref|)   (worst 3.3e-6 max|ref|, 4096 classes)
+  probs = softmax(logits) to 1e-6; CE rel 1e-5
+  gradients  8e-5 |ref| + 8e-6 max|ref| per variable (worst 2.45e-5 |ref| on the largest
+          element at the 4096-node shape; <= 3.5e-6 max|ref| at glide)
+  weights after TF-Adam atol 2e-6.
 """
 import numpy as np
 import pytest
@@ -21,6 +24,8 @@ from tests import _errlog
 pytestmark = pytest.mark.gpu
 
 GEN = _lib.PATH_GENERAL
+LOGIT_RTOL, LOGIT_ATOL = 3e-5, 3e-6       # x |ref|, x max(1, max|ref|) of the commit
+GRAD_RTOL, GRAD_ATOL = 8e-5, 8e-6         # x |ref|, x max|ref| of the variable
 
 
 def _keys(v):
@@ -52,7 +57,7 @@ def _reg_grad(flat):
 def _check_outputs(logits, probs, out):
     ref = out["logits"].transpose(0, 2, 1)
     scale = np.maximum(1.0, np.abs(ref).reshape(ref.shape[0], -1).max(1))[:, None, None]
-    tol = 1e-4 * np.abs(ref) + 1e-5 * scale
+    tol = LOGIT_RTOL * np.abs(ref) + LOGIT_ATOL * scale
     err = np.abs(logits - ref)
     _errlog.record("logits", (err / scale).max(), (err / tol).max())
     assert np.all(err <= tol), "logits: max err %.3g" % err.max()
@@ -67,7 +72,7 @@ def _grad_close(g_eng, g_ref, v):
         n = int(np.prod(shape))
         a, r = g_eng[o:o + n], g_ref[o:o + n]
         scale = max(np.abs(r).max(), 1e-12)
-        tol = 1e-3 * np.abs(r) + 1e-4 * scale + 1e-9
+        tol = GRAD_RTOL * np.abs(r) + GRAD_ATOL * scale + 1e-9
         err = np.abs(a - r)
         _errlog.record("grad:" + name, err.max() / scale, (err / tol).max())
         if not np.all(err <= tol):

@@ -1,13 +1,15 @@
 """HIP engine (via the C ABI) vs the CPU oracle.  Runs on the MI355X box only.
 
 Tolerances (fp32 engine vs float64 oracle; SURVEY 8(d) made scale-aware):
-  logits   |d| <= 1e-4 |ref| + 1e-5 * max(1, max_commit |ref|)   -- untrained random-init
+  Set at about 4-6x the worst error any case here reached (profiles/r03/parity_summary.txt):
+  logits   |d| <= 1.5e-5 |ref| + 1.5e-6 * max(1, max_commit |ref|)   -- untrained random-init
            logits reach |z| ~ 3e3 at glide sizes, where a fixed 1e-5 is below fp32 resolution
+           (worst 7.9e-7 max|ref|)
   probs    == softmax(engine logits) to 1e-6, and vs oracle |d| <= 0.5 * logit tolerance
   CE, loss_map, loss_para, train_loss: rel 1e-5
-  gradients rtol 1e-3, atol 2e-5 * max|ref| of the variable (SURVEY 8(d) says atol 1e-6;
+  gradients rtol 1.5e-4, atol 3e-6 * max|ref| of the variable (SURVEY 8(d) says atol 1e-6;
            the scale-relative form because the variables' gradients span 1e-4 .. 1e1.
-           Achieved: <= 3.0e-6 * max|ref| over every case here)
+           Achieved: <= 2.9e-6 * max|ref| over every case here)
   weights after TF-Adam steps: atol 2e-6 (lr 3e-4 per step)
 """
 import numpy as np
@@ -55,7 +57,7 @@ def _reg_grad(flat):
 
 def _logit_tol(ref):
     scale = np.maximum(1.0, np.abs(ref).reshape(ref.shape[0], -1).max(1))[:, None, None]
-    return 1e-4 * np.abs(ref) + 1e-5 * scale
+    return 1.5e-5 * np.abs(ref) + 1.5e-6 * scale
 
 
 def _check_outputs(logits, probs, out):
@@ -73,7 +75,7 @@ def _check_outputs(logits, probs, out):
     assert np.all(perr <= 0.5 * tol + 1e-6), "probs: max err %.3g" % perr.max()
 
 
-def _grad_close(g_eng, g_ref, rtol=1e-3, atol_rel=2e-5):
+def _grad_close(g_eng, g_ref, rtol=1.5e-4, atol_rel=3e-6):
     bad = []
     for name, (o, shape) in layout.offsets(2).items():
         n = int(np.prod(shape))

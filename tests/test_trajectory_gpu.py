@@ -7,7 +7,7 @@ kernel + fused reduce / TF Adam, model_2.py:336-338, 369-383).  Two checks per p
 1. Every step, teacher-forced.  Before each engine step the test reads the engine's
    weights, Adam slots and beta powers; the oracle predicts that step from exactly that
    state (oracle.model_ref.loss_and_grads in float64 + AdamTF, the restated ApplyAdam).
-   After the step:  |w - w_pred| <= 1e-3 lr + 2 ulp(w)   (a thousandth of one Adam step,
+   After the step:  |w - w_pred| <= 3e-4 lr + 2 ulp(w)   (a 3000th of one Adam step,
    plus the float32 rounding of the stored weight), and the pre-update losses rel 3e-5
    (CE falls from ~100 to ~3 while the logits stay ~1e3: the loss loses relative digits
    as training proceeds).  Achieved: <= 1.3e-4 lr and 8.9e-6 over all 50 steps.
@@ -96,7 +96,7 @@ def test_adam_trajectory_50_steps(v, path):
         opt.b1p, opt.b2p = np.float32(bp[0]), np.float32(bp[1])
         wp = opt.step(w0, g)
         ulp = np.spacing(np.abs(wp).astype(np.float32)).astype(np.float64)
-        step_err.append(float((np.abs(w1 - wp) / (1e-3 * lr + 2 * ulp)).max()))
+        step_err.append(float((np.abs(w1 - wp) / (3e-4 * lr + 2 * ulp)).max()))
         ref = np.array([float(out[k]) for k in LOSSES])
         loss_tf.append(np.abs(st[:4] - ref) / np.abs(ref))
         # the count may differ only on pairs whose logit difference is within the logit
@@ -114,7 +114,7 @@ def test_adam_trajectory_50_steps(v, path):
     w_eng = eng.get_params().astype(np.float64)
     loss_tf, loss_free = np.asarray(loss_tf), np.asarray(loss_free)
 
-    _errlog.record("teacher_step_update", max(step_err) * 1e-3, max(step_err),
+    _errlog.record("teacher_step_update", max(step_err) * 3e-4, max(step_err),
                    note="err_over_scale in units of lr")
     ltol = 3e-2 if v == 4 else 1e-2
     _errlog.record("teacher_losses", loss_tf.max(), loss_tf.max() / 3e-5)
@@ -139,7 +139,7 @@ def test_adam_trajectory_50_steps(v, path):
                    tolerance="2 lr" if v == 4 else "1e-3 |w| + 1e-3 lr steps")
 
     assert moved > 1e-3                                   # the weights did train
-    assert max(step_err) <= 1.0, "teacher-forced step error %.3g x (1e-3 lr + 2 ulp)" % max(step_err)
+    assert max(step_err) <= 1.0, "teacher-forced step error %.3g x (3e-4 lr + 2 ulp)" % max(step_err)
     assert np.all(loss_tf <= 3e-5), "teacher-forced losses: max rel err %.3g" % loss_tf.max()
     assert not any(cnt_bad), "top_ACC counts differ on %d steps" % sum(cnt_bad)
     assert np.all(loss_free <= ltol), "free-run losses: max rel err %.3g" % loss_free.max()

@@ -3,7 +3,7 @@
 #   tools/profile_config.sh <round>/<tag> [bench.py args ...]
 # writes gpurun_out/<round>/<tag>/: a kernel trace + stats of the bench command (HIP-graph
 # replay, as the bench line runs), then one --pmc pass each (eager launches): FETCH_SIZE,
-# WRITE_SIZE, SQ issue / wait counters, FP32 FLOP counters.  Summarise locally with
+# WRITE_SIZE, SQ issue / wait counters, LDS bank conflicts, FP32 FLOP counters.  Summarise locally with
 #   python tools/roofline_profile.py gpurun_out/<round>/<tag> profiles/<round>/<tag> [bench args]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -28,6 +28,8 @@ pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE
 pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
+pmc lds SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_INSTS_VMEM_RD \
+    SQ_INSTS_VMEM_WR SQ_INSTS_SALU
 pmc flops SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_MFMA_MOPS_F32 \
     SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 \
     SQ_INSTS_VALU

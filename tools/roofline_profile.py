@@ -81,11 +81,13 @@ def calibration(src, dst):
 
 
 def parse_args(argv):
-    cfg = {"variant": 2, "ne": 200, "nc": 74, "batch": 100, "path": None}
+    cfg = {"variant": 2, "ne": 200, "nc": 74, "batch": 100, "path": None, "hunk": "auto"}
     it = iter(argv)
     for a in it:
         if a in ("--variant", "--ne", "--nc", "--batch"):
             cfg[a[2:]] = int(next(it))
+        elif a == "--hunk":
+            cfg["hunk"] = next(it)
         elif a == "--path":
             cfg["path"] = {"0": None, "1": "fused", "2": "general"}[next(it)]
     return cfg
@@ -126,6 +128,7 @@ def main(src, dst, argv):
     tr, fe, wr = stats(os.path.join(src, "trace")), pmc(os.path.join(src, "fetch")), \
         pmc(os.path.join(src, "write"))
     sq, fl = pmc(os.path.join(src, "sq")), pmc(os.path.join(src, "flops"))
+    ld = pmc(os.path.join(src, "lds"))
     kernels = {}
     for k in sorted(set(tr) | set(fe) | set(sq)):
         if k.startswith("__amd") or "at::native" in k or k.startswith("at::"):
@@ -146,6 +149,11 @@ def main(src, dst, argv):
             if s.get("SQ_WAVE_CYCLES"):
                 e["wait_any_frac"] = round(s.get("SQ_WAIT_ANY", 0) / s["SQ_WAVE_CYCLES"], 4)
                 e["active_inst_frac"] = round(s.get("SQ_ACTIVE_INST_ANY", 0) / s["SQ_WAVE_CYCLES"], 4)
+        lq = ld.get(k, {})
+        if lq.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_bank_conflict_frac"] = round(lq.get("SQ_LDS_BANK_CONFLICT", 0)
+                                                / lq["SQ_LDS_IDX_ACTIVE"], 4)
+            e["vmem_rd_wave_insts"] = lq.get("SQ_INSTS_VMEM_RD")
         f = fl.get(k, {})
         if f:
             e["executed_flops"] = (64 * f.get("SQ_INSTS_VALU_FLOPS_FP32", 0)
@@ -168,21 +176,24 @@ def main(src, dst, argv):
         with open(f) as a, open(os.path.join(dst, "kernel_stats.csv"), "w") as b:
             b.write(a.read())
     with open(os.path.join(dst, "pmc_medians.json"), "w") as fh:
-        json.dump({"fetch": fe, "write": wr, "sq": sq, "flops": fl}, fh, indent=1, sort_keys=True)
+        json.dump({"fetch": fe, "write": wr, "sq": sq, "flops": fl, "lds": ld}, fh, indent=1,
+                  sort_keys=True)
     with open(os.path.join(dst, "roofline.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     rows = ["# %s  config %s" % (os.path.relpath(dst, ROOT), json.dumps(cfg)),
             "# avg_us: rocprofv3 kernel-trace (graph replay); HBM MB per launch: " + note,
-            "%-16s %6s %9s %9s %9s %9s %8s %8s %8s %7s" % (
+            "# issue: VALU wave-instructions / chip issue slots; wait: SQ_WAIT_ANY / wave cycles; "
+            "ldsc: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE",
+            "%-16s %6s %9s %9s %9s %9s %8s %8s %8s %7s %6s" % (
                 "kernel", "calls", "avg_us", "hbm_MB", "lo_MB", "hi_MB", "TB/s", "TFLOP/s",
-                "issue", "wait")]
+                "issue", "wait", "ldsc")]
     tot = sum(e.get("total_us", 0) for e in kernels.values())
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1].get("total_us", 0)):
-        rows.append("%-16s %6s %9.2f %9.2f %9.2f %9.2f %8.3f %8.2f %8.3f %7.3f" % (
+        rows.append("%-16s %6s %9.2f %9.2f %9.2f %9.2f %8.3f %8.2f %8.3f %7.3f %6.3f" % (
             k[:16], e.get("calls", "-"), e.get("avg_us", 0), e.get("hbm_bytes", 0) / 1e6,
             e.get("hbm_bytes_lower", 0) / 1e6, e.get("hbm_bytes_upper", 0) / 1e6,
             e.get("hbm_tbs", 0), e.get("tflops", 0), e.get("issue_frac_chip", 0),
-            e.get("wait_any_frac", 0)))
+            e.get("wait_any_frac", 0), e.get("lds_bank_conflict_frac", 0)))
     rows.append("# total kernel time in the trace %.1f us" % tot)
     if line:
         rows.append("# bench line: %s commits/s, %s ms/step" % (line["value"], line["ms_per_step"]))
