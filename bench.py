@@ -240,8 +240,9 @@ def main():
     ap.add_argument("--path", type=int, default=0, choices=(0, 1, 2),
                     help="engine path: 0 auto, 1 fused, 2 general (include/hdgnn.h)")
     ap.add_argument("--hunk", default="auto", choices=("auto", "dense", "sorted", "tiled"),
-                    help="general path's hunk relu / mask sums: the default crossover "
-                         "(include/hdgnn.h HDG_HUNK_SORTED_MIN_NC), or forced dense / sorted")
+                    help="general path's hunk pair sums: the automatic form by Nc (include/hdgnn.h "
+                         "HDG_HUNK_SORTED_MIN_NC / HDG_HUNK_TILED_MIN_NC), or forced dense / "
+                         "sorted / tiled")
     ap.add_argument("--edensity", type=float, default=0.05,
                     help="synthetic entity-adjacency density (data-dependence runs)")
     ap.add_argument("--hdensity", type=float, default=0.10,

@@ -56,6 +56,24 @@ constexpr double FIX = 4294967296.0;   // 2^32 fixed-point scale of the hunk bin
 __device__ __forceinline__ float relu(float v) { return fmaxf(v, 0.f); }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Wave time stamps of one kernel (timing builds only: -DHDG_WSTAMP=<kernel id>, read by
+// tools/wstamp.py through hdg_wstamp_set): 8 s_memrealtime slots (100 MHz) per wave,
+// [block (x fastest)][wave][slot], lane 0 of the wave storing.
+#ifdef HDG_WSTAMP
+__device__ unsigned long long* g_wst;
+#define WSTAMP(kid, k)                                                                      \
+  do {                                                                                      \
+    if constexpr (HDG_WSTAMP == (kid)) {                                                    \
+      if ((threadIdx.x & 63) == 0 && g_wst)                                                 \
+        g_wst[(((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) *  \
+                   (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] =                    \
+            __builtin_amdgcn_s_memrealtime();                                               \
+    }                                                                                       \
+  } while (0)
+#else
+#define WSTAMP(kid, k) do {} while (0)
+#endif
+
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -1774,9 +1792,23 @@ __host__ __device__ inline size_t hsort_tab(int b, int side, int k, int len) {
   return (((size_t)b * 2 + side) * H + k) * (size_t)len;
 }
 
-// kw_hunk_sort  grid (H, B, 2), NT threads, dynamic LDS 8 * pow2(Nc) bytes: bitonic sort
-// of 64-bit keys (order-preserving bits of the value, node index below: ties by node, so
-// every table is deterministic), then f64 suffix sums of the values
+// XCD-aware block map of a (T, B, 2) grid: blocks are dealt to the 8 XCDs round robin by
+// linear id, so the blocks of commit b all land on XCD b % 8 when B % 8 == 0 -- the sorted
+// tables one kernel writes are then read by the next from the same L2 (else identity)
+__device__ __forceinline__ void xcd_commit_map(int& t, int& b, int& z) {
+  const int T = gridDim.x, B = gridDim.y;
+  if (B & 7) {
+    t = blockIdx.x; b = blockIdx.y; z = blockIdx.z;
+    return;
+  }
+  const int L = blockIdx.x + T * (blockIdx.y + B * blockIdx.z);
+  const int s = L >> 3, per = 2 * T, bq = s / per, r = s - bq * per;
+  b = 8 * bq + (L & 7);
+  z = r / T;
+  t = r - z * T;
+}
+
+// sort keys: order-preserving u32 bits of a float value
 __device__ __forceinline__ uint32_t fkey(float v) {   // monotone float -> u32 (no NaN here)
   const uint32_t u = __float_as_uint(v);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -1785,26 +1817,6 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// inclusive f64 sum over the block's threads in thread order (NT threads): each thread
-// gets the sum of the chunks of the threads before it ("above" its own slots)
-__device__ __forceinline__ double block_excl(double a, double* cs) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double inc = a;
-#pragma unroll
-  for (int o2 = 1; o2 < 64; o2 <<= 1) {
-    const double u = __shfl_up(inc, o2);
-    if (lane >= o2) inc += u;
-  }
-  if (lane == 63) cs[w] = inc;
-  __syncthreads();
-  double base = 0.0;
-  for (int u = 0; u < w; ++u) base += cs[u];
-  return base + (inc - a);
-}
-
-// One wave per table: the Nc keys (padded to NP2 = 64 E with max keys) held E per lane,
-// element e = 64 i + lane in register i.  Bitonic network: partners at distance >= 64 are
-// registers of the same lane, below 64 lanes of the same register (shuffles).
 // the value of lane ^ ST (ST < 64) without the LDS crossbar where the VALU can: permlane
 // swaps for 32 / 16, DPP for 8 (row_ror:8 = lane ^ 8 in a 16-lane row), 2, 1 (quad_perm);
 // ds_swizzle (xor mode) for 4
@@ -1835,104 +1847,72 @@ __device__ __forceinline__ unsigned long long xlane64(unsigned long long v, int 
   return ((unsigned long long)hi << 32) | lo;
 }
 
+// Block-wide bitonic network: 4 waves per table, element e = 64 E w + 64 i + lane (wave w,
+// register i).  Distances below 64 are lanes (xlane), below 64 E registers of the lane,
+// from 64 E on partners in another wave (through LDS, two barriers per stage).  The
+// sort direction of element e at merge level LEN is (e & LEN) == 0.
 template <int ST, int LEN, int E>
-__device__ __forceinline__ void bitonic_xstage(unsigned long long (&k)[E], int lane) {
+__device__ __forceinline__ void bs_lane(unsigned long long (&k)[E], int lane, int eb) {
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const int e = 64 * i + lane;
-    const bool up = (e & LEN) == 0;
+    const bool up = ((eb + 64 * i + lane) & LEN) == 0;
     const unsigned long long o = xlane64<ST>(k[i], lane);
-    const bool lower = (lane & ST) == 0;          // this lane holds the lower slot
-    const bool keep_min = lower == up;
-    const bool lt = k[i] < o;
-    k[i] = (lt == keep_min) ? k[i] : o;
+    const bool keep_min = ((lane & ST) == 0) == up;
+    k[i] = ((k[i] < o) == keep_min) ? k[i] : o;
   }
 }
-
-template <int LEN, int E>
-__device__ __forceinline__ void bitonic_xstages(unsigned long long (&k)[E], int lane) {
-  // the cross-lane distances of one merge level, highest first
-  if constexpr (LEN > 32) bitonic_xstage<32, LEN, E>(k, lane);
-  if constexpr (LEN > 16) bitonic_xstage<16, LEN, E>(k, lane);
-  if constexpr (LEN > 8) bitonic_xstage<8, LEN, E>(k, lane);
-  if constexpr (LEN > 4) bitonic_xstage<4, LEN, E>(k, lane);
-  if constexpr (LEN > 2) bitonic_xstage<2, LEN, E>(k, lane);
-  bitonic_xstage<1, LEN, E>(k, lane);
-}
-
-template <int LEN, int E>
-__device__ __forceinline__ void bitonic_level(unsigned long long (&k)[E], int lane) {
-  // register distances (>= 64) first, then the lane distances
+template <int ST, int LEN, int E>
+__device__ __forceinline__ void bs_reg(unsigned long long (&k)[E], int lane, int eb) {
+  constexpr int rs = ST >> 6;
 #pragma unroll
-  for (int st = LEN >> 1; st >= 64; st >>= 1) {
-    const int rs = st >> 6;
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-      if (i & rs) continue;
-      const int e = 64 * i + lane;
-      const bool up = (e & LEN) == 0;
-      const unsigned long long a = k[i], c = k[i + rs];
-      const bool sw = (a > c) == up;
-      k[i] = sw ? c : a;
-      k[i + rs] = sw ? a : c;
-    }
-  }
-  bitonic_xstages<LEN, E>(k, lane);
-}
-
-template <int LEN, int E>
-__device__ __forceinline__ void bitonic_from(unsigned long long (&k)[E], int lane) {
-  bitonic_level<LEN, E>(k, lane);
-  if constexpr (LEN < 64 * E) bitonic_from<2 * LEN, E>(k, lane);
-}
-
-template <int E>
-__device__ __forceinline__ void wave_bitonic(unsigned long long (&k)[E], int lane) {
-  bitonic_from<2, E>(k, lane);
-}
-
-template <int E>
-__device__ __forceinline__ void wave_bitonic_shfl(unsigned long long (&k)[E], int lane) {
-  constexpr int N = 64 * E;
-#pragma unroll
-  for (int len = 2; len <= N; len <<= 1) {
-#pragma unroll
-    for (int st = len >> 1; st > 0; st >>= 1) {
-      if (st >= 64) {
-        const int rs = st >> 6;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-          if (i & rs) continue;
-          const int e = 64 * i + lane;
-          const bool up = (e & len) == 0;
-          const unsigned long long a = k[i], c = k[i + rs];
-          const bool sw = (a > c) == up;
-          k[i] = sw ? c : a;
-          k[i + rs] = sw ? a : c;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-          const int e = 64 * i + lane;
-          const bool up = (e & len) == 0;
-          const unsigned long long o = __shfl_xor(k[i], st);
-          const bool lower = (lane & st) == 0;       // this lane holds the lower slot
-          const unsigned long long mn = k[i] < o ? k[i] : o, mx = k[i] < o ? o : k[i];
-          k[i] = (lower == up) ? mn : mx;
-        }
-      }
-    }
+  for (int i = 0; i < E; ++i) {
+    if (i & rs) continue;
+    const bool up = ((eb + 64 * i + lane) & LEN) == 0;
+    const unsigned long long a = k[i], c = k[i + rs];
+    const bool sw = (a > c) == up;
+    k[i] = sw ? c : a;
+    k[i + rs] = sw ? a : c;
   }
 }
+template <int ST, int LEN, int E>
+__device__ __forceinline__ void bs_cross(unsigned long long (&k)[E], int lane, int eb,
+                                         unsigned long long* sh) {
+#pragma unroll
+  for (int i = 0; i < E; ++i) sh[eb + 64 * i + lane] = k[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = eb + 64 * i + lane;
+    const unsigned long long o = sh[e ^ ST];
+    const bool keep_min = ((e & ST) == 0) == ((e & LEN) == 0);
+    k[i] = ((k[i] < o) == keep_min) ? k[i] : o;
+  }
+  __syncthreads();
+}
+template <int LEN, int ST, int E>
+__device__ __forceinline__ void bs_stages(unsigned long long (&k)[E], int lane, int eb,
+                                          unsigned long long* sh) {
+  if constexpr (ST >= 64 * E) bs_cross<ST, LEN, E>(k, lane, eb, sh);
+  else if constexpr (ST >= 64) bs_reg<ST, LEN, E>(k, lane, eb);
+  else bs_lane<ST, LEN, E>(k, lane, eb);
+  if constexpr (ST > 1) bs_stages<LEN, ST / 2, E>(k, lane, eb, sh);
+}
+template <int LEN, int E>
+__device__ __forceinline__ void bs_sort(unsigned long long (&k)[E], int lane, int eb,
+                                        unsigned long long* sh) {
+  bs_stages<LEN, LEN / 2, E>(k, lane, eb, sh);
+  if constexpr (LEN < 256 * E) bs_sort<2 * LEN, E>(k, lane, eb, sh);
+}
 
-// suffix sums over the wave's strided elements (e = 64 i + lane): out(e, sum_{r >= e} v_r),
-// register i from the top with the higher registers' total carried in
+// block-wide suffix sums over the elements e = 64 E w + 64 i + lane: out(e, sum_{r >= e} v_r)
+// (each wave's chunk in registers, then the higher waves' chunk totals through LDS)
 template <int E, class V, class O>
-__device__ __forceinline__ void wave_suffix(int lane, int n, V val, O out) {
+__device__ __forceinline__ void block_suffix(int lane, int w, int n, V val, O out, double* tot) {
+  double sfx[E];
   double carry = 0.0;
 #pragma unroll
   for (int i = E - 1; i >= 0; --i) {
-    const int e = 64 * i + lane;
+    const int e = 64 * E * w + 64 * i + lane;
     double v = e < n ? val(i) : 0.0;
 #pragma unroll
     for (int o2 = 1; o2 < 64; o2 <<= 1) {
@@ -1940,77 +1920,101 @@ __device__ __forceinline__ void wave_suffix(int lane, int n, V val, O out) {
       if (lane + o2 < 64) v += u;
     }
     v += carry;
-    if (e < n) out(e, v);
+    sfx[i] = v;
     carry = __shfl(v, 0);
+  }
+  if (lane == 0) tot[w] = carry;
+  __syncthreads();
+  double hi = 0.0;
+  for (int u = NW - 1; u > w; --u) hi += tot[u];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = 64 * E * w + 64 * i + lane;
+    if (e < n) out(e, sfx[i] + hi);
   }
 }
 
+// kw_hunk_sort  grid (H, B, 2), one 4-wave block per table (side, unit): the 64-bit keys
+// (order-preserving value bits, node index below: ties by node, every table deterministic)
+// sorted by the block-wide network, then f64 suffix sums of the values.  E = pow2(Nc) / 256
+// per lane (at least 1).
 template <int E>
 __global__ __launch_bounds__(NT) void kw_hunk_sort(const float* __restrict__ alpha,
                                                    const float* __restrict__ beta, int Nc,
                                                    float* __restrict__ sv, int* __restrict__ sp,
                                                    double* __restrict__ sx) {
-  const int lane = threadIdx.x & 63;
-  const int k = blockIdx.x * NW + uni(threadIdx.x >> 6), b = blockIdx.y, side = blockIdx.z;
-  if (k >= H) return;                             // wave-uniform, no barriers
-  const int NcP = (Nc + 3) & ~3;
+  __shared__ unsigned long long sh[256 * E];
+  __shared__ double tot[NW];
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  int k, b, side;
+  xcd_commit_map(k, b, side);
+  WSTAMP(1, 0);
+  const int NcP = (Nc + 3) & ~3, eb = 64 * E * w;
   const float* src = (side ? alpha : beta) + (size_t)b * Nc * H + k;
   unsigned long long key[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const int e = 64 * i + lane;
+    const int e = eb + 64 * i + lane;
     const uint32_t kv = e < Nc ? fkey(src[(size_t)(e < Nc ? e : 0) * H]) : 0xffffffffu;
     key[i] = ((unsigned long long)kv << 32) | (uint32_t)e;
   }
-  wave_bitonic<E>(key, lane);
+  WSTAMP(1, 1);
+  bs_sort<2, E>(key, lane, eb, sh);
+  WSTAMP(1, 2);
   const size_t tb = hsort_tab(b, side, k, NcP), tx = hsort_tab(b, side, k, NcP + 1);
   float val[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const int e = 64 * i + lane;
+    const int e = eb + 64 * i + lane;
     val[i] = fkey_inv((uint32_t)(key[i] >> 32));
     if (e < Nc) {
       sv[tb + e] = val[i];
       sp[tb + e] = (int)(key[i] & 0xffffffffu);
     }
   }
-  if (lane == 0) sx[tx + Nc] = 0.0;
-  wave_suffix<E>(lane, Nc, [&](int i) { return (double)val[i]; },
-                 [&](int e, double v) { sx[tx + e] = v; });
+  if (threadIdx.x == 0) sx[tx + Nc] = 0.0;
+  WSTAMP(1, 3);
+  block_suffix<E>(lane, w, Nc, [&](int i) { return (double)val[i]; },
+                  [&](int e, double v) { sx[tx + e] = v; }, tot);
+  WSTAMP(1, 4);
 }
 
-// kw_hunk_wsum  grid (H / 4, B, 2), one wave per table: sw[m] = sum_{r >= m} w[sp[r]][k],
+// kw_hunk_wsum  grid (H, B, 2), one 4-wave block per table: sw[m] = sum_{r >= m} w[sp[r]][k],
 // side 0: w = dH, 1: dG
 template <int E>
 __global__ __launch_bounds__(NT) void kw_hunk_wsum(const int* __restrict__ sp,
                                                    const float* __restrict__ dG,
                                                    const float* __restrict__ dH, int Nc,
                                                    double* __restrict__ sw) {
-  const int lane = threadIdx.x & 63;
-  const int k = blockIdx.x * NW + uni(threadIdx.x >> 6), b = blockIdx.y, side = blockIdx.z;
-  if (k >= H) return;
-  const int NcP = (Nc + 3) & ~3;
+  __shared__ double tot[NW];
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  int k, b, side;
+  xcd_commit_map(k, b, side);
+  const int NcP = (Nc + 3) & ~3, eb = 64 * E * w;
   const float* wv = (side ? dG : dH) + (size_t)b * Nc * H + k;
   const int* pm = sp + hsort_tab(b, side, k, NcP);
   double* T = sw + hsort_tab(b, side, k, NcP + 1);
-  float v[E];
+  WSTAMP(4, 0);
   int id[E];
+  float v[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const int e = 64 * i + lane;
+    const int e = eb + 64 * i + lane;
     id[i] = pm[e < Nc ? e : 0];
   }
 #pragma unroll
   for (int i = 0; i < E; ++i) v[i] = wv[(size_t)id[i] * H];
-  if (lane == 0) T[Nc] = 0.0;
-  wave_suffix<E>(lane, Nc, [&](int i) { return (double)v[i]; },
-                 [&](int e, double x) { T[e] = x; });
+  if (threadIdx.x == 0) T[Nc] = 0.0;
+  WSTAMP(4, 1);
+  block_suffix<E>(lane, w, Nc, [&](int i) { return (double)v[i]; },
+                  [&](int e, double x) { T[e] = x; }, tot);
+  WSTAMP(4, 2);
 }
 
-// E = elements per lane of the one-wave sort: pow2(Nc) / 64, at least 2
+// E = elements per lane of the block sort: pow2(Nc) / 256, at least 1
 inline int hsort_e(int Nc) {
-  int e = 2;
-  while (64 * e < Nc) e <<= 1;
+  int e = 1;
+  while (256 * e < Nc) e <<= 1;
   return e;
 }
 
@@ -2022,25 +2026,38 @@ __device__ __forceinline__ int upper_slot(const float* __restrict__ sv, int Nc, 
   return m;
 }
 
-// The sorted passes run 8 waves over 128 nodes (two 64-node halves); wave w takes half
-// w >> 2 and hidden units [5 (w & 3), +5).  With STAGE (Nc <= HS_STAGE_MAX) the block stages
-// the sorted values of all 20 units and the swept side's node vectors (and weights) in LDS
-// (16-byte copies, every load of a thread issued before its first LDS store): the binary
-// searches and the label walks then wait on LDS, not on one dependent L2 round trip per step
-// / pair.  The walks read the node's label id list (ylist_layout) four ids per 8-byte load.
-constexpr int HSN = 128;                  // nodes per block
-constexpr int HS_STAGE_MAX = 512;
+// The sorted passes stage their tables in LDS (every load of a thread issued before its
+// first LDS store): the binary searches and the label walks then wait on LDS, not on one
+// dependent L2 round trip per step / pair.  Two block shapes:
+//   Nc <= HS_ALL_MAX: 8 waves over 128 nodes (two 64-node halves), wave w takes half w >> 2
+//     and hidden units [5 (w & 3), +5); the block stages all 20 units' tables, so the four
+//     unit groups of a node share its label list (L1 hits) and sigma / tau close in-block.
+//   larger Nc (up to the engine's 2048): one block per (256-node tile, unit group g of 5
+//     units), 4 waves, lane = node, staging only its group's tables (88 / 120 KiB at Nc =
+//     2048, where all 20 units no longer fit); sigma / tau follow in kw_hunk_sig.
+// The walks read the node's label id list (ylist_layout) four ids per 8-byte load, all of a
+// lane's groups (up to HS_LB) in flight at once.
+//   Walk rows in LDS: lane l reads the row of its own label q, so the 32 lanes of an LDS lane
+// group address random rows.  Rows of 20 floats put every row start on one of 8 banks (20 q
+// mod 32): 4-8-way conflicts on each 4-byte read, which made the walk LDS-bound
+// (tools/wstamp.py: 30.6 of mlpb_s's 46 us at 1024x512).  Rows are staged per unit group g
+// as 5 values + 1 pad (fwd) or 5 (value, weight) pairs (mlpb), node strides 26 / 42 (all
+// units) or 6 / 10 (one group): 8-byte reads (64 banks, 2 per read) whose row starts take 32
+// distinct bank pairs, three / five reads per label.
+constexpr int HSN = 128;                  // nodes per block, all-unit shape
+constexpr int HS_ALL_MAX = 512;           // largest Nc of the all-unit shape
+constexpr int HS_OSF = 26, HS_OSB = 42;   // all-unit walk-row strides (floats), fwd / mlpb
+constexpr int HSG = 256;                  // nodes per block, group shape
+constexpr int HS_NC_MAX = 2048;
+constexpr int HS_RSF = 6, HS_RSB = 10;    // group walk-row strides, fwd / mlpb
+constexpr int HS_LB = 8;                  // label id groups (4 ids each) in flight per lane
+constexpr int RS5 = KPW + 1;              // [node][unit] result rows of a group
 __host__ __device__ inline size_t hs_lds_bytes(int Nc, int nvec) {   // nvec: 1 (fwd) / 2 (mlpb)
   const size_t NcP = (Nc + 3) & ~3;
-  return ((size_t)H * NcP + (size_t)H * Nc * nvec) * 4;
+  if (Nc <= HS_ALL_MAX) return ((size_t)H * NcP + (size_t)Nc * (nvec == 1 ? HS_OSF : HS_OSB)) * 4;
+  return ((size_t)KPW * NcP + (size_t)Nc * (nvec == 1 ? HS_RSF : HS_RSB)) * 4;
 }
-
-struct HsView {
-  const float* sv;      // [H][svs]: the sorted values (LDS or the global tables)
-  int svs;
-  const float* oth;     // [Nc][H]
-  const float* woth;    // [Nc][H] (mlpb)
-};
+__host__ __device__ inline int hs_tiles(int Nc) { return (Nc + HSG - 1) / HSG; }
 
 // copy n16 16-byte words src -> dst with every load of the thread in flight first
 template <int U>
@@ -2061,37 +2078,119 @@ __device__ __forceinline__ void copy16(float4* __restrict__ dst, const float4* _
   }
 }
 
-template <bool STAGE>
-__device__ __forceinline__ HsView hs_stage(int z, int b, int Nc, const float* sv_g,
-                                           const float* oth_g, const float* woth_g, void* lds) {
+// all-unit shape: stage the 20 sorted tables sv [H][NcP], then [Nc][H] node vectors (and
+// weights) into the walk-row layout, 4 float4 loads (per table) of a thread in flight
+template <int NV>
+__device__ __forceinline__ void hs_stage_all(int z, int b, int Nc, const float* __restrict__ sv_g,
+                                             const float* __restrict__ oth,
+                                             const float* __restrict__ woth, float* lds) {
+  constexpr int OS = NV == 1 ? HS_OSF : HS_OSB, U = 4;
   const int NcP = (Nc + 3) & ~3;
-  HsView v;
-  const float* svb = sv_g + hsort_tab(b, z, 0, NcP);       // the 20 tables, contiguous
-  if constexpr (STAGE) {
-    float* svl = reinterpret_cast<float*>(lds);
-    float* ol = svl + (size_t)H * NcP;
-    float* wl = ol + (size_t)H * Nc;
-    copy16<6>(reinterpret_cast<float4*>(svl), reinterpret_cast<const float4*>(svb), H * NcP / 4);
-    copy16<6>(reinterpret_cast<float4*>(ol), reinterpret_cast<const float4*>(oth_g), H * Nc / 4);
-    if (woth_g)
-      copy16<6>(reinterpret_cast<float4*>(wl), reinterpret_cast<const float4*>(woth_g),
-                H * Nc / 4);
-    __syncthreads();
-    v.sv = svl;
-    v.oth = ol;
-    v.woth = wl;
-  } else {
-    v.sv = svb;
-    v.oth = oth_g;
-    v.woth = woth_g;
+  copy16<6>(reinterpret_cast<float4*>(lds),
+            reinterpret_cast<const float4*>(sv_g + hsort_tab(b, z, 0, NcP)), H * NcP / 4);
+  float* dst = lds + H * NcP;
+  const int n4 = Nc * (H / 4);
+  const float4* o4 = reinterpret_cast<const float4*>(oth);
+  const float4* w4 = reinterpret_cast<const float4*>(woth);
+  for (int e0 = threadIdx.x; e0 < n4; e0 += U * blockDim.x) {
+    float4 v[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x < n4 ? e0 + u * blockDim.x : e0;
+      v[u] = o4[e];
+      if constexpr (NV == 2) w[u] = w4[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x;
+      if (e >= n4) continue;
+      const int n = e / (H / 4), q4 = e - n * (H / 4);
+      const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      float ww[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (NV == 2) {
+        ww[0] = w[u].x; ww[1] = w[u].y; ww[2] = w[u].z; ww[3] = w[u].w;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = 4 * q4 + c, g = k / KPW, m = k - g * KPW;
+        if constexpr (NV == 1) {
+          dst[n * OS + g * 6 + m] = vv[c];
+        } else {
+          dst[n * OS + g * 10 + 2 * m] = vv[c];
+          dst[n * OS + g * 10 + 2 * m + 1] = ww[c];
+        }
+      }
+    }
   }
-  v.svs = NcP;
-  return v;
+  __syncthreads();
+}
+
+// group shape: stage unit group g's sorted values sv [KPW][NcP], then its walk rows
+template <int NV>
+__device__ __forceinline__ void hs_stage_g(int z, int b, int g, int Nc,
+                                           const float* __restrict__ sv_g,
+                                           const float* __restrict__ oth,
+                                           const float* __restrict__ woth, float* lds) {
+  constexpr int RS = NV == 1 ? HS_RSF : HS_RSB, U = 4;
+  const int NcP = (Nc + 3) & ~3;
+  copy16<4>(reinterpret_cast<float4*>(lds),
+            reinterpret_cast<const float4*>(sv_g + hsort_tab(b, z, g * KPW, NcP)), KPW * NcP / 4);
+  float* rows = lds + KPW * NcP;
+  const float* ob = oth + g * KPW;
+  const float* wb = woth + g * KPW;
+  for (int n0 = threadIdx.x; n0 < Nc; n0 += U * blockDim.x) {
+    float v[U][KPW], w[U][KPW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * blockDim.x < Nc ? n0 + u * blockDim.x : n0;
+#pragma unroll
+      for (int m = 0; m < KPW; ++m) {
+        v[u][m] = ob[(size_t)n * H + m];
+        if constexpr (NV == 2) w[u][m] = wb[(size_t)n * H + m];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * blockDim.x;
+      if (n >= Nc) continue;
+#pragma unroll
+      for (int m = 0; m < KPW; ++m) {
+        if constexpr (NV == 1) {
+          rows[n * RS + m] = v[u][m];
+        } else {
+          rows[n * RS + 2 * m] = v[u][m];
+          rows[n * RS + 2 * m + 1] = w[u][m];
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// the swept side's staged row q of unit group g: o (and w for NV = 2); RS the node stride,
+// GS the group stride within a node row (6 / 10 in the all-unit layout, 0 in the group one)
+template <int NV, int RS, int GS>
+__device__ __forceinline__ void walk_row(const float* rows, int q, int g, float (&o)[KPW],
+                                         float (&w)[KPW]) {
+  const float* r = rows + q * RS + g * GS;
+  if constexpr (NV == 1) {
+    const float2 a = *reinterpret_cast<const float2*>(r);
+    const float2 c = *reinterpret_cast<const float2*>(r + 2);
+    const float2 e = *reinterpret_cast<const float2*>(r + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = c.x; o[3] = c.y; o[4] = e.x;
+  } else {
+#pragma unroll
+    for (int m = 0; m < KPW; ++m) {
+      const float2 a = *reinterpret_cast<const float2*>(r + 2 * m);
+      o[m] = a.x;
+      w[m] = a.y;
+    }
+  }
 }
 
 // node r's label ids (ylist_layout): f(id, valid) for each, the sentinel padding invalid;
 // LB groups of four ids loaded before any is used
-template <int LB = 2, class F>
+template <int LB = HS_LB, class F>
 __device__ __forceinline__ void for_ylist(const uint32_t* __restrict__ prep, const ListLayout& Y,
                                           size_t r, int Nc, F f) {
   const int ng = ((int)prep[Y.cnt + r] + 3) >> 2;
@@ -2115,9 +2214,114 @@ __device__ __forceinline__ void for_ylist(const uint32_t* __restrict__ prep, con
   }
 }
 
-// kw_hunk_fwd_s  grid (ceil(Nc / 128), B, 2), NTP threads: kw_hunk_fwd's results (G / H,
-// sigma / tau) from the sorted tables
-template <bool STAGE>
+// the five binary searches of a lane interleaved (independent LDS chains): m[kk] = first slot
+// of unit kk's ascending table (svl + kk NcP) with value > -ow[kk]
+__device__ __forceinline__ void hs_search(const float* svl, int NcP, int Nc,
+                                          const float (&ow)[KPW], int (&m)[KPW]) {
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) m[kk] = 0;
+  for (int st = top_pow2(Nc); st > 0; st >>= 1) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int c = m[kk] + st - 1;
+      if (c < Nc && !(svl[kk * NcP + c] > -ow[kk])) m[kk] += st;
+    }
+  }
+}
+
+// The per-lane core of the forward sorted pass: node ncl's sums over the swept side for the
+// five units of group g: the dense part from the search and the f64 suffix table, the self
+// pair removed, the y = 1 pairs' relu(z1) replacing relu(z0) (the sentinel ids: a zero term)
+template <int RS, int GS>
+__device__ __forceinline__ void fwd_s_lane(const float* svl, const float* rows, int NcP, int Nc,
+                                           int b, int z, int g, int ncl, bool ys,
+                                           const float (&ow)[KPW], const float (&dl)[KPW],
+                                           const double* __restrict__ sx,
+                                           const uint32_t* __restrict__ prep,
+                                           const ListLayout& Y, size_t yrow, float (&out)[KPW]) {
+  int m[KPW];
+  hs_search(svl, NcP, Nc, ow, m);
+  double dense[KPW];
+  float acc[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk)
+    dense[kk] = (double)(Nc - m[kk]) * (double)ow[kk] +
+                sx[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]];
+  {
+    float os[KPW], unused[KPW];
+    walk_row<1, RS, GS>(rows, ncl, g, os, unused);
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float zs = ow[kk] + os[kk];                        // the self pair, as the walk
+      acc[kk] = -relu(ys ? zs + dl[kk] : zs);                  // and the dense part count it
+    }
+  }
+  for_ylist(prep, Y, yrow, Nc, [&](int q, bool ok) {
+    float oq[KPW], unused[KPW];
+    walk_row<1, RS, GS>(rows, q, g, oq, unused);
+    const float vm = ok ? 1.f : 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = ow[kk] + oq[kk];
+      acc[kk] += vm * (relu(z0 + dl[kk]) - relu(z0));
+    }
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) out[kk] = (float)dense[kk] + acc[kk];
+}
+
+// ... and of the backward one: Dalpha / Dbeta sums (out) and the y-weighted sums (yout)
+template <int RS, int GS>
+__device__ __forceinline__ void mlpb_s_lane(const float* svl, const float* rows, int NcP, int Nc,
+                                            int b, int z, int g, int ncl, bool ys,
+                                            const float (&ow)[KPW], const float (&wo)[KPW],
+                                            const float (&dl)[KPW],
+                                            const double* __restrict__ sw,
+                                            const uint32_t* __restrict__ prep,
+                                            const ListLayout& Y, size_t yrow, float (&out)[KPW],
+                                            float (&yout)[KPW]) {
+  int m[KPW];
+  hs_search(svl, NcP, Nc, ow, m);
+  double dense[KPW];
+  float acc[KPW], ya[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk)
+    dense[kk] = (double)(Nc - m[kk]) * (double)wo[kk] +
+                sw[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]];
+  {
+    float os[KPW], ws[KPW];
+    walk_row<2, RS, GS>(rows, ncl, g, os, ws);
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float zs = ow[kk] + os[kk];                        // the self pair
+      const float gs = wo[kk] + ws[kk];
+      const bool ms = (ys ? zs + dl[kk] : zs) > 0.f;
+      acc[kk] = ms ? -gs : 0.f;
+      ya[kk] = (ms && ys) ? -gs : 0.f;
+    }
+  }
+  // y = 1 pairs: the mask of z1 replaces z0's (the sentinel ids: weight 0)
+  for_ylist(prep, Y, yrow, Nc, [&](int q, bool ok) {
+    float oq[KPW], wq[KPW];
+    walk_row<2, RS, GS>(rows, q, g, oq, wq);
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const float z0 = ow[kk] + oq[kk];
+      const float gq = ok ? wo[kk] + wq[kk] : 0.f;
+      const float m1 = (z0 + dl[kk]) > 0.f ? gq : 0.f;
+      acc[kk] += m1 - (z0 > 0.f ? gq : 0.f);
+      ya[kk] += m1;
+    }
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    out[kk] = (float)dense[kk] + acc[kk];
+    yout[kk] = ya[kk];
+  }
+}
+
+// kw_hunk_fwd_s  grid (ceil(Nc / 128), B, 2), NTP threads, Nc <= HS_ALL_MAX: kw_hunk_fwd's
+// results (G / H, sigma / tau) from the sorted tables
 __global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
@@ -2128,52 +2332,29 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
   extern __shared__ __attribute__((aligned(16))) float hs_lds[];
   __shared__ float res[HSN * HP];
   __shared__ float Ml[H * H];
-  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * HSN, B = gridDim.y;
+  int tile, b, z;
+  xcd_commit_map(tile, b, z);
+  const int t0 = tile * HSN, B = gridDim.y, NcP = (Nc + 3) & ~3;
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
   const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
+  WSTAMP(2, 0);
   stage_w(Ml, D + D_M, H * H);
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
-  const HsView V = hs_stage<STAGE>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
-                                   nullptr, hs_lds);
-  float ow[KPW], dl[KPW], acc[KPW];
-  int m[KPW];
+  float ow[KPW], dl[KPW], out[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    ow[kk] = own[(size_t)ncl * H + g * KPW + kk];
+    dl[kk] = D[D_DLT + g * KPW + kk];
+  }
   const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
+  hs_stage_all<1>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H, nullptr, hs_lds);
+  WSTAMP(2, 1);
+  fwd_s_lane<HS_OSF, 6>(hs_lds + g * KPW * NcP, hs_lds + H * NcP, NcP, Nc, b, z, g, ncl, ys, ow,
+                        dl, sx, prep, Y, ((size_t)z * B + b) * Nc + ncl, out);
+  WSTAMP(2, 2);
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    const int k = g * KPW + kk;
-    ow[kk] = own[(size_t)ncl * H + k];
-    dl[kk] = D[D_DLT + k];
-    m[kk] = 0;
-  }
-  // the five binary searches interleaved (independent LDS chains)
-  for (int st = top_pow2(Nc); st > 0; st >>= 1) {
-#pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const int c = m[kk] + st - 1;
-      if (c < Nc && !(V.sv[(g * KPW + kk) * V.svs + c] > -ow[kk])) m[kk] += st;
-    }
-  }
-  double dense[KPW];
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    const int k = g * KPW + kk;
-    dense[kk] = (double)(Nc - m[kk]) * (double)ow[kk] + sx[hsort_tab(b, z, k, ((Nc + 3) & ~3) + 1) + m[kk]];
-    const float zs = ow[kk] + V.oth[(size_t)ncl * H + k];   // the self pair, as the walk
-    acc[kk] = -relu(ys ? zs + dl[kk] : zs);                  // and the dense part count it
-  }
-  // y = 1 pairs: relu(z1) replaces relu(z0) (the sentinel ids: a zero term)
-  for_ylist(prep, Y, ((size_t)z * B + b) * Nc + ncl, Nc, [&](int q, bool ok) {
-    const float* oq = V.oth + (size_t)q * H + g * KPW;
-    const float vm = ok ? 1.f : 0.f;
-#pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const float z0 = ow[kk] + oq[kk];
-      acc[kk] += vm * (relu(z0 + dl[kk]) - relu(z0));
-    }
-  });
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) res[nl * HP + g * KPW + kk] = (float)dense[kk] + acc[kk];
+  for (int kk = 0; kk < KPW; ++kk) res[nl * HP + g * KPW + kk] = out[kk];
   __syncthreads();
   float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
   float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
@@ -2186,14 +2367,77 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
     gout[(t0 + n) * H + k] = res[n * HP + k];
     sout[(t0 + n) * H + k] = sacc + off[k];
   }
+  WSTAMP(2, 3);
 }
 
-// kw_hunk_mlpb_s  grid (ceil(Nc / 128), B, 2), NTP threads: kw_hunk_mlpb's results from the
-// sorted tables.  Row pass (z = 0, node p): D alpha_p = dG_p |S_p| + sum_{q in S_p} dH_q with
-// S_p = {q : beta_q > -alpha_p}; the column pass (node q) with alpha's order and dG; then
-// the y = 1 pairs' mask changes, ysum = sum y dz, and the self pair removed.  The epilogue
-// (partial gradient rows) per 64-node half, as kw_hunk_mlpb's tiles write them.
-template <bool STAGE>
+// kw_hunk_fwd_g  grid (4 hs_tiles(Nc), B, 2), NT threads, Nc > HS_ALL_MAX: G (z = 0) / H
+// (z = 1) of one unit group; sigma / tau follow in kw_hunk_sig
+__global__ __launch_bounds__(NT) void kw_hunk_fwd_g(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ sv, const double* __restrict__ sx,
+    const uint32_t* __restrict__ prep, ListLayout Y, float* __restrict__ G,
+    float* __restrict__ Hh) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
+  int tg, b, z;
+  xcd_commit_map(tg, b, z);
+  const int g = tg & 3, t0 = (tg >> 2) * HSG, B = gridDim.y, NcP = (Nc + 3) & ~3;
+  const int nd = t0 + threadIdx.x, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H + g * KPW;
+  float ow[KPW], dl[KPW], out[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    ow[kk] = own[(size_t)ncl * H + kk];
+    dl[kk] = D[D_DLT + g * KPW + kk];
+  }
+  const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
+  hs_stage_g<1>(z, b, g, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H, nullptr, hs_lds);
+  fwd_s_lane<HS_RSF, 0>(hs_lds, hs_lds + KPW * NcP, NcP, Nc, b, z, g, ncl, ys, ow, dl, sx, prep,
+                        Y, ((size_t)z * B + b) * Nc + ncl, out);
+  if (nd < Nc) {
+    float* gout = (z ? Hh : G) + ((size_t)b * Nc + nd) * H + g * KPW;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) gout[kk] = out[kk];
+  }
+}
+
+// kw_hunk_sig  grid (tc, B, 2): sigma = G M + s0 (z = 0), tau = H M + t0 (z = 1), the
+// classifier first layer on kw_hunk_fwd_g's node sums (kw_hunk_fwd's epilogue)
+__global__ __launch_bounds__(NT) void kw_hunk_sig(const float* __restrict__ D, int Nc,
+                                                  const float* __restrict__ G,
+                                                  const float* __restrict__ Hh,
+                                                  float* __restrict__ sig,
+                                                  float* __restrict__ tau) {
+#pragma clang fp contract(off)
+  __shared__ float Ml[H * H];
+  __shared__ float gl[TN * HP];
+  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * TN;
+  stage_w(Ml, D + D_M, H * H);
+  const float* src = (z ? Hh : G) + (size_t)b * Nc * H;
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    gl[n * HP + k] = t0 + n < Nc ? src[(size_t)(t0 + n) * H + k] : 0.f;
+  }
+  __syncthreads();
+  float* out = (z ? tau : sig) + (size_t)b * Nc * H;
+  const float* off = D + (z ? D_T0 : D_S0);
+  for (int e = threadIdx.x; e < TN * H; e += NT) {
+    const int n = e / H, k = e - n * H;
+    if (t0 + n >= Nc) continue;
+    float sacc = 0.f;
+    for (int l = 0; l < H; ++l) sacc = fmaf(gl[n * HP + l], Ml[l * H + k], sacc);
+    out[(size_t)(t0 + n) * H + k] = sacc + off[k];
+  }
+}
+
+// kw_hunk_mlpb_s  grid (ceil(Nc / 128), B, 2), NTP threads, Nc <= HS_ALL_MAX: kw_hunk_mlpb's
+// results from the sorted tables.  Row pass (z = 0, node p): D alpha_p = dG_p |S_p| +
+// sum_{q in S_p} dH_q with S_p = {q : beta_q > -alpha_p}; the column pass (node q) with
+// alpha's order and dG; then the y = 1 pairs' mask changes, ysum = sum y dz, and the self
+// pair removed.  The epilogue (partial gradient rows) per 64-node half, as kw_hunk_mlpb's
+// tiles write them.
 __global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
@@ -2204,68 +2448,114 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float hs_lds[];
   __shared__ float res[HSN * HP], yres[HSN * HP], nt[TN * 4];
-  const int z = blockIdx.z, b = blockIdx.y, t0 = blockIdx.x * HSN, B = gridDim.y;
+  int btile, b, z;
+  xcd_commit_map(btile, b, z);
+  const int t0 = btile * HSN, B = gridDim.y, NcP = (Nc + 3) & ~3;
   const int tc = (Nc + TN - 1) / TN;
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
   const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
   const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
-  const HsView V = hs_stage<STAGE>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
-                                   (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
+  WSTAMP(3, 0);
+  float ow[KPW], wo[KPW], dl[KPW], out[KPW], yout[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    ow[kk] = own[(size_t)ncl * H + g * KPW + kk];
+    wo[kk] = wown[(size_t)ncl * H + g * KPW + kk];
+    dl[kk] = D[D_DLT + g * KPW + kk];
+  }
   const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
-  float ow[KPW], wo[KPW], dl[KPW], acc[KPW], ya[KPW];
-  int m[KPW];
+  hs_stage_all<2>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
+                  (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
+  WSTAMP(3, 1);
+  mlpb_s_lane<HS_OSB, 10>(hs_lds + g * KPW * NcP, hs_lds + H * NcP, NcP, Nc, b, z, g, ncl, ys,
+                          ow, wo, dl, sw, prep, Y, ((size_t)z * B + b) * Nc + ncl, out, yout);
+  WSTAMP(3, 2);
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
-    const int k = g * KPW + kk;
-    ow[kk] = own[(size_t)ncl * H + k];
-    wo[kk] = wown[(size_t)ncl * H + k];
-    dl[kk] = D[D_DLT + k];
-    m[kk] = 0;
-  }
-  for (int st = top_pow2(Nc); st > 0; st >>= 1) {
-#pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const int c = m[kk] + st - 1;
-      if (c < Nc && !(V.sv[(g * KPW + kk) * V.svs + c] > -ow[kk])) m[kk] += st;
-    }
-  }
-  double dense[KPW];
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    const int k = g * KPW + kk;
-    dense[kk] = (double)(Nc - m[kk]) * (double)wo[kk] + sw[hsort_tab(b, z, k, ((Nc + 3) & ~3) + 1) + m[kk]];
-    const float zs = ow[kk] + V.oth[(size_t)ncl * H + k];       // the self pair
-    const float gs = wo[kk] + V.woth[(size_t)ncl * H + k];
-    const bool ms = (ys ? zs + dl[kk] : zs) > 0.f;
-    acc[kk] = ms ? -gs : 0.f;
-    ya[kk] = (ms && ys) ? -gs : 0.f;
-  }
-  // y = 1 pairs: the mask of z1 replaces z0's (the sentinel ids: weight 0)
-  for_ylist(prep, Y, ((size_t)z * B + b) * Nc + ncl, Nc, [&](int q, bool ok) {
-    const size_t e = (size_t)q * H + g * KPW;
-#pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) {
-      const float z0 = ow[kk] + V.oth[e + kk];
-      const float gq = ok ? wo[kk] + V.woth[e + kk] : 0.f;
-      const float m1 = (z0 + dl[kk]) > 0.f ? gq : 0.f;
-      acc[kk] += m1 - (z0 > 0.f ? gq : 0.f);
-      ya[kk] += m1;
-    }
-  });
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    res[nl * HP + g * KPW + kk] = (float)dense[kk] + acc[kk];
-    yres[nl * HP + g * KPW + kk] = ya[kk];
+    res[nl * HP + g * KPW + kk] = out[kk];
+    yres[nl * HP + g * KPW + kk] = yout[kk];
   }
   __syncthreads();
   for (int half = 0; half < 2; ++half) {        // kw_hunk_mlpb's rows, one per 64-node tile
-    const int tile = blockIdx.x * 2 + half;
+    const int tile = btile * 2 + half;
     if (tile >= tc) break;                       // block-uniform
     mlpb_epilogue(z, b, tile * TN, tc, Nc, nvec, res + half * TN * HP, yres + half * TN * HP,
                   nt, Dal, Dbe, part, sg, tile);
     __syncthreads();
+  }
+  WSTAMP(3, 3);
+}
+
+// kw_hunk_mlpb_g  grid (4 hs_tiles(Nc), B, 2), NT threads, Nc > HS_ALL_MAX: kw_hunk_mlpb_s for
+// one unit group; the epilogue of its four 64-node tiles in one pass (the group's columns of
+// each tile's partial rows)
+__global__ __launch_bounds__(NT) void kw_hunk_mlpb_g(
+    const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
+    const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
+    const float* __restrict__ nvec, const float* __restrict__ sv, const double* __restrict__ sw,
+    const uint32_t* __restrict__ prep, ListLayout Y, float* __restrict__ Dal,
+    float* __restrict__ Dbe, float* __restrict__ part, Segs sg) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float hs_lds[];
+  __shared__ float res[HSG * RS5], yres[HSG * RS5], nt[HSG * 4];
+  int tg, b, z;
+  xcd_commit_map(tg, b, z);
+  const int g = tg & 3, btile = tg >> 2, t0 = btile * HSG, B = gridDim.y, NcP = (Nc + 3) & ~3;
+  const int tc = (Nc + TN - 1) / TN;
+  const int nl = threadIdx.x, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
+  const int WC = (Nc + 31) >> 5;
+  const float* own = (z ? beta : alpha) + (size_t)b * Nc * H + g * KPW;
+  const float* wown = (z ? dH : dG) + (size_t)b * Nc * H + g * KPW;
+  float ow[KPW], wo[KPW], dl[KPW], out[KPW], yout[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    ow[kk] = own[(size_t)ncl * H + kk];
+    wo[kk] = wown[(size_t)ncl * H + kk];
+    dl[kk] = D[D_DLT + g * KPW + kk];
+  }
+  const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
+  hs_stage_g<2>(z, b, g, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
+                (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
+  mlpb_s_lane<HS_RSB, 0>(hs_lds, hs_lds + KPW * NcP, NcP, Nc, b, z, g, ncl, ys, ow, wo, dl, sw,
+                         prep, Y, ((size_t)z * B + b) * Nc + ncl, out, yout);
+  const bool in = nd < Nc;
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    res[nl * RS5 + kk] = in ? out[kk] : 0.f;
+    yres[nl * RS5 + kk] = in ? yout[kk] : 0.f;
+  }
+  float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H + g * KPW;
+  if (in) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) dout[(size_t)nd * H + kk] = out[kk];
+  }
+  for (int e = threadIdx.x; e < HSG * 4; e += NT)
+    nt[e] = (t0 + e / 4 < Nc) ? nvec[((size_t)b * Nc + t0) * 4 + e] : 0.f;
+  __syncthreads();
+  // the group's columns of mlpb_epilogue's rows 0..9 of V1 and c1, every tile of the block
+  const Seg& s = sg.s[SG_MLPB];
+  constexpr int NI = 11 * KPW;
+  for (int e = threadIdx.x; e < (HSG / TN) * NI; e += NT) {
+    const int q = e / NI, r = e - q * NI, l = r / KPW, kk = r - l * KPW;
+    const int tile = btile * (HSG / TN) + q;
+    if (tile >= tc) continue;
+    const float* rq = res + q * TN * RS5;
+    const float* yq = yres + q * TN * RS5;
+    const float* nq = nt + q * TN * 4;
+    float a = 0.f;
+    if (l < 8) {
+      const int m = l & 3;
+      if ((l >> 2) == z)
+        for (int n = 0; n < TN; ++n) a = fmaf(nq[n * 4 + m], rq[n * RS5 + kk], a);
+    } else if (z == 0) {
+      float sd = 0.f, sy = 0.f;
+      for (int n = 0; n < TN; ++n) { sd += rq[n * RS5 + kk]; sy += yq[n * RS5 + kk]; }
+      a = l == 8 ? sd - sy : (l == 9 ? sy : sd);
+    }
+    put(part, s, l * H + g * KPW + kk, (b * tc + tile) * 2 + z, a);
   }
 }
 
@@ -3613,16 +3903,17 @@ struct WideWork {
 
 // the sorted-threshold form of the hunk relu / mask sums (kw_hunk_sort, _fwd_s, _wsum,
 // _mlpb_s) instead of the dense sweeps (kw_hunk_fwd, kw_hunk_mlpb)
-bool hunk_sorted(const hdg_shape* s) {
-  if (s->flags & (HDG_FLAG_HUNK_DENSE | HDG_FLAG_HUNK_TILED)) return false;
-  if (s->flags & HDG_FLAG_HUNK_SORTED) return true;
-  return s->nc >= HDG_HUNK_SORTED_MIN_NC;
-}
-// the one-sweep tiles (kh_tile + kw_hunk_fin*) for all three hunk pair passes
+// automatic form by Nc (flags force one): tiled from HDG_HUNK_TILED_MIN_NC, sorted from
+// HDG_HUNK_SORTED_MIN_NC below that, the dense two-pass sweep otherwise
 bool hunk_tiled(const hdg_shape* s) {
   if (s->flags & (HDG_FLAG_HUNK_DENSE | HDG_FLAG_HUNK_SORTED)) return false;
   if (s->flags & HDG_FLAG_HUNK_TILED) return true;
-  return s->nc >= HDG_HUNK_TILED_MIN_NC && !hunk_sorted(s);
+  return s->nc >= HDG_HUNK_TILED_MIN_NC;
+}
+bool hunk_sorted(const hdg_shape* s) {
+  if (s->flags & (HDG_FLAG_HUNK_DENSE | HDG_FLAG_HUNK_TILED)) return false;
+  if (s->flags & HDG_FLAG_HUNK_SORTED) return true;
+  return s->nc >= HDG_HUNK_SORTED_MIN_NC && !hunk_tiled(s);
 }
 
 // the hunk label id lists (the sorted passes' walks) are part of every general-path
@@ -3725,12 +4016,18 @@ int set_wide_attrs() {
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_clsb,      // 41 KiB static + 32 KiB at Ne 4096
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_hunk_fwd_s<true>,
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_fwd_s,
                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)hs_lds_bytes(HS_STAGE_MAX, 1)));
-    WTRY(hipFuncSetAttribute((const void*)kw_hunk_mlpb_s<true>,
+                             (int)hs_lds_bytes(HS_ALL_MAX, 1)));
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_mlpb_s,
                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)hs_lds_bytes(HS_STAGE_MAX, 2)));
+                             (int)hs_lds_bytes(HS_ALL_MAX, 2)));
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_fwd_g,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hs_lds_bytes(HS_NC_MAX, 1)));
+    WTRY(hipFuncSetAttribute((const void*)kw_hunk_mlpb_g,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hs_lds_bytes(HS_NC_MAX, 2)));
     attr_set = true;
   }
   return 0;
@@ -3997,29 +4294,33 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   const HTileSums hts{F(w.htr), F(w.htc), F(w.hty), (Nc + hunk_tile_cols() - 1) / hunk_tile_cols(),
                       (Nc + hunk_tile_rows() - 1) / hunk_tile_rows()};
   if (hs) {
-    const dim3 gw((H + NW - 1) / NW, B, 2);
+    const dim3 gw(H, B, 2);
 #define HDG_SORT(E_)                                                                            \
   hipLaunchKernelGGL(kw_hunk_sort<E_>, gw, dim3(NT), 0, st, F(w.alpha), F(w.beta), Nc, F(w.hsv), \
                      (int*)F(w.hsp), (double*)F(w.hsx))
     switch (hsort_e(Nc)) {
+      case 1: HDG_SORT(1); break;
       case 2: HDG_SORT(2); break;
       case 4: HDG_SORT(4); break;
-      case 8: HDG_SORT(8); break;
-      case 16: HDG_SORT(16); break;
-      default: HDG_SORT(32); break;
+      default: HDG_SORT(8); break;
     }
 #undef HDG_SORT
     WTRY(kmark("kw_hunk_sort", st));
-    const dim3 gs((Nc + HSN - 1) / HSN, B, 2);
-    if (Nc <= HS_STAGE_MAX)
-      hipLaunchKernelGGL(kw_hunk_fwd_s<true>, gs, dim3(NTP), hs_lds_bytes(Nc, 1), st, bt->ybits,
-                         yT, D, Nc, F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx),
-                         prep, YL, F(w.G), F(w.Hh), F(w.sig), F(w.tau));
-    else
-      hipLaunchKernelGGL(kw_hunk_fwd_s<false>, gs, dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
-                         F(w.alpha), F(w.beta), F(w.hsv), (const double*)F(w.hsx), prep, YL,
-                         F(w.G), F(w.Hh), F(w.sig), F(w.tau));
-    WTRY(kmark("kw_hunk_fwd_s", st));
+    if (Nc <= HS_ALL_MAX) {
+      hipLaunchKernelGGL(kw_hunk_fwd_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(NTP),
+                         hs_lds_bytes(Nc, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         F(w.hsv), (const double*)F(w.hsx), prep, YL, F(w.G), F(w.Hh),
+                         F(w.sig), F(w.tau));
+      WTRY(kmark("kw_hunk_fwd_s", st));
+    } else {
+      hipLaunchKernelGGL(kw_hunk_fwd_g, dim3(4 * hs_tiles(Nc), B, 2), dim3(NT),
+                         hs_lds_bytes(Nc, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         F(w.hsv), (const double*)F(w.hsx), prep, YL, F(w.G), F(w.Hh));
+      WTRY(kmark("kw_hunk_fwd_g", st));
+      hipLaunchKernelGGL(kw_hunk_sig, dim3(tc, B, 2), dim3(NT), 0, st, D, Nc, F(w.G), F(w.Hh),
+                         F(w.sig), F(w.tau));
+      WTRY(kmark("kw_hunk_sig", st));
+    }
   } else if (ht) {
     HTileArgs ha{Nc, F(w.alpha), F(w.beta), nullptr, nullptr, nullptr, D + D_DLT, bt->ybits,
                  F(w.htr), F(w.htc), F(w.hty)};
@@ -4065,29 +4366,31 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     WTRY(kmark("kw_hunk_clsb", st));
   }
   if (hs) {
-    const dim3 gw((H + NW - 1) / NW, B, 2);
+    const dim3 gw(H, B, 2);
 #define HDG_WSUM(E_)                                                                        \
   hipLaunchKernelGGL(kw_hunk_wsum<E_>, gw, dim3(NT), 0, st, (const int*)F(w.hsp), F(w.dG), \
                      F(w.dH), Nc, (double*)F(w.hsw))
     switch (hsort_e(Nc)) {
+      case 1: HDG_WSUM(1); break;
       case 2: HDG_WSUM(2); break;
       case 4: HDG_WSUM(4); break;
-      case 8: HDG_WSUM(8); break;
-      case 16: HDG_WSUM(16); break;
-      default: HDG_WSUM(32); break;
+      default: HDG_WSUM(8); break;
     }
 #undef HDG_WSUM
     WTRY(kmark("kw_hunk_wsum", st));
-    const dim3 gs((Nc + HSN - 1) / HSN, B, 2);
-    if (Nc <= HS_STAGE_MAX)
-      hipLaunchKernelGGL(kw_hunk_mlpb_s<true>, gs, dim3(NTP), hs_lds_bytes(Nc, 2), st, bt->ybits,
-                         yT, D, Nc, F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
-                         (const double*)F(w.hsw), prep, YL, F(w.Dal), F(w.Dbe), part, w.segs);
-    else
-      hipLaunchKernelGGL(kw_hunk_mlpb_s<false>, gs, dim3(NTP), 0, st, bt->ybits, yT, D, Nc,
-                         F(w.alpha), F(w.beta), F(w.dG), F(w.dH), F(w.nvec), F(w.hsv),
-                         (const double*)F(w.hsw), prep, YL, F(w.Dal), F(w.Dbe), part, w.segs);
-    WTRY(kmark("kw_hunk_mlpb_s", st));
+    if (Nc <= HS_ALL_MAX) {
+      hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(NTP),
+                         hs_lds_bytes(Nc, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         F(w.dG), F(w.dH), F(w.nvec), F(w.hsv), (const double*)F(w.hsw), prep,
+                         YL, F(w.Dal), F(w.Dbe), part, w.segs);
+      WTRY(kmark("kw_hunk_mlpb_s", st));
+    } else {
+      hipLaunchKernelGGL(kw_hunk_mlpb_g, dim3(4 * hs_tiles(Nc), B, 2), dim3(NT),
+                         hs_lds_bytes(Nc, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         F(w.dG), F(w.dH), F(w.nvec), F(w.hsv), (const double*)F(w.hsw), prep,
+                         YL, F(w.Dal), F(w.Dbe), part, w.segs);
+      WTRY(kmark("kw_hunk_mlpb_g", st));
+    }
   } else if (ht) {
     HTileArgs ha{Nc, F(w.alpha), F(w.beta), F(w.dG), F(w.dH), nullptr, D + D_DLT, bt->ybits,
                  F(w.htr), F(w.htc), F(w.hty)};
@@ -4147,3 +4450,9 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
 }
 
 }  // namespace hdg
+
+#ifdef HDG_WSTAMP
+extern "C" int hdg_wstamp_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(hdg::g_wst), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif

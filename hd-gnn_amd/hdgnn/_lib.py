@@ -22,7 +22,9 @@ class Shape(ctypes.Structure):
 
 PATH_AUTO, PATH_FUSED, PATH_GENERAL = 0, 1, 2
 FLAG_NO_SPLIT, FLAG_HUNK_DENSE, FLAG_HUNK_SORTED, FLAG_HUNK_TILED = 1, 2, 4, 8
-HUNK_SORTED_MIN_NC = 0x7fffffff   # the general path's default crossover (include/hdgnn.h)
+# the general path's automatic hunk pair-sum form (include/hdgnn.h): tiled from nc >= 1024,
+# sorted from nc >= 384 below that, dense otherwise
+HUNK_SORTED_MIN_NC, HUNK_TILED_MIN_NC = 384, 1024
 STATS_LEN = 8          # hdg_outputs.stats: ce, loss_map, loss_para, train_loss, count x3, fault
 
 

@@ -68,8 +68,11 @@ typedef struct hdg_shape {
  * one sweep over blocks of the pair grid giving row and column sums together (the fused
  * kernel's pair tiles), instead of a row pass and a column pass over every pair.        */
 #define HDG_FLAG_HUNK_TILED 8
-#define HDG_HUNK_SORTED_MIN_NC 0x7fffffff   /* default: never (the measured crossover) */
-#define HDG_HUNK_TILED_MIN_NC 0x7fffffff    /* default: not yet (measured crossover) */
+/* Without a form flag the general path picks by nc: tiled from HDG_HUNK_TILED_MIN_NC, sorted
+ * from HDG_HUNK_SORTED_MIN_NC below that, dense otherwise (the measured crossovers at the
+ * default 10% label density).                                              */
+#define HDG_HUNK_SORTED_MIN_NC 384
+#define HDG_HUNK_TILED_MIN_NC 1024
 
 /* Engine paths.  FUSED: one block per commit with the commit's state in LDS; model_2
  * and model_4 with ne <= 256, nc <= 160 (the benchmark shapes; model_4's entity-edge

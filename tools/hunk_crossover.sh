@@ -7,7 +7,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/hunk}
 mkdir -p "$OUT"
 line() { grep -h '^{' "$1" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("%.1f commits/s %.4f ms/step" % (d["value"], d["ms_per_step"]))'; }
-for cfg in "200 74 100" "250 150 100" "250 200 100" "250 256 64" "250 384 32" "1024 512 32" "512 1024 8"; do
+for cfg in "200 74 100" "250 150 100" "250 200 100" "250 256 64" "250 384 32" "1024 512 32" "512 768 16" "512 1024 8" "512 2048 2"; do
   set -- $cfg
   for h in dense sorted tiled; do
     tag=${1}x${2}_$h
