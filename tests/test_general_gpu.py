@@ -4,7 +4,8 @@ Variants: 1 model_1 HD-GNN/ES (hunk stage on B_1), 2 model_2 HD-GNN
 3 model_3 HD-GNN/E (entity-edge stage computed, unused), 4 model_4 HD-GNN (entity-edge
 probabilities replace E_edge in B_2).  Tolerances, set at about 4x the worst error any
 case here reached (profiles/r03/parity_summary.txt):
-  logits  3e-5 |ref| + 3e-6 max(1, max|ref|)   (worst 3.3e-6 max|ref|, 4096 classes)
+  logits  2e-5 |ref| + 2e-6 max(1, max|ref|)   (worst 8.7e-7 max|ref| in round 4; 3.3e-6 with
+          the dense form at Nc = 2048, which the automatic choice no longer runs)
   probs = softmax(logits) to 1e-6; CE rel 1e-5
   gradients  8e-5 |ref| + 8e-6 max|ref| per variable (worst 2.45e-5 |ref| on the largest
           element at the 4096-node shape; <= 3.5e-6 max|ref| at glide)
@@ -24,7 +25,7 @@ from tests import _errlog
 pytestmark = pytest.mark.gpu
 
 GEN = _lib.PATH_GENERAL
-LOGIT_RTOL, LOGIT_ATOL = 3e-5, 3e-6       # x |ref|, x max(1, max|ref|) of the commit
+LOGIT_RTOL, LOGIT_ATOL = 2e-5, 2e-6       # x |ref|, x max(1, max|ref|) of the commit
 GRAD_RTOL, GRAD_ATOL = 8e-5, 8e-6         # x |ref|, x max|ref| of the variable
 
 
