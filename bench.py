@@ -362,6 +362,10 @@ def main():
     path_name = {_lib.PATH_FUSED: "fused", _lib.PATH_GENERAL: "general"}[eng.path]
     dom = max(kern_ms, key=kern_ms.get)          # the dominant kernel of the step
     roofline = build_roofline(dom, kern_ms, v, path_name, ne, nc, B, default_data, args.hunk)
+    # the general path's hunk pair-sum form this run used (include/hdgnn.h's rule by Nc)
+    hunk_form = args.hunk if args.hunk != "auto" else (
+        "tiled" if nc >= _lib.HUNK_TILED_MIN_NC else
+        "sorted" if nc >= _lib.HUNK_SORTED_MIN_NC else "dense") + " (auto)"
     e2e = None
     if world == 1 and args.e2e > 0:
         try:                     # a side measurement: never costs the bench line
@@ -391,7 +395,7 @@ def main():
                                  "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world,
-                       **({} if args.hunk == "auto" else {"hunk_sums": args.hunk}),
+                       **({"hunk_sums": hunk_form} if eng.path == _lib.PATH_GENERAL else {}),
                        **({} if default_data else {"data_knobs": knobs})},
             "roofline": roofline, "cpu_baseline": cpu,
             "dp": {"allreduce": eng.allreduce_kind, "selftest": eng.allreduce_selftest,

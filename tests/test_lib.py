@@ -96,3 +96,19 @@ def test_prep_counts_layout_host():
     bad = _lib.Shape(4, 5000, 74, 2, 4, 0)
     z = ctypes.c_int64()
     assert lib.hdg_prep_counts_layout(ctypes.byref(bad), *(ctypes.byref(z) for _ in range(4))) != 0
+
+
+def test_python_mirror_matches_header_constants():
+    """hdgnn._lib's flag values and the general path's automatic hunk-form thresholds are
+    the ones include/hdgnn.h defines (bench.py reports the form from the Python mirror)."""
+    from hdgnn import _lib
+    with open(os.path.join(ROOT, "include", "hdgnn.h")) as f:
+        defs = dict(re.findall(r"#define\s+(HDG_[A-Z_0-9]+)\s+(0x[0-9a-fA-F]+|\d+)", f.read()))
+    val = {k: int(v, 0) for k, v in defs.items()}
+    assert val["HDG_FLAG_NO_SPLIT"] == _lib.FLAG_NO_SPLIT
+    assert val["HDG_FLAG_HUNK_DENSE"] == _lib.FLAG_HUNK_DENSE
+    assert val["HDG_FLAG_HUNK_SORTED"] == _lib.FLAG_HUNK_SORTED
+    assert val["HDG_FLAG_HUNK_TILED"] == _lib.FLAG_HUNK_TILED
+    assert val["HDG_HUNK_SORTED_MIN_NC"] == _lib.HUNK_SORTED_MIN_NC
+    assert val["HDG_HUNK_TILED_MIN_NC"] == _lib.HUNK_TILED_MIN_NC
+    assert val["HDG_PATH_FUSED"] == _lib.PATH_FUSED and val["HDG_PATH_GENERAL"] == _lib.PATH_GENERAL
