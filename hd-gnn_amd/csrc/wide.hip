@@ -975,6 +975,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
     if (blockIdx.y == 0 && blockIdx.z == 0) derive_body(W, o, Nc, D, bpow);
     return;
   }
+  WSTAMP(7, 0);
   const bool ent_part = blockIdx.z == 0 && ent;
   if (ent_part)
     ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
@@ -982,8 +983,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
     ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
   // the per-node products on the tile (node_fwd_tile): its inputs are this block's outputs
   // (global writes made visible to the block by the barrier)
+  WSTAMP(7, 1);
   __syncthreads();
+  WSTAMP(7, 2);
   node_fwd_tile(x, W, o, Ne, ent_part, P, R1, C1, no);
+  WSTAMP(7, 3);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1049,6 +1053,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   float* gl = tsum + ((2 * Ne + 3) & ~3);                                     // gam [Ne][H]
   float* gdl = gl + Ne * H;                                                   // gam + d
   EE_STAMP(0);
+  WSTAMP(5, 0);
   const int b = blockIdx.y, t0 = blockIdx.x * TF;
   const int t = threadIdx.x, lane = t & 63, wv = uni(t >> 6), half = lane >> 5;
   unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
@@ -1095,6 +1100,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   }
   __syncthreads();
   EE_STAMP(1);
+  WSTAMP(5, 1);
   const int WE = (Ne + 31) >> 5;
   const int ip = t0 + (lane & 31);
   const bool live = ip < n;
@@ -1132,6 +1138,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   widx = widx < wlast ? widx : wlast;
   uint32_t wcur = ab[widx], wnxt = ab[widx + 1 < wlast ? widx + 1 : wlast];
   EE_STAMP(2);
+  WSTAMP(5, 2);
   for (int it = 0; it < trips; ++it) {
     const int jp = jlo + it;
     const bool valid = live && jp < jhi && jp != ip;
@@ -1190,6 +1197,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     if ((lane & 15) == 0 && jp < jhi) tsum[2 * jp + ((lane >> 4) & 1)] = v;
   }
   EE_STAMP(3);
+  WSTAMP(5, 3);
   if (live) {                          // source bins: the lane's row i'
     const int hs = hsv;
     if (hs >= 0 && hs < Nc) {
@@ -1206,6 +1214,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   // per-tile partial bins, summed in tile order by kw_cross_fwd / k_commit_step (no global
   // atomics: the L2s of the 8 XCDs are not coherent for device-scope atomics)
   EE_STAMP(4);
+  WSTAMP(5, 4);
   for (int c = t; c < 2 * Nc; c += NTP) outp[c] = bins[c];
   EE_FLUSH();
 }
@@ -3473,6 +3482,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   const int b = lrow / te, tile = lrow - b * te;
   const int t0 = tile * TN, t = threadIdx.x;
   const size_t base = ((size_t)b * Ne + t0) * H;
+  WSTAMP(6, 0);
   stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
   stage_w(Wl + 400, W + o.EE_W2, 400);
   // staging: every element's loads issued before the first use (NE_IT elements per thread;
@@ -3508,12 +3518,14 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
         for (int u = 0; u < 8; ++u) dr[it] += v[it][u];
     }
   }
+  WSTAMP(6, 1);
 #pragma unroll
   for (int it = 0; it < NE_IT; ++it) {
     const int e = t + it * NT, n = e / H, k = e - n * H;
     A[n * HP + k] = dr[it] * D[D_EEC + k];   // kw_ee_clsb's row partials leave c out
   }
   __syncthreads();
+  WSTAMP(6, 2);
   const int lane = t & 63;
   // dR = A U1e^T, dC = Bq U1e^T, then phi = dR Q2^T, psi = dC Q2^T over the tile's 64
   // nodes as 16x16 MFMA tiles (4 node tiles x 2 column tiles per product, K = 20); columns
@@ -3546,6 +3558,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
       }
     }
   }
+  WSTAMP(6, 3);
   const int row = lrow;
   const Seg& s1 = sg.s[SG_ECW1E];
   const Seg& s2 = sg.s[SG_EEW2];
@@ -3577,6 +3590,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     for (int n = 0; n < TN; ++n) a += dR[n * HP + t] + dC[n * HP + t];
     put(part, s2, 400 + t, row, a * Ne1);
   }
+  WSTAMP(6, 4);
 }
 
 // ---------------------------------------------------------------------------------

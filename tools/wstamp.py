@@ -29,10 +29,11 @@ ap.add_argument("--nc", type=int, default=512)
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--variant", type=int, default=2)
 ap.add_argument("--hunk", default="sorted")
+ap.add_argument("--path", type=int, default=2, help="0 auto, 1 fused (model_4: hybrid), 2 general")
 a = ap.parse_args()
 flags = {"dense": _lib.FLAG_HUNK_DENSE, "sorted": _lib.FLAG_HUNK_SORTED,
          "tiled": _lib.FLAG_HUNK_TILED}[a.hunk]
-eng = Engine(a.ne, a.nc, a.batch, variant=a.variant, path=_lib.PATH_GENERAL, flags=flags)
+eng = Engine(a.ne, a.nc, a.batch, variant=a.variant, path=a.path, flags=flags)
 eng.set_params(layout.init_flat(0, a.variant))
 db = eng.upload(synth_commits(a.batch, a.ne, a.nc, 1))
 N = 1 << 22
@@ -60,3 +61,5 @@ t0 = (s[:, 0] - s[:, 0].min()) * 1e-2
 print("wave starts: p10 %.2f median %.2f p90 %.2f max %.2f us; kernel span %.2f us" % (
     np.percentile(t0, 10), np.median(t0), np.percentile(t0, 90), t0.max(),
     (s[:, -1].max() - s[:, 0].min()) * 1e-2))
+h, edges = np.histogram(t0, bins=np.arange(0, t0.max() + 1.0, 1.0))
+print("wave starts per us: " + " ".join("%d" % c for c in h))
