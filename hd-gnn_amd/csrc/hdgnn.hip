@@ -249,10 +249,6 @@ __device__ __forceinline__ f2 step2(f2 z) {
   return r;
 }
 
-__device__ __forceinline__ uint32_t getbit(const uint32_t* rowbits, int j) {
-  return (rowbits[j >> 5] >> (j & 31)) & 1u;
-}
-
 // q = r / d, rem = r % d for 0 <= r < 2^22, 1 <= d < 2^12: float estimate + one select
 // correction, 24-bit multiplies, no branches (keeps unrolled loads in flight)
 __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& rem) {
@@ -790,15 +786,6 @@ __device__ __forceinline__ void for_each_nbr(const uint8_t* list, const int d, c
   }
 }
 
-// clamp(x * a + b, 0, 1) on both halves of a packed pair, x broadcast: ONE v_pk_fma_f32
-__device__ __forceinline__ f2 clamp_fma2(const float x, const f2 a, const f2 b) {
-  f2 xx;
-  xx.x = x;
-  f2 r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(r) : "v"(xx), "v"(a), "v"(b));
-  return r;
-}
-
 // the same with x taken from the low / high half of a packed pair (op_sel: no copy of the
 // half into a register of its own)
 __device__ __forceinline__ f2 clamp_fma2_lo(const f2 x, const f2 a, const f2 b) {
@@ -812,8 +799,6 @@ __device__ __forceinline__ f2 clamp_fma2_hi(const f2 x, const f2 a, const f2 b) 
       : "=v"(r) : "v"(x), "v"(a), "v"(b));
   return r;
 }
-
-__device__ __forceinline__ f2 relu2(f2 v) { return __builtin_elementwise_max(v, (f2){0.f, 0.f}); }
 
 
 
@@ -1146,7 +1131,7 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   StepLayout L;
   const int NC16 = 16 * smaxc;
   const int NE4 = (Ne + 3) & ~3;
-  const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
+  const int WC = (Nc + 31) >> 5;
   const int cred = 4 * 16 * smaxc * KK_MID + 8 * KK_MID;
   int o = 0;
   L.W = o;    o += (m2::NP + 3) & ~3;
@@ -1180,20 +1165,6 @@ __host__ __device__ inline StepLayout step_layout(int Ne, int Nc, int smaxc) {
   L.U = o; L.Uwords = u; o += u;
   L.total = o;
   return L;
-}
-
-// dot of a 20-float LDS row (16-B aligned) with 20 register weights
-__device__ __forceinline__ float dot20(const float* row, const float (&w)[HS], float acc) {
-  const float4* r4 = reinterpret_cast<const float4*>(row);
-#pragma unroll
-  for (int v = 0; v < HS / 4; ++v) {
-    const float4 q = r4[v];
-    acc = fmaf(q.x, w[4 * v], acc);
-    acc = fmaf(q.y, w[4 * v + 1], acc);
-    acc = fmaf(q.z, w[4 * v + 2], acc);
-    acc = fmaf(q.w, w[4 * v + 3], acc);
-  }
-  return acc;
 }
 
 using hdg::f4v;
@@ -1678,7 +1649,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   int t = threadIdx.x;
   int lane = t & 63, wv = t >> 6, g = t >> 8, tg = t & 255;
   int mk = t % HS, msl = t / HS;                  // (k, slice) map; msl == NSL idles
-  const int WE = (Ne + 31) >> 5, WC = (Nc + 31) >> 5;
+  const int WC = (Nc + 31) >> 5;
   const int NE4 = (Ne + 3) & ~3;
   const int Pc = Nc * (Nc - 1);
   int nstamp = 0;

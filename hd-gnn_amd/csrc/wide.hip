@@ -115,18 +115,6 @@ __device__ __forceinline__ float row_total16(float v) {
   v += dppf<0xB1>(v);
   return v;
 }
-// wave sums of two values: lanes 0-31 end with a's total, lanes 32-63 with b's
-__device__ __forceinline__ float wsum2(float a, float b) {
-  swap32(a, b);
-  float v = a + b, x = v, y = v;
-  swap16(x, y);
-  v = x + y;
-  v += dppf<0x128>(v);
-  v += dppf<0x141>(v);
-  v += dppf<0x4E>(v);
-  v += dppf<0xB1>(v);
-  return v;
-}
 
 // Sums of the 20 values v[k] over the 64 lanes of a wave by a transposed butterfly (one
 // exchange per pair of values and level instead of six per value), all in the VALU:
@@ -288,14 +276,6 @@ __device__ __forceinline__ unsigned long long qfix(float v) {
   return (unsigned long long)__double2ll_rn((double)v * FIX);
 }
 
-// q = r / d, rem = r % d for 0 <= r < 2^24, d >= 1 (float estimate, exact correction)
-__device__ __forceinline__ void divmod24(int r, int d, float inv, int& q, int& rem) {
-  q = (int)((float)r * inv);
-  rem = r - q * d;
-  while (rem < 0) { --q; rem += d; }
-  while (rem >= d) { ++q; rem -= d; }
-}
-
 // derived weights (kw_derive), float offsets into the D buffer
 enum : int {
   D_M = 0,                 // [20][20] V2 . U1e  (hunk MLP second layer into the classifier)
@@ -411,21 +391,6 @@ __device__ __forceinline__ void stage_w(float* dst, const float* src, int n) {
 // ---------------------------------------------------------------------------------
 // block helpers
 // ---------------------------------------------------------------------------------
-// Combine per-wave accumulators acc[H] of the 64 lane-nodes over the 4 waves (fixed order)
-// into res[64][HP].  buf: [NW][64][HP].
-__device__ __forceinline__ void combine4(const float (&acc)[H], float* buf, float* res) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < H; ++k) buf[(w * TN + lane) * HP + k] = acc[k];
-  __syncthreads();
-  for (int e = threadIdx.x; e < TN * H; e += NT) {
-    const int n = e / H, k = e - n * H;
-    res[n * HP + k] = ((buf[(0 * TN + n) * HP + k] + buf[(1 * TN + n) * HP + k]) +
-                       buf[(2 * TN + n) * HP + k]) + buf[(3 * TN + n) * HP + k];
-  }
-  __syncthreads();
-}
-
 // Block sum of nv per-thread values (each wave xor-reduces, then a fixed 4-way sum);
 // result in out[0..nv) of LDS.  red: [NW][nv].
 template <int NV>
@@ -1597,7 +1562,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   __shared__ float Wl[3 * H * H + H];
   __shared__ float kzh[1];                        // 0.f: stride-0 operand of padding tiles
   if (threadIdx.x == 0) kzh[0] = 0.f;
-  const float *Ml = Wl, *V2 = Wl + H * H, *c2 = Wl + 2 * H * H, *U1e = Wl + 2 * H * H + H;
+  // Wl = M | V2 | c2 | U1e (clsb_epilogue's layout)
   stage_w(Wl, D + D_M, H * H);                    // visible after the first chunk barrier
   stage_w(Wl + H * H, W + o.H1_W2, H * H + H);    // V2 | c2
   stage_w(Wl + 2 * H * H + H, W + o.H2_W1 + 2 * H, H * H);
@@ -2025,14 +1990,6 @@ inline int hsort_e(int Nc) {
   int e = 1;
   while (256 * e < Nc) e <<= 1;
   return e;
-}
-
-// first slot m with sv[m] > thr (Nc if none): sv ascending
-__device__ __forceinline__ int upper_slot(const float* __restrict__ sv, int Nc, float thr) {
-  int m = 0;
-  for (int st = top_pow2(Nc); st > 0; st >>= 1)
-    if (m + st - 1 < Nc && !(sv[m + st - 1] > thr)) m += st;
-  return m;
 }
 
 // The sorted passes stage their tables in LDS (every load of a thread issued before its
@@ -3124,83 +3081,6 @@ __device__ __forceinline__ void divmod_sel(int r, int d, float inv, int& q, int&
 
 constexpr int TB = 32;   // kw_ee_clsb: columns per block (a wave's two halves take two rows)
 __host__ __device__ inline int ee_bwd_tiles(int Ne) { return (Ne + TB - 1) / TB; }
-
-__device__ __forceinline__ void ee_clsb_rows(
-    const int lo, const int hi, const int c0, const float* os_, const uint32_t* abl,
-    const int Ne, const int jn, const bool live, const int nrel, const int dn1, const float inv,
-    const bool aligned, const float* Eq, const float Ej, const float4* gl, const float4* gdl,
-    const float* __restrict__ D, float* rowp, f2 (&acc)[H2], f2 (&ag)[H2], float& sdl,
-    float& zr, int& kst) {
-  const int lane = threadIdx.x & 63, half = lane >> 5;
-  const float bq = D[D_EEBQ];
-  const int trips = (hi - lo + 1) >> 1;
-  int wi = -1;
-  uint32_t word = 0;
-  for (int it = 0; it < trips; ++it) {
-    const int mr = lo + 2 * it + half;           // the half's row
-    const bool inr = mr < hi;
-    const int m = inr ? mr : lo;                 // past the share: a staged row, d1 = 0
-    if ((m >> 5) != wi) { wi = m >> 5; word = abl[wi * TB]; }
-    const bool a1 = (word >> (m & 31)) & 1u;
-    const float af = a1 ? 1.f : 0.f;
-    const f2 a2 = {af, af};
-    const int r = m * (Ne - 1) + jn - (jn > m ? 1 : 0);
-    const bool valid = live && inr && m != jn && r < nrel;
-    float dp;
-    if (aligned) {                     // n = Ne: (i', j') = (i, j)   (block-uniform branch)
-      dp = Eq[m] + Ej;
-    } else {
-      int ip, jj;
-      divmod_sel(r < nrel ? r : 0, dn1, inv, ip, jj);
-      dp = Eq[ip] + Eq[jj + (jj >= ip ? 1 : 0)];
-    }
-    const float* orow = os_ + (m - c0) * H;
-    const float4* o4 = reinterpret_cast<const float4*>(orow);
-    const float4* g4 = a1 ? gdl : gl;            // gam_j + a d: the LDS table by address
-    f2 pre[H2], st[H2];
-#pragma unroll
-    for (int v = 0; v < H / 4; ++v) {   // kappa = rho_i + (gam_j + a d), as kw_ee_fwd
-      const float4 q = o4[v], g = g4[v * TB];
-      pre[2 * v] = (f2){q.x, q.y} + (f2){g.x, g.y};
-      pre[2 * v + 1] = (f2){q.z, q.w} + (f2){g.z, g.w};
-    }
-    f2 dz = {bq, 0.f}, dzb = {0.f, 0.f};   // two chains: the fma latency overlaps
-#pragma unroll
-    for (int kk = 0; kk < H2; ++kk) {  // relu(kappa) = kappa [kappa > 0]
-      st[kk] = step2(pre[kk]);
-      if (kk & 1)
-        dzb = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dzb);
-      else
-        dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
-    }
-    dz += dzb;
-    const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
-    const float p1 = __builtin_amdgcn_rcpf(1.f + e);
-    const float d1 = valid ? (e * p1) * (p1 * dp) : 0.f;
-    const f2 d2 = {d1, d1};
-    sdl += d1;
-    float sv[H];
-#pragma unroll
-    for (int kk = 0; kk < H2; ++kk) {
-      const f2 sd = st[kk] * d2;
-      // as asm: kept ahead of half_sums20's swaps (volatile order), so the swaps work on
-      // the sd registers in place instead of on copies
-      asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc[kk]) : "v"(sd));
-      asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(ag[kk]) : "v"(a2), "v"(sd));
-      sv[2 * kk] = sd.x;
-      sv[2 * kk + 1] = sd.y;
-    }
-    // the half's row sums over the tile's 32 columns: this tile's drho partial (without c:
-    // kw_ee_nodeb scales the summed partials) and, for the classifier's second layer,
-    // sum_j relu(kappa) dz1 = sum_j kappa s dz1: its rho part rho_i . (row sum) here, the
-    // gam + a d part from the column sums after the loop
-    half_sums20(sv, lane, [&](int, int k, float x) {
-      if (inr) rowp[(size_t)m * H + k] = x;
-      zr = fmaf(orow[k], x, zr);
-      kst = k;
-    });
-  }
-}
 
 // The same pair loop with two columns per lane (c and c + 16 of the tile): a wave's four
 // 16-lane quarters take four rows at once, the lane adds its two columns' s-vectors
