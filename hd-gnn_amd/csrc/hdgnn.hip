@@ -1713,6 +1713,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   float* EbG = EG + Ne * HS;
   float* hEG = EbG + Ne * HS;
   float* pb = part + (size_t)prow * NPART;
+  // the rows' fault slots again, contiguous past the 2B rows (work_layout): the reduction
+  // reads 2B consecutive floats instead of one cache line per row
+  float* fsl = part + (size_t)2 * B * NPART;
   constexpr bool GAML = gam_lds(SMAXC);
   // LDS gamma row stride: 8 words past NC16 puts rows 2 apart (the two rows a 32-lane
   // group of pass B reads in split mode) 16 banks apart: no 2-way conflict on its reads
@@ -2631,6 +2634,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   // trailer zeros (fault slot: t = 2) before the rho send, whose vmcnt(0) completes them:
   // a late thread's fault store at the end then lands after them
   if (t < HDG_TRAILER - 2) pb[NP + 2 + t] = 0.f;
+  if (t == 2) fsl[prow] = 0.f;                      // same thread as the fault slot
   if constexpr (SPLIT) pair_send(rho + nlo * HS, (nhi - nlo) * HS, xout + XSLOTS * XS, xtag(epoch, 5) ^ xsend, t);
   MID_STAMP();
   // ---- M13: reductions over rows: dW1' = [x, E_bar, 1]^T dq (waves 0-3),
@@ -2787,6 +2791,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   if (SPLIT && xlate) {
     pb[NP + HDG_TR_CE] = __builtin_nanf("");
     pb[NP + HDG_TR_FAULT] = 1.f;
+    fsl[prow] = 1.f;
     if (status) xstore1(status, HDG_STATUS_XCH_TIMEOUT);
   }
   MID_STAMP();
@@ -2891,10 +2896,11 @@ __global__ __launch_bounds__(1024) void k_reduce_adam(const float* __restrict__ 
   // the update's operands are fetched before the reduction so both latencies overlap
   const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
   const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
-  // split mode: any block whose pair exchange timed out voids the whole update
+  // split mode: any block whose pair exchange timed out voids the whole update (the rows'
+  // fault slots, contiguous past the rows: k_commit_step's fsl)
   bool bad = false;
   for (int r = threadIdx.x; r < fault_rows; r += NT_MID)
-    bad |= part[(size_t)r * NPART + NP + HDG_TR_FAULT] != 0.f;
+    bad |= part[(size_t)fault_rows * NPART + r] != 0.f;
   uint32_t cnt;
   const float g = reduce_commits(part, B, p, p < GRAD_LEN, sh, cnt);
   if (fault_rows > 0 && __syncthreads_or(bad)) upd = false;
@@ -3103,8 +3109,8 @@ __global__ __launch_bounds__(1024) void k_dp_tail(const float* __restrict__ src,
   float g = 0.f;
   bool bad = false;
   if constexpr (MODE == dpk::PART) {
-    for (int q = t; q < fault_rows; q += 1024)
-      bad |= src[(size_t)q * NPART + m2::NP + HDG_TR_FAULT] != 0.f;
+    for (int q = t; q < fault_rows; q += 1024)             // k_commit_step's fsl
+      bad |= src[(size_t)fault_rows * NPART + q] != 0.f;
     uint32_t cnt;
     g = reduce_commits(src, R, p, p < glen, sh, cnt);
     if (t < RED_P && p == CNT_SLOT) s_cnt = cnt;
@@ -3238,7 +3244,8 @@ Work work_layout(const hdg_shape* s) {
   w.Esave = take(3 * B * Ne * HS);
   w.rowq = take((B * Ne * HS + 1) / 2);     // u16
   w.gam = take(B * NC16 * NC16);
-  w.part = take(2 * B * (size_t)NPART);    // one partial row per block (2 per commit split)
+  // one partial row per block (2 per commit split), then the rows' fault slots (2B floats)
+  w.part = take(2 * B * (size_t)NPART + 2 * B);
   w.aux = take(8);
   // block-pair inboxes (split mode): [B][2 halves][XSLOTS][NC16*HS] u64 (value, tag) words;
   // zero at allocation, left zero by every completed launch
@@ -3680,7 +3687,8 @@ int hybrid_run(const hdg_shape* s, const hdg_batch* bt, const float* params, flo
   const int R = part_rows(s, split);
   if (adam) {   // the fused rows are reduced inside the final reduce + Adam kernel
     hdg::WideAdam ad = *adam;
-    ad.fused = hdg::FusedRows{ws + w.part, R, NPART, m2::H1_W1, ins, m2::NP};
+    ad.fused = hdg::FusedRows{ws + w.part, R, NPART, m2::H1_W1, ins, m2::NP,
+                              split ? ws + w.part + (size_t)R * NPART : nullptr};
     if (int rc = hdg::wide_ee_bwd(s, &bw, params, wws, grad, st, &ad)) return rc;
   } else {
     // the fused rows: [0, H1_W1) in place, [H1_W1, GRAD_LEN) past the entity-edge block

@@ -87,6 +87,7 @@ Off param_offsets(int variant);   // NP = -1 for an unknown variant
 struct FusedRows {
   const float* fp;
   int frows, fstride, f_at, f_shift, f_np;
+  const float* ffault;   // split mode: the rows' fault slots, contiguous (NULL: no check)
 };
 struct WideAdam {
   hdg_state* state;

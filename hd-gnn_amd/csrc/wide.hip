@@ -3591,9 +3591,8 @@ __global__ __launch_bounds__(NT) void kw_reduce_adam(
   // the first one is used, and the fault flag is OR-ed at the block's one barrier: the
   // kernel is one memory round trip deep.  Sums keep their fixed row order.
   bool bad = false;   // the step kernel's fault slot: any block-pair exchange timed out
-  if (fr.fp)
-    for (int r = t; r < fr.frows; r += NT)
-      bad |= fr.fp[(size_t)r * fr.fstride + fr.f_np + HDG_TR_FAULT] != 0.f;
+  if (fr.ffault)
+    for (int r = t; r < fr.frows; r += NT) bad |= fr.ffault[r] != 0.f;
   if ((int)blockIdx.x < nfb) {
     const int sl = t & 15, ph = t >> 4;
     const int p2 = blockIdx.x * 16 + sl;
