@@ -100,6 +100,24 @@ __device__ __forceinline__ void row16_sum5(float* v) {
 #undef HDG_DPP_STEP4
 #undef HDG_DPP_STEP3
 #undef HDG_DPP_STEP
+#ifndef HDG_SETPRIO  // wave priority by progress in the pair passes, E1, E2 and M7 (0 = off)
+#define HDG_SETPRIO 1
+#endif
+// Wave priority by progress.  The SIMD's issue arbiter favours the oldest wave, so in a
+// phase of equal per-wave work wave 0 of each SIMD finishes first and the youngest runs its
+// last trips alone, with nothing to hide its latencies (the per-wave stamps show the
+// stagger: E1 done at 1.8 / 2.1 / 2.6 / 3.1 us for waves 0-3 / 4-7 / 8-11 / 12-15).  A wave
+// lowers its priority as it passes trips / milestones, so waves that are behind get the
+// issue slots first and the SIMD's waves finish together: pair passes M5 / M8 / M10
+// 4.60 / 5.56 / 7.04 -> 4.20 / 5.08 / 6.52 us, E1 3.12 -> 2.80, median block 54.8 -> 53.2 us
+// (tools/gpu_ph_ab.sh, two runs each).  Priority 3, 2, 1, 0 for trips 0, 1, 2, later
+// (s_setprio takes an immediate).
+__device__ __forceinline__ void trip_prio(int s) {
+  if (s == 0) __builtin_amdgcn_s_setprio(3);
+  else if (s == 1) __builtin_amdgcn_s_setprio(2);
+  else if (s == 2) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
 #ifndef HDG_HOIST   // pair tiles: the columns' B (and MODE 1 wc) operands held in registers
 #define HDG_HOIST 1  // for the whole sweep instead of re-read from LDS every 16-row trip
 #endif
@@ -387,6 +405,10 @@ __device__ __forceinline__ void pair_tile(
     }
   }
   for (int s = 0; s < S; ++s) {
+    // waves still on an earlier trip get the issue arbiter first (it otherwise favours
+    // the oldest wave, which finishes its trips first and leaves the SIMD to one wave at
+    // the end of the pass)
+    if constexpr (HDG_SETPRIO) trip_prio(s);
     if (wrow + 16 * s >= nown) continue;    // wave-uniform: no row of this wave in the trip
     const int r = ti + 16 * s;
     const int i = rmul * r + radd;
@@ -512,6 +534,7 @@ __device__ __forceinline__ void pair_tile(
     yacc[2 * p + 1] = yacc2[p].y;
   }
   if constexpr (KT) yacc[KK - 1] = yacct;
+  if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(0);
   // close the column partials: 4 ti per wave by shuffles, then 4 waves via LDS
   float* credy = cred + 4 * NP16 * KK;
   {                          // column partials summed over the wave's 4 rows (transposed)
@@ -588,6 +611,10 @@ __device__ __forceinline__ void pair_tile32(
   }
 
   for (int s = 0; s < S; ++s) {
+    // waves still on an earlier trip get the issue arbiter first (it otherwise favours
+    // the oldest wave, which finishes its trips first and leaves the SIMD to one wave at
+    // the end of the pass)
+    if constexpr (HDG_SETPRIO) trip_prio(s);
     if (wrow + 8 * s >= nown) continue;     // wave-uniform skip
     const int r = ti + 8 * s;
     const int i = rmul * r + radd;
@@ -684,6 +711,7 @@ __device__ __forceinline__ void pair_tile32(
       for (int k = 0; k < KK; ++k) Rout[i * LD + kof(k)] = rs[k];
     }
   }
+  if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(0);
   float cf[SMAX * KK], yacc[KK];
 #pragma unroll
   for (int c = 0; c < SMAX; ++c) {
@@ -1288,6 +1316,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f}, ca[2] = {ea.w0 >= 0.f, eb.w0 >= 0.f};
   constexpr int NG = NT_MID / EG_L;                // 102 node groups per pass
   for (int base = n0; base < n1; base += NG) {       // block-uniform
+    if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(3);   // milestones: see trip_prio
     const int i = base + sub;
     const bool live = sub < NG && i < n1;
     const int ic = live ? i : 0;
@@ -1314,6 +1343,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
       br[h] = br[h] < nd ? br[h] : nd;
       bc[h] = bc[h] < nd ? bc[h] : nd;
     }
+    if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(2);
     // the a = 0 set sums: cnt u + w1 sum x (row side), cnt (v + c0) + w0 sum x (column
     // side).  The x sums are differences of the f64 prefix table (exact to 2^-53 of the
     // set, rounded once to f32); the rest in f32 with fma: the same rounding order as the
@@ -1374,6 +1404,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
     };
     xsum(xlr, ((ABL & 4) || !live) ? 0 : offr[ic], ((ABL & 4) || !live) ? 0 : offr[ic + 1],
          sg * w1 * rd, __builtin_elementwise_fma(sg, u, tg) * rd);
+    if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(1);
     xsum(xlc, ((ABL & 8) || !live) ? 0 : offc[ic], ((ABL & 8) || !live) ? 0 : offc[ic + 1],
          sg * w0 * rd, __builtin_elementwise_fma(sg, c0 + v, tg) * rd);
     sp *= dd;
@@ -1385,6 +1416,7 @@ __device__ __forceinline__ void entity_fwd(const int t, const float* Ws,
       rq[i * HS + k0 + 1] = (uint16_t)br[1];
     }
   }
+  if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // E2 body: per-wave partial sums S0..S3 (dW1 rows, model_2.py:165-170 backward) for
@@ -1405,7 +1437,9 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
   // rounds of 96 nodes; wave w takes nodes w + 16 s (s < 6) of a round, so the last,
   // partial round's nodes land on as many waves -- and SIMDs -- as there are nodes
   constexpr int NWV = NT_MID / 64;
+  int ms = 0;                                      // progress milestones (trip_prio)
   for (int base = n0; base + wv < n1; base += EG_N * NWV) {   // wave-uniform
+    if constexpr (HDG_SETPRIO) trip_prio(ms++);
     const int i = base + wv + NWV * sub;
     const bool live = sub < EG_N && i < n1;
     const int ic = live ? i : 0;
@@ -1434,6 +1468,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       s1[h] = a1;
       s2[h] = rs;
     }
+    if constexpr (HDG_SETPRIO) trip_prio(ms++);
     f2 sd = {0.f, 0.f}, sx = sd;                     // sum dm, sum x_j dm
     // row neighbours from the padded (id, x) lists: 4 ids in one u32 and 4 x values in one
     // 16-byte read per step, identical across the node group's lanes (LDS broadcast)
@@ -1472,6 +1507,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
     s2 += sd;
     if (live) { S0 += s0; S1 += s1; S2 += s2; S3 += s3; }
   }
+  if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(0);
   // fold the 6 node groups (lanes kp + 10 s), then lanes 0..9 write the wave's sums
   f2 sv[4] = {S0, S1, S2, S3};
 #pragma unroll
@@ -2146,7 +2182,9 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
         gam[(rmul * r2 + radd) * GLD + Nc + (e - r2 * npad)] = 0.f;
       }
     }
+    int trip = 0;
     for (int el = t; el < Pown; el += NT_MID) {
+      if constexpr (HDG_SETPRIO) trip_prio(trip++);
       const int p = rmul * r + radd;
       const int e = SPLIT ? p * Nc1i + qq : el;
       const int q = qq + (qq >= p ? 1 : 0);
@@ -2227,6 +2265,7 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
       }
     }
   }
+  if constexpr (HDG_SETPRIO) __builtin_amdgcn_s_setprio(0);
   WAVE_STAMP(1);
   if constexpr (TRAIN) {   // red[wv][0] CE, [1] sum gamma, [2 + HS] count
     float v[3] = {ce_acc, gsum, corr};
