@@ -552,6 +552,38 @@ __device__ __forceinline__ void block_sum8(float (&v)[NV], float* red, float* ou
   __syncthreads();
 }
 
+#ifndef HDG_WPRIO   // wave priority by progress through the wave's share: kw_hunk_fwd and
+#define HDG_WPRIO 1  // kw_hunk_mlpb (stress, dense form: 35.0 -> 33.8 and 54.3 -> 52.1 us; in
+#endif               // kw_hunk_clsb it cost 66.7 -> 73.5 us, in kw_hunk_cls nothing)
+// priority 3 / 2 / 1 / 0 from the start / first quarter / half / three quarters of a wave's
+// share (the issue arbiter then favours waves that are behind; all values wave-uniform)
+__device__ __forceinline__ void share_prio(int m, int lo, int hi) {
+  if constexpr (HDG_WPRIO) {
+    const int d = m - lo, n = hi - lo;
+    if (d == 0) __builtin_amdgcn_s_setprio(3);
+    else if (d == n >> 2) __builtin_amdgcn_s_setprio(2);
+    else if (d == n >> 1) __builtin_amdgcn_s_setprio(1);
+    else if (d == (3 * n) >> 2) __builtin_amdgcn_s_setprio(0);
+  }
+}
+__device__ __forceinline__ void prio0() {
+  if constexpr (HDG_WPRIO) __builtin_amdgcn_s_setprio(0);
+}
+#ifndef HDG_EPRIO   // experiment: the same in kw_ee_fwd's relation loop / kw_ee_clsb's trips
+#define HDG_EPRIO 0
+#endif
+__device__ __forceinline__ void trip_prio_e(int it, int n) {
+  if constexpr (HDG_EPRIO) {
+    if (it == 0) __builtin_amdgcn_s_setprio(3);
+    else if (it == n >> 2) __builtin_amdgcn_s_setprio(2);
+    else if (it == n >> 1) __builtin_amdgcn_s_setprio(1);
+    else if (it == (3 * n) >> 2) __builtin_amdgcn_s_setprio(0);
+  }
+}
+__device__ __forceinline__ void prio0_e() {
+  if constexpr (HDG_EPRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 // the wave's share [lo, hi) of chunk [c0, c1)
 __device__ __forceinline__ void wave_share(int c0, int c1, int& lo, int& hi) {
   const int w = uni(threadIdx.x >> 6), len = c1 - c0;
@@ -1105,6 +1137,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   EE_STAMP(2);
   WSTAMP(5, 2);
   for (int it = 0; it < trips; ++it) {
+    trip_prio_e(it, trips);
     const int jp = jlo + it;
     const bool valid = live && jp < jhi && jp != ip;
     float p0 = 0.f, p1 = 0.f;
@@ -1161,6 +1194,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     const float v = row_total16(x + y);
     if ((lane & 15) == 0 && jp < jhi) tsum[2 * jp + ((lane >> 4) & 1)] = v;
   }
+  prio0_e();
   EE_STAMP(3);
   WSTAMP(5, 3);
   if (live) {                          // source bins: the lane's row i'
@@ -1290,6 +1324,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
     int wi = -1;
     uint32_t word = 0;
     for (int m = lo; m < hi; ++m) {
+      share_prio(m, lo, hi);
       if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
       const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
       const f2 y2 = {yf, yf};
@@ -1303,6 +1338,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
         acc[2 * v + 1] = fma2(zb, step2(zb), acc[2 * v + 1]);
       }
     }
+    prio0();
   }
   if ((threadIdx.x >> 6) == 0) {   // remove the self pair once
     const float yf = bitf(brow, ncl);
@@ -1707,6 +1743,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
     int wi = -1;
     uint32_t word = 0;
     for (int m = lo; m < hi; ++m) {
+      share_prio(m, lo, hi);
       if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
       const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
       const f2 y2 = {yf, yf};
@@ -1726,6 +1763,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb(
         ya[2 * v + 1] = fma2(y2, db, ya[2 * v + 1]);
       }
     }
+    prio0();
   }
   if ((threadIdx.x >> 6) == 0) {   // remove the self pair once
     const float yf = bitf(brow, ncl);
@@ -3101,6 +3139,7 @@ __device__ __forceinline__ void ee_clsb_rows_q(
   int wi = -1;
   uint32_t word0 = 0, word1 = 0;
   for (int it = 0; it < trips; ++it) {
+    trip_prio_e(it, trips);
     const int mr = lo + 4 * it + qr;             // the quarter's row
     const bool inr = mr < hi;
     const int m = inr ? mr : lo;                 // past the share: a staged row, d1 = 0
@@ -3260,6 +3299,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
     ee_clsb_rows_q(lo, hi, c0, os_, abl, Ne, t0, nrel, dn1, inv, aligned, Eq, gl4, gdl4, D,
                    rowp, acc0, acc1, ag, sdl, zr, kst);
   }
+  prio0_e();
   for (int e = lane; e < 4 * H; e += 64) zred[wv * 4 * H + e] = 0.f;
   __syncthreads();
 #pragma unroll
