@@ -1377,8 +1377,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     const float* __restrict__ tau, float* __restrict__ probs, float* __restrict__ logits,
     float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float ss[CHM * H];
-  __shared__ __attribute__((aligned(16))) float se[CHM * H];   // sigma + eps (y = 1 rows)
+  // sigma rows | 4 pad words | sigma + eps (the y = 1 rows): a lane's row is picked by its
+  // y bit, and the pad puts the two tables' rows on different banks (the b128 reads of a
+  // wave hit two addresses, else 2-way conflicts: the tables are 2560 words apart)
+  __shared__ __attribute__((aligned(16))) float sst[2 * CHM * H + 4];
+  float* ss = sst;
+  float* se = sst + CHM * H + 4;
   __shared__ float red[NWP * 23];
   __shared__ float tot[23];
   const int b = blockIdx.y, t0 = blockIdx.x * TN, tc = gridDim.x;
@@ -1418,28 +1422,49 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
       const float yf = ((word >> (p & 31)) & 1u) ? 1.f : 0.f;
       const float4* s4 = reinterpret_cast<const float4*>((yf > 0.f ? se : ss) + (p - c0) * H);
       f2 kap[H2];
-      f2 zz = bb;
 #pragma unroll
       for (int v = 0; v < H / 4; ++v) {
         const float4 sv = s4[v];
         kap[2 * v] = relu2((f2){sv.x, sv.y} + tq[2 * v]);
         kap[2 * v + 1] = relu2((f2){sv.z, sv.w} + tq[2 * v + 1]);
       }
+      float p0, p1, cep;
+      if (lgb) {   // both logits (returned; probs = softmax of them, block-uniform branch)
+        f2 zz = bb;
 #pragma unroll
-      for (int kk = 0; kk < H2; ++kk) {
-        zz = fma2((f2){kap[kk].x, kap[kk].x}, ld2(W + o.H2_W2 + 4 * kk), zz);
-        zz = fma2((f2){kap[kk].y, kap[kk].y}, ld2(W + o.H2_W2 + 4 * kk + 2), zz);
-      }
-      const float z0 = zz.x, z1 = zz.y;
-      if (live && q != p) {
+        for (int kk = 0; kk < H2; ++kk) {
+          zz = fma2((f2){kap[kk].x, kap[kk].x}, ld2(W + o.H2_W2 + 4 * kk), zz);
+          zz = fma2((f2){kap[kk].y, kap[kk].y}, ld2(W + o.H2_W2 + 4 * kk + 2), zz);
+        }
+        const float z0 = zz.x, z1 = zz.y;
         const float mx = fmaxf(z0, z1);
         const float e0 = __expf(z0 - mx), e1 = __expf(z1 - mx);
         const float ssum = e0 + e1, inv = __builtin_amdgcn_rcpf(ssum);   // [1, 2]: 1-ulp rcp
-        const float p0 = e0 * inv, p1 = e1 * inv;
+        p0 = e0 * inv;
+        p1 = e1 * inv;
+        cep = (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+        if (live && q != p) {
+          const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
+          lgb[r] = z0;
+          lgb[Pc + r] = z1;
+        }
+      } else {     // two classes need only d = z1 - z0 = relu(kappa) . c + (b1 - b0), as the
+                   // fused kernel's M7: p1 = 1 / (1 + e^-d), CE = softplus(-+d)
+        f2 dd = {bb.y - bb.x, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < H2; ++kk) dd = fma2(kap[kk], ld2(D + D_CV + 2 * kk), dd);
+        const float d = dd.x + dd.y;
+        const float ex = __expf(-fabsf(d));
+        const float inv = __builtin_amdgcn_rcpf(1.f + ex);   // 1 + e in (1, 2]: 1-ulp rcp
+        const float ps = ex * inv;
+        p1 = d >= 0.f ? inv : ps;
+        p0 = d >= 0.f ? ps : inv;
+        cep = __logf(1.f + ex) + relu(yf > 0.f ? -d : d);
+      }
+      if (live && q != p) {
         const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
         if (prb) { prb[r] = p0; prb[Pc + r] = p1; }
-        if (lgb) { lgb[r] = z0; lgb[Pc + r] = z1; }
-        ce += (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+        ce += cep;
         corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
         if constexpr (TRAIN) {
           const float g = ce_scale * (p1 - yf);
@@ -1575,7 +1600,10 @@ __device__ __forceinline__ void clsb_epilogue(
 //   column pass: Dtau_q = c (.) sum_p e_pq.  Epilogue: dG = Dsig M^T (dH = Dtau M^T) and
 //   the partial rows of dU1 (rows 0..1 from the row pass, rows 2..21 through
 //   X = sum_p G_p (x) Dsig_p + H_p (x) Dtau_p), dd1, dV2 and dc2 (model_2.py:265-275).
-//   The row pass reads gamma through a transposing LDS tile (coalesced global loads).
+//   kappa = own + (other + y eps): the y = 1 rows of the swept side from a second staged
+//   table (picked by address, as kw_hunk_cls), so the column pass's kappa is the forward's
+//   bit for bit.  The row pass reads gamma through a transposing LDS tile (coalesced 16-byte
+//   global loads, no index division).
 // ---------------------------------------------------------------------------------
 constexpr int GTP = CHM + 1;   // gamma tile pitch
 __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
@@ -1587,11 +1615,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
   // the swept rows and the gamma tile are dead once the sweep ends: combine8's buffer
-  // overlays them (66 KB of LDS instead of 109: two blocks per CU)
-  constexpr int SWEEP_W = CHM * H + TN * GTP, BUF_W = NWP * TN * HP;
+  // overlays them (76 KB of LDS: two blocks per CU)
+  constexpr int SWEEP_W = 2 * CHM * H + 4 + TN * GTP, BUF_W = NWP * TN * HP;
   __shared__ __attribute__((aligned(16))) float big[SWEEP_W > BUF_W ? SWEEP_W : BUF_W];
   float* os_ = big;
-  float* gt = big + CHM * H;
+  float* ose = big + CHM * H + 4;                 // other + eps: the y = 1 rows (4 pad words:
+  float* gt = big + 2 * CHM * H + 4;              // its rows on other banks than os_'s)
   float* buf = big;
   __shared__ float res[TN * HP], yres[TN * HP], Gt[TN * HP];
   __shared__ float X[H * H], sumD[H], ysum[H];
@@ -1610,23 +1639,50 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
   const float* oth = (z ? sig : tau) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
   const float* gb = gam + (size_t)b * Nc * Nc;
-  f2 ow[H2], ep[H2], acc[H2], ya[H2];
+  f2 ow[H2], acc[H2], ya[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
     ow[kk] = ld2(own + ncl * H + 2 * kk);
-    ep[kk] = ld2(D + D_EPS + 2 * kk);
     acc[kk] = (f2){0.f, 0.f};
     ya[kk] = (f2){0.f, 0.f};
   }
+  // gamma tile loads: thread -> (row tr + 16 i, 4 columns at tc4); rows / columns past the
+  // grid read a clamped address and store 0
+  const int tr = threadIdx.x >> 5, tc4 = (threadIdx.x & 31) * 4;
+  const bool al4 = (Nc & 3) == 0;                 // rows 16-byte aligned: float4 loads
   for (int c0 = 0; c0 < Nc; c0 += CHM) {   // gamma's diagonal is 0: no self pair to remove
     const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
     __syncthreads();
     stage_rows(os_, oth, c0, c1);
+    for (int e = threadIdx.x; e < (c1 - c0) * H; e += NTP)
+      ose[e] = oth[(size_t)c0 * H + e] + D[D_EPS + e % H];
     if (z == 0) {
-      const int len = c1 - c0;
-      for (int e = threadIdx.x; e < TN * len; e += NTP) {
-        const int r = e / len, c = e - r * len;
-        gt[r * GTP + c] = (t0 + r < Nc) ? gb[(size_t)(t0 + r) * Nc + c0 + c] : 0.f;
+      float4 gv[TN / 16];
+      const int cg = c0 + tc4;
+#pragma unroll
+      for (int i = 0; i < TN / 16; ++i) {
+        const int r = t0 + tr + 16 * i;
+        const float* src = gb + (size_t)(r < Nc ? r : Nc - 1) * Nc;
+        if (al4 && cg + 3 < c1) {
+          gv[i] = *reinterpret_cast<const float4*>(src + cg);
+        } else {
+          gv[i].x = cg < c1 ? src[cg] : 0.f;
+          gv[i].y = cg + 1 < c1 ? src[cg + 1] : 0.f;
+          gv[i].z = cg + 2 < c1 ? src[cg + 2] : 0.f;
+          gv[i].w = cg + 3 < c1 ? src[cg + 3] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TN / 16; ++i) {
+        const int rl = tr + 16 * i;
+        const bool rin = t0 + rl < Nc;
+        float* d = gt + rl * GTP + tc4;
+        if (tc4 < c1 - c0) {
+          d[0] = rin ? gv[i].x : 0.f;
+          d[1] = rin ? gv[i].y : 0.f;
+          d[2] = rin ? gv[i].z : 0.f;
+          d[3] = rin ? gv[i].w : 0.f;
+        }
       }
     }
     __syncthreads();
@@ -1636,21 +1692,20 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     uint32_t word = 0;
     for (int m = lo; m < hi; ++m) {
       if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
-      const float yf = ((word >> (m & 31)) & 1u) ? 1.f : 0.f;
-      const f2 y2 = {yf, yf};
+      const bool y1 = (word >> (m & 31)) & 1u;
       const float g = z ? gb[(size_t)m * Nc + ncl] : gt[lane * GTP + (m - c0)];
-      const float4* o4 = reinterpret_cast<const float4*>(os_ + (m - c0) * H);
+      const f2 g2 = {g, g}, gy2 = y1 ? g2 : (f2){0.f, 0.f};
+      // [kappa > 0] g and [kappa > 0] y g as one fma each (the products are exact)
+      const float4* o4 = reinterpret_cast<const float4*>((y1 ? ose : os_) + (m - c0) * H);
 #pragma unroll
       for (int v = 0; v < H / 4; ++v) {
         const float4 q = o4[v];
-        const f2 pa = fma2(y2, ep[2 * v], ow[2 * v] + (f2){q.x, q.y});
-        const f2 pb = fma2(y2, ep[2 * v + 1], ow[2 * v + 1] + (f2){q.z, q.w});
-        const f2 ea = step2(pa) * (f2){g, g};   // [p > 0] g (gamma finite, 0 on the diagonal)
-        const f2 eb = step2(pb) * (f2){g, g};
-        acc[2 * v] += ea;
-        acc[2 * v + 1] += eb;
-        ya[2 * v] = fma2(y2, ea, ya[2 * v]);
-        ya[2 * v + 1] = fma2(y2, eb, ya[2 * v + 1]);
+        const f2 sa = step2(ow[2 * v] + (f2){q.x, q.y});
+        const f2 sb = step2(ow[2 * v + 1] + (f2){q.z, q.w});
+        acc[2 * v] = fma2(sa, g2, acc[2 * v]);   // gamma finite, 0 on the diagonal
+        acc[2 * v + 1] = fma2(sb, g2, acc[2 * v + 1]);
+        ya[2 * v] = fma2(sa, gy2, ya[2 * v]);
+        ya[2 * v + 1] = fma2(sb, gy2, ya[2 * v + 1]);
       }
     }
   }
