@@ -453,6 +453,7 @@ __device__ __forceinline__ void pair_tile(
         const float gl = gam[ic * gld + jc];
         g = (iv && j < NCOL && j + doff != i) ? gl : 0.f;
       }
+      const float gy = af * g;             // MODE 2: exact (af is 0 or 1)
       const float* Bj = Bv + j * LD;
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
@@ -466,14 +467,17 @@ __device__ __forceinline__ void pair_tile(
           const p2 sz = step2(z);
           racc2[p] = __builtin_elementwise_fma(z, sz, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(z, sz, cacc2[c][p]);
+        } else if constexpr (MODE == 2) {
+          // w = g is one value per pair: [z > 0] g and [z > 0] a g as one fma each (the
+          // products are exact: the same bits as multiply, then add)
+          const p2 sz = step2(z), g2 = {g, g}, gy2 = {gy, gy};
+          yacc2[p] = __builtin_elementwise_fma(sz, gy2, yacc2[p]);
+          racc2[p] = __builtin_elementwise_fma(sz, g2, racc2[p]);
+          cacc2[c][p] = __builtin_elementwise_fma(sz, g2, cacc2[c][p]);
         } else {
           p2 w;
-          if constexpr (MODE == 1) {
-            if constexpr (HW) w = rw2[p] + wcol[c][p];
-            else w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
-          } else {
-            w = (p2){g, g};
-          }
+          if constexpr (HW) w = rw2[p] + wcol[c][p];
+          else w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
           const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;
@@ -654,6 +658,7 @@ __device__ __forceinline__ void pair_tile32(
         const float gl = gam[ic * gld + jc];
         g = (iv && j < N && j != i) ? gl : 0.f;
       }
+      const float gy = af * g;             // MODE 2: exact (af is 0 or 1)
       const float* Bj = Bv + j * LD;
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
@@ -665,13 +670,13 @@ __device__ __forceinline__ void pair_tile32(
           const p2 sz = step2(z);
           racc2[p] = __builtin_elementwise_fma(z, sz, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(z, sz, cacc2[c][p]);
+        } else if constexpr (MODE == 2) {   // as pair_tile: one exact fma per sum
+          const p2 sz = step2(z), g2 = {g, g}, gy2 = {gy, gy};
+          yacc2[p] = __builtin_elementwise_fma(sz, gy2, yacc2[p]);
+          racc2[p] = __builtin_elementwise_fma(sz, g2, racc2[p]);
+          cacc2[c][p] = __builtin_elementwise_fma(sz, g2, cacc2[c][p]);
         } else {
-          p2 w;
-          if constexpr (MODE == 1) {
-            w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
-          } else {
-            w = (p2){g, g};
-          }
+          const p2 w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
           const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;

@@ -40,6 +40,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "hdgnn.h"
 #include "hdgnn_internal.h"
 
@@ -1606,7 +1608,7 @@ __device__ __forceinline__ void clsb_epilogue(
 //   global loads, no index division).
 // ---------------------------------------------------------------------------------
 constexpr int GTP = CHM + 1;   // gamma tile pitch
-__global__ __launch_bounds__(NTP) void kw_hunk_clsb(
+__global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void kw_hunk_clsb(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Nc,
     const float* __restrict__ sig, const float* __restrict__ tau, const float* __restrict__ gam,
@@ -1688,26 +1690,36 @@ __global__ __launch_bounds__(NTP) void kw_hunk_clsb(
     __syncthreads();
     int lo, hi;
     wave_share(c0, c1, lo, hi);
-    int wi = -1;
-    uint32_t word = 0;
-    for (int m = lo; m < hi; ++m) {
-      if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
-      const bool y1 = (word >> (m & 31)) & 1u;
-      const float g = z ? gb[(size_t)m * Nc + ncl] : gt[lane * GTP + (m - c0)];
-      const f2 g2 = {g, g}, gy2 = y1 ? g2 : (f2){0.f, 0.f};
-      // [kappa > 0] g and [kappa > 0] y g as one fma each (the products are exact)
-      const float4* o4 = reinterpret_cast<const float4*>((y1 ? ose : os_) + (m - c0) * H);
+    // one loop per pass (block-uniform): gamma from the LDS tile (row pass) or global
+    // memory (column pass) by its own load instruction, not a flat load through a selected
+    // pointer; the column pass has no y-weighted sums
+    auto sweep = [&](auto row_pass) {
+      constexpr bool ROW = decltype(row_pass)::value;
+      int wi = -1;
+      uint32_t word = 0;
+      for (int m = lo; m < hi; ++m) {
+        if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
+        const bool y1 = (word >> (m & 31)) & 1u;
+        const float g = ROW ? gt[lane * GTP + (m - c0)] : gb[(size_t)m * Nc + ncl];
+        const f2 g2 = {g, g}, gy2 = y1 ? g2 : (f2){0.f, 0.f};
+        // [kappa > 0] g and [kappa > 0] y g as one fma each (the products are exact)
+        const float4* o4 = reinterpret_cast<const float4*>((y1 ? ose : os_) + (m - c0) * H);
 #pragma unroll
-      for (int v = 0; v < H / 4; ++v) {
-        const float4 q = o4[v];
-        const f2 sa = step2(ow[2 * v] + (f2){q.x, q.y});
-        const f2 sb = step2(ow[2 * v + 1] + (f2){q.z, q.w});
-        acc[2 * v] = fma2(sa, g2, acc[2 * v]);   // gamma finite, 0 on the diagonal
-        acc[2 * v + 1] = fma2(sb, g2, acc[2 * v + 1]);
-        ya[2 * v] = fma2(sa, gy2, ya[2 * v]);
-        ya[2 * v + 1] = fma2(sb, gy2, ya[2 * v + 1]);
+        for (int v = 0; v < H / 4; ++v) {
+          const float4 q = o4[v];
+          const f2 sa = step2(ow[2 * v] + (f2){q.x, q.y});
+          const f2 sb = step2(ow[2 * v + 1] + (f2){q.z, q.w});
+          acc[2 * v] = fma2(sa, g2, acc[2 * v]);   // gamma finite, 0 on the diagonal
+          acc[2 * v + 1] = fma2(sb, g2, acc[2 * v + 1]);
+          if constexpr (ROW) {
+            ya[2 * v] = fma2(sa, gy2, ya[2 * v]);
+            ya[2 * v + 1] = fma2(sb, gy2, ya[2 * v + 1]);
+          }
+        }
       }
-    }
+    };
+    if (z == 0) sweep(std::true_type{});
+    else sweep(std::false_type{});
   }
   __syncthreads();                       // every wave is done with os_ / gt (= buf)
   combine8(acc, buf, res);
