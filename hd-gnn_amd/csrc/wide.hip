@@ -1366,12 +1366,14 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd(const uint32_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------
-// kw_hunk_cls  grid (tc, B): lane = hunk column q, the 8 waves split the rows p
+// kw_hunk_cls  grid (tc, B, CLS_SPLIT): lane = hunk column q, grid z and then the 8 waves
+//   split the rows p
 //   mlp_hunkedge_B2 (model_2.py:304-324) + softmax CE (115-118):
 //     kappa_pq = relu(sigma_p + tau_q + y_pq eps), z = kappa U2 + d2, CE = lse(z) - z_y
 //   TRAIN: gamma_pq = 10 / (B Pc) (p1 - y) = dL/dz1 (= -dL/dz0), parked for the backward;
 //   partial rows of dU2, dd2 and the CE sum
 // ---------------------------------------------------------------------------------
+constexpr int CLS_SPLIT = 2;   // kw_hunk_cls row ranges per column tile (grid z)
 template <bool TRAIN>
 __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     const uint32_t* __restrict__ yT, const float* __restrict__ W, Off o,
@@ -1408,8 +1410,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   f2 za[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) za[kk] = (f2){0.f, 0.f};
-  for (int c0 = 0; c0 < Nc; c0 += CHM) {
-    const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
+  // grid z splits the rows p into gridDim.z contiguous ranges (more waves per SIMD; one
+  // partial row each)
+  const int r0 = (Nc * (int)blockIdx.z) / (int)gridDim.z;
+  const int r1 = (Nc * ((int)blockIdx.z + 1)) / (int)gridDim.z;
+  for (int c0 = r0; c0 < r1; c0 += CHM) {
+    const int c1 = c0 + CHM < r1 ? c0 + CHM : r1;
     __syncthreads();
     stage_rows(ss, sgb, c0, c1);
     for (int e = threadIdx.x; e < (c1 - c0) * H; e += NTP)
@@ -1487,7 +1493,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
   for (int kk = 0; kk < H2; ++kk) { acc[2 + 2 * kk] = za[kk].x; acc[3 + 2 * kk] = za[kk].y; }
   acc[22] = corr;
   block_sum8<23>(acc, red, tot);
-  const int row = b * tc + blockIdx.x;
+  const int row = (b * tc + blockIdx.x) * gridDim.z + blockIdx.z;
   if (threadIdx.x == 0) {
     put(part, sg.s[SG_CE], 0, row, tot[0]);
     put(part, sg.s[SG_CE], 1, row, tot[22]);
@@ -3973,8 +3979,8 @@ WideWork wide_layout(const hdg_shape* s) {
     w.segs.s[id].rows = rows;
     w.segs.s[id].off = (long long)take((size_t)n * rows);
   };
-  seg(SG_CLS, o.H2_W2, 42, rc);
-  seg(SG_CE, o.NP, 2, rc);
+  seg(SG_CLS, o.H2_W2, 42, CLS_SPLIT * rc);
+  seg(SG_CE, o.NP, 2, CLS_SPLIT * rc);
   seg(SG_CLSB_H2, o.H2_W1, 460, 2 * rc);
   seg(SG_CLSB_H1, o.H1_W2, 420, 2 * rc);
   seg(SG_MLPB, o.H1_W1, 220, 2 * rc);
@@ -4336,7 +4342,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   float* probs = out ? out->probs : nullptr;
   float* logits = out ? out->logits : nullptr;
   if (!train) {
-    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D,
+    hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B, CLS_SPLIT), dim3(NTP), 0, st, yT, params,
+                       o, D,
                        Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
     WTRY(kmark("kw_hunk_cls", st));
     if (ce_sum) {
@@ -4349,7 +4356,8 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
     return 0;
   }
-  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B), dim3(NTP), 0, st, yT, params, o, D, Nc,
+  hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B, CLS_SPLIT), dim3(NTP), 0, st, yT, params,
+                     o, D, Nc,
                      F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
   WTRY(kmark("kw_hunk_cls", st));
   if (ht) {
