@@ -12,5 +12,6 @@ step() {   # step <name> <timeout> <cmd...>
 }
 HDG_PARITY_REPORT=gpurun_out/parity_report.json step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python __graft_entry__.py smoke
+step bench_driver_cmd 300 python bench.py --gpus 1 --steps 20 --warmup 5
 step bench 600 python bench.py --e2e 50
 step phases 200 python tools/mid_phases.py

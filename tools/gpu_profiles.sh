@@ -7,7 +7,8 @@ source "$R/tools/configs.sh"
 RND=$1
 shift
 TAGS=${*:-$ORDER}
-if [ ! -f "$R/gpurun_out/$RND/cal/done" ]; then
+# NOCAL=1: skip the counter calibration (profiles/<round>/calibration.json already committed)
+if [ -z "$NOCAL" ] && [ ! -f "$R/gpurun_out/$RND/cal/done" ]; then
   bash "$R/tools/calibrate.sh" "$RND" || exit $?
   touch "$R/gpurun_out/$RND/cal/done"
 fi
