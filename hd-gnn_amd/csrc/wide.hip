@@ -2808,8 +2808,24 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     const float* dnb = dn + (size_t)b * Nc * 4;
     const int c0 = (Nc * w) / NW, c1 = (Nc * (w + 1)) / NW;
     float a = 0.f;
-    if (I < Ne) {                  // four hunks' counts in flight per step, same fma order
+    if (I < Ne) {                  // NB_U hunks' counts in flight per step, same fma order
+      constexpr int NB_U = 16;     // (a wave walks Nc / 4 hunks: at Nc = 512, 8 round trips)
       int c = c0;
+      for (; c + NB_U <= c1; c += NB_U) {
+        float vs[NB_U], vt[NB_U], d0[NB_U], d1[NB_U];
+#pragma unroll
+        for (int u = 0; u < NB_U; ++u) {
+          vs[u] = (float)ks[(size_t)(c + u) * Ne + I];
+          vt[u] = (float)kt[(size_t)(c + u) * Ne + I];
+          d0[u] = dnb[4 * (c + u)];
+          d1[u] = dnb[4 * (c + u) + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < NB_U; ++u) {
+          a = fmaf(d0[u], vs[u], a);
+          a = fmaf(d1[u], vt[u], a);
+        }
+      }
       for (; c + 4 <= c1; c += 4) {
         float vs[4], vt[4], d0[4], d1[4];
 #pragma unroll
