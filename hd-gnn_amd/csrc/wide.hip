@@ -1011,9 +1011,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
 constexpr int TF = 32;                // index rows per kw_ee_fwd block
 constexpr int EE_TAB_LDS_MAX = 400;   // Ne up to which gam, gam + d sit in LDS
 __host__ __device__ inline int ee_fwd_tiles(int Ne) { return (Ne + TF - 1) / TF; }
+// table modes: 1 gam and gam + d in LDS (Ne <= EE_TAB_LDS_MAX), 2 gam alone in LDS (+ a d
+// by one fma per unit pair; while it fits), 0 gam rows from HBM / L2
+__host__ __device__ inline size_t ee_fwd_head(int Ne, int Nc) {
+  return (size_t)((2 * Nc + 1) & ~1) * 8 + (size_t)((2 * Ne + 3) & ~3) * 4;
+}
+constexpr size_t EE_FWD_LDS_CAP = 160 * 1024;
+__host__ __device__ inline int ee_fwd_mode(int Ne, int Nc) {
+  if (Ne <= EE_TAB_LDS_MAX) return 1;
+  return ee_fwd_head(Ne, Nc) + (size_t)Ne * H * 4 <= EE_FWD_LDS_CAP ? 2 : 0;
+}
 __host__ __device__ inline size_t ee_fwd_lds(int Ne, int Nc) {
-  const size_t head = (size_t)((2 * Nc + 1) & ~1) * 8 + (size_t)((2 * Ne + 3) & ~3) * 4;
-  return head + (Ne <= EE_TAB_LDS_MAX ? (size_t)2 * Ne * H * 4 : 0);
+  const int m = ee_fwd_mode(Ne, Nc);
+  return ee_fwd_head(Ne, Nc) + (m == 1 ? (size_t)2 * Ne * H * 4 : m == 2 ? (size_t)Ne * H * 4 : 0);
 }
 
 #ifdef HDG_EE_PROBE   // timing probe builds only (tools/probe/eefwd_probe.hip)
@@ -1035,7 +1045,7 @@ __device__ unsigned long long* g_ee_stamps;
 #define EE_FLUSH() do {} while (0)
 #endif
 
-template <bool LDS>
+template <int TM>   // table mode (ee_fwd_mode)
 __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                  const int32_t* __restrict__ hidg,
                                                  const int32_t* __restrict__ nleng,
@@ -1063,6 +1073,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   // instead of one per loop trip, and none waiting on nleng
   constexpr int GQ = (EE_TAB_LDS_MAX * H / 4 + NTP - 1) / NTP;
   const int nq = Ne * H / 4;                       // H % 4 == 0: whole float4 per row
+  constexpr bool LDS = TM == 1;
   float4 gv[LDS ? GQ : 1];
   if constexpr (LDS) {
 #pragma unroll
@@ -1085,6 +1096,10 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     return;
   }
   for (int e = t; e < 2 * n; e += NTP) tsum[e] = 0.f;
+  if constexpr (TM == 2) {        // gam alone: the commit's rows, float4 copies
+    for (int q = t; q < nq; q += NTP)
+      reinterpret_cast<float4*>(gl)[q] = reinterpret_cast<const float4*>(gb)[q];
+  }
   if constexpr (LDS) {
 #pragma unroll
     for (int u = 0; u < GQ; ++u) {
@@ -1168,10 +1183,10 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
           dz = fma2(ka, cq[2 * v], dz);
           dzb = fma2(kb, cq[2 * v + 1], dzb);
         }
-      } else {
+      } else {   // kappa = rho_i + fma(a, d, gam_j): the same bits as gam + d for a = 1
         const float af = a1 ? 1.f : 0.f;
         const f2 a2 = {af, af};
-        const float4* g4 = reinterpret_cast<const float4*>(gb + (size_t)ej * H);
+        const float4* g4 = reinterpret_cast<const float4*>((TM == 2 ? gl : gb) + (size_t)ej * H);
 #pragma unroll
         for (int v = 0; v < H / 4; ++v) {
           const float4 g = g4[v];
@@ -4032,9 +4047,11 @@ int set_wide_attrs() {
                              96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,    // + 15 KiB static hand-over
                              hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<true>,
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<1>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<false>,
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<2>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<0>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_clsb,      // 41 KiB static + 32 KiB at Ne 4096
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
@@ -4055,17 +4072,22 @@ int set_wide_attrs() {
   return 0;
 }
 
-// kw_ee_fwd over the batch: LDS tables up to EE_TAB_LDS_MAX nodes, HBM reads beyond
+// kw_ee_fwd over the batch: both LDS tables up to EE_TAB_LDS_MAX nodes, the gam table alone
+// while it fits the LDS, HBM reads beyond
 int launch_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, const float* D,
                   const float* rho, const float* gmm, unsigned long long* ncpart, hipStream_t st) {
   const int B = s->batch, Ne = s->ne, Nc = s->nc;
   const Off o = param_offsets(s->variant);
   const dim3 grid(ee_fwd_tiles(Ne), B);
-  if (Ne <= EE_TAB_LDS_MAX)
-    hipLaunchKernelGGL(kw_ee_fwd<true>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+  const int tm = ee_fwd_mode(Ne, Nc);
+  if (tm == 1)
+    hipLaunchKernelGGL(kw_ee_fwd<1>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+  else if (tm == 2)
+    hipLaunchKernelGGL(kw_ee_fwd<2>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
                        bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
   else
-    hipLaunchKernelGGL(kw_ee_fwd<false>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+    hipLaunchKernelGGL(kw_ee_fwd<0>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
                        bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
   WTRY(kmark("kw_ee_fwd", st));
   return 0;

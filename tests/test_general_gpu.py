@@ -164,6 +164,13 @@ def test_stress_shape_matches_oracle(v):
     _run_and_check(synth_commits(1, 1024, 512, 9), v, 9)
 
 
+@pytest.mark.parametrize("ne", [401, 600])
+def test_ee_gamma_table_mode_matches_oracle(ne):
+    """kw_ee_fwd's gam-only LDS table (Ne past the two-table limit 400, while the table
+    fits the LDS; Ne = 1024 is covered by the stress shape), ragged node counts."""
+    _run_and_check(synth_commits(2, ne, 50, 21), 4, 21)
+
+
 def test_general_equals_fused_model2():
     B, ne, nc = 4, 200, 74
     cb = synth_commits(B, ne, nc, 12)

@@ -47,13 +47,13 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dD, D.data(), 4096, hipMemcpyHostToDevice));
   CK(hipMemset(dst, 0, nst * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_ee_stamps), &dst, sizeof(dst)));
-  CK(hipFuncSetAttribute((const void*)kw_ee_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)kw_ee_fwd<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   float best = 1e9f;
   for (int r = 0; r < 30; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(kw_ee_fwd<true>, dim3(tiles, B), dim3(NTP), ee_fwd_lds(Ne, Nc), 0, dab, dhid,
+    hipLaunchKernelGGL(kw_ee_fwd<1>, dim3(tiles, B), dim3(NTP), ee_fwd_lds(Ne, Nc), 0, dab, dhid,
                        dnl, (const float*)nullptr, Off{}, dD, Ne, Nc, drho, dgam, dnc);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
