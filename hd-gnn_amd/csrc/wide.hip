@@ -663,15 +663,25 @@ __host__ __device__ inline size_t sort_lds_bytes(int Ne) {
 __device__ __forceinline__ int top_pow2(int n) { return 1 << (31 - __builtin_clz((unsigned)n)); }
 
 // boundary q of the set {distinct values v : pred(v)} when pred is monotone: with
-// inc = pred increasing in v the set is [q, nd) (suffix), otherwise [0, q) (prefix)
-template <class P>
-__device__ __forceinline__ int set_bound(const SortTabs& T, bool inc, P pred) {
-  int q = 0;
+// inc = pred increasing in v the set is [q, nd) (suffix), otherwise [0, q) (prefix);
+// NB independent searches in lockstep (search n: pred(n, v), increasing when inc[n]): one
+// LDS round trip per level for all of them instead of one per level and search
+template <int NB, class P>
+__device__ __forceinline__ void set_bounds(const SortTabs& T, const bool (&inc)[NB],
+                                           int (&q)[NB], P pred) {
+#pragma unroll
+  for (int n = 0; n < NB; ++n) q[n] = 0;
   for (int s = top_pow2(T.nd); s > 0; s >>= 1) {
-    const int m = q + s - 1;
-    if (m < T.nd && pred(T.xu[m]) != inc) q += s;
+    float xv[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int m = q[n] + s - 1;
+      xv[n] = T.xu[m < T.nd ? m : T.nd - 1];
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      if (q[n] + s - 1 < T.nd && pred(n, xv[n]) != inc[n]) q[n] += s;
   }
-  return q;
 }
 
 // walk node i's neighbour id list (list_layout; side 0: a_ij = 1, 1: a_ji = 1) four ids per
@@ -768,9 +778,35 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
       wb[kk] = w1;
       u[kk] = fmaf(xi, w0, c0[kk]);
       v[kk] = xi * w1;
-      const float uu = u[kk], vv = v[kk], cc = c0[kk];
-      const int br = set_bound(T, w1 >= 0.f, [&](float xq) { return (uu + xq * w1) > 0.f; });
-      const int bc = set_bound(T, w0 >= 0.f, [&](float xq) { return (fmaf(xq, w0, cc) + vv) > 0.f; });
+    } else {
+      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
+      dd[kk] = W[o.EE_W12 + H + k] - w20;
+      wa[kk] = w;
+      u[kk] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
+    }
+    s1[kk] = 0.f;
+    s2[kk] = 0.f;
+  }
+  // the set boundaries of every unit (and both pair orders in MODE 0) searched in lockstep
+  constexpr int NS = MODE == 0 ? 2 * KPW : KPW;
+  bool sinc[NS];
+  int sb[NS];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) sinc[n] = (MODE == 0 && n < KPW ? wb[n] : wa[n % KPW]) >= 0.f;
+  set_bounds<NS>(T, sinc, sb, [&](int n, float xq) {
+    if constexpr (MODE == 0) {
+      if (n < KPW) return (u[n] + xq * wb[n]) > 0.f;
+      const int kk = n - KPW;
+      return (fmaf(xq, wa[kk], c0[kk]) + v[kk]) > 0.f;
+    } else {
+      return fmaf(xq, wa[n], u[n]) > 0.f;
+    }
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    if constexpr (MODE == 0) {
+      const float w0 = wa[kk], w1 = wb[kk], uu = u[kk], vv = v[kk], cc = c0[kk];
+      const int br = sb[kk], bc = sb[KPW + kk];
       const int rlo = w1 >= 0.f ? br : 0, rhi = w1 >= 0.f ? T.nd : br;
       const int clo = w0 >= 0.f ? bc : 0, chi = w0 >= 0.f ? T.nd : bc;
       double acc = (double)(T.cum[rhi] - T.cum[rlo]) * (double)uu +
@@ -780,20 +816,14 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
       acc -= 2.0 * (double)relu(uu + vv);
       dense[kk] = acc;
     } else {
-      const float w = W[o.EE_W11 + k], w20 = W[o.EE_W12 + k];
-      dd[kk] = W[o.EE_W12 + H + k] - w20;
-      wa[kk] = w;
-      u[kk] = fmaf(xi, w, w20 + W[o.EE_B1 + k]);
-      const float uu = u[kk];
-      const int br = set_bound(T, w >= 0.f, [&](float xq) { return fmaf(xq, w, uu) > 0.f; });
+      const float w = wa[kk], uu = u[kk];
+      const int br = sb[kk];
       const int lo = w >= 0.f ? br : 0, hi = w >= 0.f ? T.nd : br;
       const double acc = (double)(T.cum[hi] - T.cum[lo]) * (double)uu +
                          (double)w * (T.pxd[hi] - T.pxd[lo]) - (double)relu(fmaf(xi, w, uu));
       dense[kk] = acc;
       dense2[kk] = acc;
     }
-    s1[kk] = 0.f;
-    s2[kk] = 0.f;
   }
   // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i)), one clamped
   // packed fma per two hidden units and neighbour (clamp_coef); KPW = 5: two packed
@@ -3050,12 +3080,21 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     S1[kk] = 0.f;
     S2[kk] = 0.f;
     S3[kk] = 0.f;
-    if (hw) continue;                             // the dense part: hw 0
-    const float uu = u[kk];
+  }
+  if (!hw) {                                      // the dense part: hw 0
+  bool sinc[KPW];
+  int sb[KPW];
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) sinc[kk] = wb[kk] >= 0.f;
+  set_bounds<KPW>(T, sinc, sb, [&](int n, float xq) {   // the units' searches in lockstep
+    return MODE == 0 ? (u[n] + xq * wb[n]) > 0.f : fmaf(xq, wb[n], u[n]) > 0.f;
+  });
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) {
+    const int k = g * KPW + kk;
+    const float uu = u[kk], slope = wb[kk];
     const bool inc = slope >= 0.f;
-    const int br = MODE == 0
-        ? set_bound(T, inc, [&](float xq) { return (uu + xq * slope) > 0.f; })
-        : set_bound(T, inc, [&](float xq) { return fmaf(xq, slope, uu) > 0.f; });
+    const int br = sb[kk];
     const int lo = inc ? br : 0, hi = inc ? T.nd : br;
     const double cnt = (double)(T.cum[hi] - T.cum[lo]);
     const double sx = T.pxd[hi] - T.pxd[lo];
@@ -3071,6 +3110,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     }
     S2[kk] = (float)gs;
     S1[kk] = (float)gx;
+  }
   }
   float cs[KPW];                                  // sum of the corrections' dm
 #pragma unroll
