@@ -3532,9 +3532,13 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     float* __restrict__ psi, float* __restrict__ part, Segs sg) {
   __shared__ float A[TN * HP], Bq[TN * HP], R1t[TN * HP], C1t[TN * HP], Rt[TN * HP],
       Ct[TN * HP], dR[TN * HP], dC[TN * HP];
-  __shared__ float Wl[800];
+  // the weights' rows at pitch WPN = 50 words (= 18 mod 32): the 16 rows x 2 k-offsets a
+  // ds_read_b32 group of the MFMA B operand reads fall on 32 distinct banks (pitch 20 put
+  // rows m and m + 8 on one bank)
+  constexpr int WPN = 50;
+  __shared__ float Wl[2 * H * WPN];
   __shared__ float kz[1];                         // 0.f: stride-0 operand of padding tiles
-  const float *U1e = Wl, *Q2 = Wl + 400;          // classifier rows 2..21 | EE second layer
+  const float *U1e = Wl, *Q2 = Wl + H * WPN;      // classifier rows 2..21 | EE second layer
   if (threadIdx.x == 0) kz[0] = 0.f;
   // XCD-grouped rows: the partial-gradient stores below are 4-byte values at a stride of
   // the te*B rows, so a 64-byte line holds 16 neighbouring rows' values; dealing the rows
@@ -3547,8 +3551,11 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   const int t0 = tile * TN, t = threadIdx.x;
   const size_t base = ((size_t)b * Ne + t0) * H;
   WSTAMP(6, 0);
-  stage_w(Wl, W + o.EC_W1 + 2 * H, 400);
-  stage_w(Wl + 400, W + o.EE_W2, 400);
+  for (int e = threadIdx.x; e < H * H; e += NT) {
+    const int r = e / H, c = e - r * H;
+    Wl[r * WPN + c] = W[o.EC_W1 + 2 * H + e];
+    Wl[H * WPN + r * WPN + c] = W[o.EE_W2 + e];
+  }
   // staging: every element's loads issued before the first use (NE_IT elements per thread;
   // the np row partials of drho (kw_ee_clsb's column tiles) eight at a time, in tile order)
   constexpr int NE_IT = TN * H / NT;
@@ -3599,7 +3606,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     const int mc = m0 + (lane & 15);
     const bool cv = mc < H;
     const f4v c = mfma_tile16_p((which ? Bq : A) + (n0 + (lane & 15)) * HP, 1,
-                                cv ? U1e + mc * H : kz, cv ? 1 : 0, H, lane);
+                                cv ? U1e + mc * WPN : kz, cv ? 1 : 0, H, lane);
     if (cv) {
       float* d = which ? dC : dR;
 #pragma unroll
@@ -3612,7 +3619,7 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     const int lc = l0 + (lane & 15);
     const bool cv = lc < H;
     const f4v c = mfma_tile16_p((which ? dC : dR) + (n0 + (lane & 15)) * HP, 1,
-                                cv ? Q2 + lc * H : kz, cv ? 1 : 0, H, lane);
+                                cv ? Q2 + lc * WPN : kz, cv ? 1 : 0, H, lane);
     if (cv) {
       float* d = which ? psi : phi;
 #pragma unroll
