@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N` without a launcher starts the N ranks itself (a torch.distributed.run child);
+under a launcher WORLD_SIZE must equal --gpus.  Rank r runs on device r mod device_count;
+more ranks than devices (a rehearsal) share them over a gloo control plane.
+
 A step = the fused step kernel + the gradient reduction + TF Adam on 100 resident
 synthetic glide-shaped commits per GPU (weak scaling); under torch.distributed.run the
 reduction kernel also all-reduces the flat gradient over xGMI (hdg_train_step_dp; RCCL
@@ -70,6 +74,13 @@ def build_roofline(dom, kern_ms, variant, path, ne, nc, batch, default_data, hun
                      "per-node algebra (DESIGN.md 3) executes ~13x fewer operations, so this "
                      "is work-equivalent throughput, not a hardware roofline (no frac)"},
          "profile": None}
+    # SURVEY 8(d)'s algorithmic bytes over the live launch time: the contract's byte roofline
+    alg = r["algorithmic_bytes_per_launch"]
+    r["alg_hbm_gbs"] = round(alg / t / 1e9, 2)
+    r["alg_hbm_frac"] = round(alg / t / 1e9 / HBM_PEAK_GBS, 4)
+    r["frac_basis"] = ("executed FP32 FLOPs per launch (calibrated rocprofv3 PMC counters of "
+                       "the committed profile) / fp32 peak; alg_hbm_frac = SURVEY 8(d) "
+                       "algorithmic bytes / live launch time / 8 TB/s")
     if pj is None:
         r["profile"] = "no committed profile of this workload (tools/profile_config.sh)"
         return r
@@ -222,9 +233,40 @@ def e2e_train(B, ne, nc, v, epochs, dev):
                     "and a TF-bundle checkpoint written by libhdgnn on the saver thread"}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: run the N ranks as one
+    torch.distributed.run child (one process per rank, rendezvous on 127.0.0.1) and return
+    its exit code.  This process has not touched the GPU (nothing is exec'd: the child is a
+    fresh process tree; rank 0's JSON line reaches stdout through the inherited pipe)."""
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd, env=env)
+
+
+def rank_layout(world, local):
+    """(device index, ranks share a device) for this rank: local rank modulo the node's
+    device count.  torch.cuda.device_count() does not initialise the GPU on this image."""
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise RuntimeError("bench.py needs a HIP device (torch.cuda.device_count() == 0)")
+    return local % ndev, world > ndev
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU; default: WORLD_SIZE under a launcher, "
+                         "else 1).  Without a launcher, N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=100, help="commits per GPU")
@@ -254,17 +296,30 @@ def main():
                          "EPOCHS epochs of one --batch-commit step each (0: skip)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        sys.exit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks; refusing "
+                 "to report n_gpus=%d for a %d-rank run" % (args.gpus, world, args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # under torch.distributed.run (any world size, so the RCCL step can be exercised on
     # one GPU) every step all-reduces the flat gradient inside the captured graph
     launched = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    didx, shared = rank_layout(world, local) if launched else (0, False)
     if launched:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(didx)
+        if shared:
+            # more ranks than devices (a rehearsal on a smaller box): RCCL refuses two ranks
+            # on one GPU, so the control plane runs on gloo and the gradient exchange must
+            # be the xGMI mailboxes (IPC-mapped between the processes)
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", didx))
+    dev = torch.device("cuda", didx)
 
     from hdgnn.engine import Engine
     from hdgnn import layout
@@ -279,7 +334,11 @@ def main():
               "tiled": _lib.FLAG_HUNK_TILED}[args.hunk]
     eng = Engine(ne, nc, B, variant=v, device=dev, batch_global=B * world, path=args.path,
                  process_group=torch.distributed.group.WORLD if launched else None,
-                 flags=hflags)
+                 flags=hflags, allreduce="xgmi" if shared else None)
+    if shared:
+        # the fused split mode needs both blocks of a commit resident at once; ranks
+        # sharing a device compete for its CUs, so one block per commit
+        eng.set_split(False)
     eng.set_params(layout.init_flat(0, v))
     eng.upload(cb)                               # warm the upload / prepare path once
     torch.cuda.synchronize(dev)
@@ -315,7 +374,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.check_status()             # a failed launch (exchange timeout) voids the run: raise
     if launched:
-        t = torch.tensor([elapsed], device=dev)
+        t = torch.tensor([elapsed], device="cpu" if shared else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
     value = world * B * args.steps / elapsed
@@ -395,6 +454,10 @@ def main():
                                  "hipGraph replay, %d training steps per graph" % gsteps,
                        "ne": ne, "nc": nc, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world,
+                       **({"ranks_share_device": "%d ranks on %d device(s): gloo control plane, "
+                                                 "xGMI-mailbox gradient exchange, one block per "
+                                                 "commit" % (world, torch.cuda.device_count())}
+                          if shared else {}),
                        **({"hunk_sums": hunk_form} if eng.path == _lib.PATH_GENERAL else {}),
                        **({} if default_data else {"data_knobs": knobs})},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -22,6 +22,7 @@
 //   are prefix/suffix sums over the x-sorted order (O(Ne log nd) per hidden unit)
 //   plus sparse corrections for a = 1.  Hunk pairs run as dense register tiles.
 #include <hip/hip_runtime.h>
+#include <string>
 #include <vector>
 
 #include <math.h>
@@ -4011,14 +4012,19 @@ static int write_file(const char* path, const void* p, size_t n) {
 }
 
 int hdg_bundle_write(const char* data_path, const char* index_path, const float* state,
-                     const int32_t* gather, int64_t n_floats, uint8_t* index_img,
-                     int64_t index_len, const int64_t* entries, int32_t n_entries,
-                     const int64_t* blocks, int32_t n_blocks) {
-  if (!data_path || !index_path || !state || !gather || n_floats < 0 || !index_img ||
-      index_len < 48 || (n_entries && !entries) || (n_blocks && !blocks))
+                     int64_t n_state, const int32_t* gather, int64_t n_floats,
+                     uint8_t* index_img, int64_t index_len, const int64_t* entries,
+                     int32_t n_entries, const int64_t* blocks, int32_t n_blocks) {
+  if (!data_path || !index_path || !state || n_state < 0 || !gather || n_floats < 0 ||
+      !index_img || index_len < 48 || (n_entries && !entries) || (n_blocks && !blocks))
     return fail(HDG_EINVAL, "hdg_bundle_write: bad arguments");
   std::vector<float> blob((size_t)n_floats);
-  for (int64_t i = 0; i < n_floats; ++i) blob[i] = state[gather[i]];
+  for (int64_t i = 0; i < n_floats; ++i) {
+    if (gather[i] < 0 || gather[i] >= n_state)
+      return fail(HDG_EINVAL, "hdg_bundle_write: gather[%lld] = %d outside the %lld-float state",
+                  (long long)i, (int)gather[i], (long long)n_state);
+    blob[i] = state[gather[i]];
+  }
   const uint8_t* bytes = reinterpret_cast<const uint8_t*>(blob.data());
   const int64_t nbytes = n_floats * 4;
   for (int32_t e = 0; e < n_entries; ++e) {        // entry proto field 6: masked CRC of bytes
@@ -4035,8 +4041,20 @@ int hdg_bundle_write(const char* data_path, const char* index_path, const float*
     const uint32_t c = mask_crc(hdg_crc32c(index_img + off, (size_t)len + 1, 0));
     memcpy(index_img + off + len + 1, &c, 4);
   }
-  if (int rc = write_file(data_path, bytes, (size_t)nbytes)) return rc;
-  return write_file(index_path, index_img, (size_t)index_len);
+  // both files under temporary names first, then renamed data before index: a crash or a
+  // full disk mid-save never leaves a new .index beside a stale or partial .data
+  const std::string dtmp = std::string(data_path) + ".tmp", itmp = std::string(index_path) + ".tmp";
+  int rc = write_file(dtmp.c_str(), bytes, (size_t)nbytes);
+  if (!rc) rc = write_file(itmp.c_str(), index_img, (size_t)index_len);
+  if (!rc && rename(dtmp.c_str(), data_path) != 0)
+    rc = fail(HDG_EINVAL, "cannot rename %s to %s", dtmp.c_str(), data_path);
+  if (!rc && rename(itmp.c_str(), index_path) != 0)
+    rc = fail(HDG_EINVAL, "cannot rename %s to %s", itmp.c_str(), index_path);
+  if (rc) {
+    remove(dtmp.c_str());
+    remove(itmp.c_str());
+  }
+  return rc;
 }
 
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle) {

@@ -52,7 +52,7 @@ class Dp(ctypes.Structure):
 
 DP_MAX_WORLD, DP_HANDLE_BYTES, DP_MAX_LEN = 16, 64, 3152
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 # gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
 TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
 STATUS_XCH_TIMEOUT, STATUS_DP_TIMEOUT = 1, 2
@@ -121,8 +121,8 @@ def load(path=None):
     lib.hdg_dp_allreduce.argtypes = [P(Dp), vp, vp, i32, vp, vp]
     lib.hdg_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
     lib.hdg_crc32c.restype = ctypes.c_uint32
-    lib.hdg_bundle_write.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, vp, ctypes.c_int64, vp,
-                                     ctypes.c_int64, vp, i32, vp, i32]
+    lib.hdg_bundle_write.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, ctypes.c_int64, vp,
+                                     ctypes.c_int64, vp, ctypes.c_int64, vp, i32, vp, i32]
     for name in EXPORTS:
         getattr(lib, name)
     _lib = lib

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .layout import n_params
+from .layout import n_params, state_offsets
 
 
 class Engine:
@@ -51,10 +51,14 @@ class Engine:
         self.workspace = torch.zeros(wsb // 4, dtype=f32, device=dev)   # block-pair inboxes start at 0
         # the training state as one flat buffer [params | adam_m | adam_v | beta_pow]: one
         # copy snapshots, restores or reads it (the checkpoint's host copy)
-        P = self.np
-        self.state = torch.zeros(3 * P + 2, dtype=f32, device=dev)
-        self.params, self.m, self.v, self.beta_pow = (self.state[:P], self.state[P:2 * P],
-                                                      self.state[2 * P:3 * P], self.state[3 * P:])
+        # (each slice 64-byte aligned, layout.state_offsets; the pads stay zero)
+        P, so = self.np, state_offsets(variant)
+        self.state = torch.zeros(so["len"], dtype=f32, device=dev)
+        self.params, self.m, self.v, self.beta_pow = (
+            self.state[:P], self.state[so["m"]:so["m"] + P], self.state[so["v"]:so["v"] + P],
+            self.state[so["beta_pow"]:so["beta_pow"] + 2])
+        for t in (self.params, self.m, self.v, self.beta_pow):
+            assert t.data_ptr() % 64 == 0, "training-state slice not 64-byte aligned"
         self.beta_pow.copy_(torch.tensor([0.9, 0.999]))
         self.grad = torch.zeros(self.glen, dtype=f32, device=dev)
         # ce, loss_map, loss_para, train_loss, count parts (3), fault count (hdg_outputs.stats)

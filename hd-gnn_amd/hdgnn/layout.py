@@ -53,6 +53,18 @@ def offsets(variant=2):
     return out
 
 
+STATE_ALIGN = 16     # floats: each slice of the flat training state starts on 64 bytes
+
+
+def state_offsets(variant=2):
+    """Offsets of [params | adam_m | adam_v | beta_pow] in the engine's flat training state
+    (Engine.state) and its length: each slice starts on a 64-byte boundary, so a vector
+    access (float4) to any of them through hdg_state is aligned."""
+    P = n_params(variant)
+    S = -(-P // STATE_ALIGN) * STATE_ALIGN
+    return {"params": 0, "m": S, "v": 2 * S, "beta_pow": 3 * S, "len": 3 * S + 2}
+
+
 def split(flat, variant=2):
     return {name: np.asarray(flat[o:o + int(np.prod(s))]).reshape(s)
             for name, (o, s) in offsets(variant).items()}

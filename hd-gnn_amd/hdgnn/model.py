@@ -91,13 +91,9 @@ class Saver(object):
         self._tmpl = None
 
     def _host_state(self):
-        """[params | adam_m | adam_v | beta_pow] in one device->host copy."""
-        import torch
-        eng = self._model.engine
-        st = getattr(eng, "state", None)
-        if st is None:
-            st = torch.cat([eng.params.detach(), eng.m, eng.v, eng.beta_pow])
-        return st.detach().cpu().numpy().copy()
+        """[params | adam_m | adam_v | beta_pow] (layout.state_offsets) in one device->host
+        copy."""
+        return self._model.engine.state.detach().cpu().numpy().copy()
 
     def save(self, sess, save_path, global_step=None, background=False, state=None):
         """background=True: the state is copied to the host now (the bundle holds exactly

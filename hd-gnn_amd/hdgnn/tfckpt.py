@@ -479,25 +479,28 @@ def write(prefix, tensors):
 class BundleTemplate(object):
     """The byte layout of one model variant's training checkpoint (model variables, TF1 Adam
     slots, beta powers: every tensor float32, fixed shapes), built once.  write() fills it
-    from the flat engine state [params | adam_m | adam_v | beta_pow] in libhdgnn's
+    from the flat engine state [params | adam_m | adam_v | beta_pow] (Engine.state, slices at
+    layout.state_offsets) in libhdgnn's
     hdg_bundle_write: the tensor bytes gathered in name order, each entry's CRC and each
     index block's trailer CRC patched into the index image, both files written -- native
     code that runs with the GIL released (ctypes), so the saver thread does not stall the
     training loop.  Same bytes as write(prefix, state_tensors(...)) (tests/test_tfckpt.py)."""
 
     def __init__(self, variant, slots=True):
+        from . import layout
         sl = _var_slices(variant)
         P = sum(n for _, _, n, _ in sl)
+        so = layout.state_offsets(variant)
         spans = {}
         for base, o, n, shape in sl:
             spans[base] = (o, n, shape)
             if slots:
-                spans[base + "/Adam"] = (P + o, n, shape)
-                spans[base + "/Adam_1"] = (2 * P + o, n, shape)
+                spans[base + "/Adam"] = (so["m"] + o, n, shape)
+                spans[base + "/Adam_1"] = (so["v"] + o, n, shape)
         if slots:
-            spans["beta1_power"] = (3 * P, 1, ())
-            spans["beta2_power"] = (3 * P + 1, 1, ())
-        self.n_state = 3 * P + 2 if slots else P
+            spans["beta1_power"] = (so["beta_pow"], 1, ())
+            spans["beta2_power"] = (so["beta_pow"] + 1, 1, ())
+        self.n_state = so["len"] if slots else P
         names = sorted(spans, key=lambda n: n.encode("utf-8"))
         gather, entries, offs = [], [(b"", encode_header(1))], []
         nbytes = 0
@@ -529,7 +532,8 @@ class BundleTemplate(object):
         lib = _lib.load()
         _lib.check(lib.hdg_bundle_write(
             _shard_name(prefix, 0, 1).encode(), (prefix + ".index").encode(),
-            state.ctypes.data, self.gather.ctypes.data, self.gather.size, img.ctypes.data,
+            state.ctypes.data, state.size, self.gather.ctypes.data, self.gather.size,
+            img.ctypes.data,
             img.size, self.entries.ctypes.data, len(self.entries), self.blocks.ctypes.data,
             len(self.blocks)))
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 6
+#define HDG_ABI_VERSION 7
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -270,16 +270,18 @@ uint32_t hdg_crc32c(const void* data, size_t n, uint32_t crc);
 /* Host utility: write one TF V2 checkpoint bundle of float32 tensors from a prebuilt
  * template (hdgnn.tfckpt.BundleTemplate; replaces the Python encoder of saver.save,
  * model_2.py:427-437, so the caller's thread runs it without holding the GIL):
- *   data file  = state[gather[i]] for i < n_floats (the tensors' bytes, sorted by name)
+ *   data file  = state[gather[i]] for i < n_floats (the tensors' bytes, sorted by name;
+ *                every gather index is checked against the n_state floats of state)
  *   index file = index_img with each entry's masked CRC-32C of its bytes written at
  *                entries[3e + 2] (the tensor spans [entries[3e], +entries[3e + 1]) bytes of
  *                the data file), then each block's trailer CRC (blocks[2b] offset,
  *                blocks[2b + 1] length; type byte at offset + length) -- index_img is
- *                modified in place.  0, or HDG_EINVAL (message in hdg_last_error).     */
+ *                modified in place.  Both files are written under "<path>.tmp" and renamed
+ *                into place, data before index.  0, or HDG_EINVAL (hdg_last_error).    */
 int hdg_bundle_write(const char* data_path, const char* index_path, const float* state,
-                     const int32_t* gather, int64_t n_floats, uint8_t* index_img,
-                     int64_t index_len, const int64_t* entries, int32_t n_entries,
-                     const int64_t* blocks, int32_t n_blocks);
+                     int64_t n_state, const int32_t* gather, int64_t n_floats,
+                     uint8_t* index_img, int64_t index_len, const int64_t* entries,
+                     int32_t n_entries, const int64_t* blocks, int32_t n_blocks);
 /* allocate + zero this rank's mailbox on the current device; handle: 64 bytes out */
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle);
 /* map a peer's mailbox (its handle) into this process; close / free undo the calls */

@@ -194,9 +194,13 @@ def test_background_saver_keeps_order_and_state(tmp_path):
     from hdgnn.model import Saver
     v = 2
     flat = layout.init_flat(3, v).astype(np.float32)
-    eng = types.SimpleNamespace(params=torch.from_numpy(flat.copy()),
-                                m=torch.zeros(flat.size), v=torch.zeros(flat.size),
-                                beta_pow=torch.tensor([0.9, 0.999]))
+    P, so = flat.size, layout.state_offsets(v)      # Engine.state's layout, on the host
+    state = torch.zeros(so["len"])
+    eng = types.SimpleNamespace(state=state, params=state[:P], m=state[so["m"]:so["m"] + P],
+                                v=state[so["v"]:so["v"] + P],
+                                beta_pow=state[so["beta_pow"]:so["beta_pow"] + 2])
+    eng.params.copy_(torch.from_numpy(flat))
+    eng.beta_pow.copy_(torch.tensor([0.9, 0.999]))
     sv = Saver(types.SimpleNamespace(engine=eng, variant=v))
     want = {}
     for step in range(1, 8):
@@ -222,17 +226,42 @@ def test_native_bundle_template_bytes_equal_python_writer(tmp_path):
     bundle reads back to the state it was given."""
     for v in (1, 2, 3, 4):
         P = layout.n_params(v)
-        st = np.random.default_rng(v).standard_normal(3 * P + 2).astype(np.float32)
+        so = layout.state_offsets(v)              # Engine.state: 64-byte aligned slices
+        st = np.random.default_rng(v).standard_normal(so["len"]).astype(np.float32)
+        sm, sv, sb = st[so["m"]:so["m"] + P], st[so["v"]:so["v"] + P], st[so["beta_pow"]:]
         t = tfckpt.BundleTemplate(v)
         for rep in range(2):                 # the template is reused across saves
-            st = st + np.float32(rep)
+            st += np.float32(rep)
             t.write(str(tmp_path / ("n%d" % v)), st)
-            tfckpt.write(str(tmp_path / ("p%d" % v)),
-                         tfckpt.state_tensors(st[:P], v, st[P:2 * P], st[2 * P:3 * P], st[3 * P:]))
+            tfckpt.write(str(tmp_path / ("p%d" % v)), tfckpt.state_tensors(st[:P], v, sm, sv, sb))
             for ext in (".index", ".data-00000-of-00001"):
                 assert (tmp_path / ("n%d%s" % (v, ext))).read_bytes() == \
                     (tmp_path / ("p%d%s" % (v, ext))).read_bytes()
             fl, m, vv, bp = tfckpt.engine_state(tfckpt.read(str(tmp_path / ("n%d" % v))), v)
-            np.testing.assert_array_equal(np.concatenate([fl, m, vv, bp]), st)
+            np.testing.assert_array_equal(np.concatenate([fl, m, vv, bp]),
+                                          np.concatenate([st[:P], sm, sv, sb]))
+        assert not list(tmp_path.glob("*.tmp"))   # written under .tmp names, renamed in place
     with pytest.raises(tfckpt.CheckpointError):
         tfckpt.BundleTemplate(2).write(str(tmp_path / "bad"), np.zeros(5, np.float32))
+
+
+def test_native_bundle_write_checks_gather_bounds(tmp_path):
+    """hdg_bundle_write bounds-checks every gather index against n_state itself (not only
+    the Python wrapper's size check) and leaves no file behind when it refuses."""
+    import ctypes
+    from hdgnn import _lib
+    lib = _lib.load()
+    t = tfckpt.BundleTemplate(2)
+    st = np.zeros(t.n_state, np.float32)
+    gather = t.gather.copy()
+    gather[7] = t.n_state                     # one past the end
+    img = t.image.copy()
+    prefix = str(tmp_path / "oob")
+    rc = lib.hdg_bundle_write((prefix + ".data-00000-of-00001").encode(),
+                              (prefix + ".index").encode(), st.ctypes.data, st.size,
+                              gather.ctypes.data, gather.size, img.ctypes.data, img.size,
+                              t.entries.ctypes.data, len(t.entries), t.blocks.ctypes.data,
+                              len(t.blocks))
+    assert rc == 1000                          # HDG_EINVAL
+    assert b"gather" in lib.hdg_last_error()
+    assert not list(tmp_path.iterdir())
