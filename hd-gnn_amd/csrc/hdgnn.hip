@@ -125,6 +125,12 @@ __device__ __forceinline__ void trip_prio(int s) {
 #ifndef HDG_XROW
 #define HDG_XROW 1
 #endif
+#ifndef HDG_QMAP   // pair tiles: quad unit map (16-byte unit quads, ds_read_b128; below)
+#define HDG_QMAP 1
+#endif
+#ifndef HDG_QTAIL  // quad map: tail units of the column operands by 8-byte reads (1 B, 2 wc)
+#define HDG_QTAIL 1
+#endif
 // Row sums of 5 values over a 16-lane DPP row as a transposed butterfly: 12 DPP adds
 // instead of 20, no selects -- at the two bank-crossing levels (row_mirror: lanes 0-7 vs
 // 8-15; row_half_mirror: banks 0, 2 vs 1, 3) one register takes the a-values' sums in
@@ -302,6 +308,37 @@ __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& 
 template <int SMAX, int KK>
 constexpr int tile_cred_words() { return 4 * 16 * SMAX * KK + 8 * KK; }
 
+// quad unit map of the pair tiles: 4 groups of KK = 5 of the 20 units, group g's pairs are
+// the 16-byte-aligned units 4g..4g+3 of a row (row pitch LD a multiple of 4 words)
+template <int KK, int LD>
+constexpr bool pair_qmap() { return HDG_QMAP && KK == 5 && LD % 4 == 0; }
+
+// the KP packed pairs of units p0, p0 + 1, ... at q (LDS): one 16-byte read when QM
+template <bool QM, int KP>
+__device__ __forceinline__ void ld_pairs(const float* q, f2* out) {
+  if constexpr (QM && KP == 2) {
+    const float4 v = *reinterpret_cast<const float4*>(q);
+    out[0] = (f2){v.x, v.y};
+    out[1] = (f2){v.z, v.w};
+  } else {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) out[p] = *reinterpret_cast<const f2*>(q + 2 * p);
+  }
+}
+
+// a row's tail unit (row base r): QM reads the 8-byte pair {16 + (g & ~1), +1} -- a
+// ds_read_b64 (mod-64 banks: 16 columns at pitch 20 on distinct banks) instead of a
+// 4-byte read whose mod-32 banks repeat every 8 columns -- and takes its half
+template <bool QM>
+__device__ __forceinline__ float ld_tail(const float* r, const int ktl, const int grp) {
+  if constexpr (QM) {
+    const f2 v = *reinterpret_cast<const f2*>(r + 16 + (grp & ~1));
+    return (grp & 1) ? v.y : v.x;
+  } else {
+    return r[ktl];
+  }
+}
+
 // Column closing of a pair pass: element e = (node j, local unit k) of the group's
 // column sums is the fixed-order sum of the 4 waves' partials in cred.  Every partial
 // of the thread is loaded before the first add (one LDS round trip).  fix(j, unit, v)
@@ -355,11 +392,16 @@ __device__ __forceinline__ void pair_tile(
   const int grp = k0 / KK;
   const int tj = t & 15, ti = ((t >> 4) + 4 * grp) & 15, lane = t & 63, wv = t >> 6;
   const int wrow = __builtin_amdgcn_readfirstlane(4 * ((wv + grp) & 3));   // wave's first ti
-  // hidden units of the chunk [k0, k0 + KK): the packed pairs start at the even unit kpb
-  // (k0 or k0 + 1), so every pair is one 8-byte-aligned LDS read at an immediate offset
-  // from a per-thread base; the unit left over is the tail ktl
-  const int kpb = k0 + (k0 & 1);
-  const int ktl = (k0 & 1) ? k0 : k0 + KK - 1;
+  // hidden units of the group: the packed pairs start at the even unit kpb, so every pair
+  // is one 8-byte-aligned LDS read at an immediate offset from a per-thread base; the unit
+  // left over is the tail ktl.  Quad map (QM): group g takes units 4g..4g+3 (one 16-byte
+  // read per row: ds_read_b128, whose 16-lane groups see 16 distinct columns on 64 banks)
+  // and the tail 16 + g; otherwise units [k0, k0 + KK), pairs from k0 or k0 + 1 (the
+  // compiler merges the two 8-byte reads into a ds_read2_b64, whose mod-32 banks put
+  // columns j and j + 8 of a row pitch of 20 words on one bank: 2-way on every read)
+  constexpr bool QM = pair_qmap<KK, LD>();
+  const int kpb = QM ? 4 * grp : k0 + (k0 & 1);
+  const int ktl = QM ? 16 + grp : ((k0 & 1) ? k0 : k0 + KK - 1);
   auto kof = [&](const int k) { return k < 2 * KP ? kpb + k : ktl; };   // local -> unit
   const int nown = (N - radd + rmul - 1) / rmul;   // rows i = rmul r + radd < N
   const int S = (nown + 15) >> 4;
@@ -379,10 +421,8 @@ __device__ __forceinline__ void pair_tile(
   p2 yacc2[KP > 0 ? KP : 1], dk2[KP > 0 ? KP : 1];
   float yacct = 0.f, dkt = KT ? dl[ktl] : 0.f;
 #pragma unroll
-  for (int p = 0; p < KP; ++p) {
-    yacc2[p] = z2;
-    dk2[p] = *reinterpret_cast<const p2*>(dl + kpb + 2 * p);
-  }
+  for (int p = 0; p < KP; ++p) yacc2[p] = z2;
+  ld_pairs<QM, KP>(dl + kpb, dk2);
 
   // loop-invariant column operands (the trip loop's stores to Rout may alias A in general,
   // so the compiler does not hoist these LDS reads itself; B / wc are not written in the loop)
@@ -396,13 +436,10 @@ __device__ __forceinline__ void pair_tile(
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) {
       const int j = tj + 16 * c;
-#pragma unroll
-      for (int p = 0; p < KP; ++p) {
-        if constexpr (HB) bcol[c][p] = *reinterpret_cast<const p2*>(Bv + j * LD + kpb + 2 * p);
-        if constexpr (HW) wcol[c][p] = *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
-      }
-      if constexpr (HB) bcolt[c] = KT ? Bv[j * LD + ktl] : 0.f;
-      if constexpr (HW) wcolt[c] = KT ? wc[j * LD + ktl] : 0.f;
+      if constexpr (HB) ld_pairs<QM, KP>(Bv + j * LD + kpb, bcol[c]);
+      if constexpr (HW) ld_pairs<QM, KP>(wc + j * LD + kpb, wcol[c]);
+      if constexpr (HB) bcolt[c] = KT ? ld_tail<QM && (HDG_QTAIL & 1)>(Bv + j * LD, ktl, grp) : 0.f;
+      if constexpr (HW) wcolt[c] = KT ? ld_tail<QM && (HDG_QTAIL & 2)>(wc + j * LD, ktl, grp) : 0.f;
     }
   }
   for (int s = 0; s < S; ++s) {
@@ -424,11 +461,13 @@ __device__ __forceinline__ void pair_tile(
     // with its own LDS round trip
     const float addm = iv ? 0.f : PADNEG, mulm = iv ? 1.f : 0.f;
     const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
+    ld_pairs<QM, KP>(Ai + kpb, a2);
+    if constexpr (MODE == 1) ld_pairs<QM, KP>(wr + ib * LD + kpb, rw2);
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      a2[p] = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p) + addm2;
+      a2[p] += addm2;
       if constexpr (MODE == 1)
-        rw2[p] = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p) * mulm2;
+        rw2[p] *= mulm2;
       else
         rw2[p] = z2;
       racc2[p] = z2;
@@ -456,11 +495,14 @@ __device__ __forceinline__ void pair_tile(
       }
       const float gy = af * g;             // MODE 2: exact (af is 0 or 1)
       const float* Bj = Bv + j * LD;
+      p2 bbv[KP > 0 ? KP : 1], wcv[KP > 0 ? KP : 1];
+      if constexpr (!HB) ld_pairs<QM, KP>(Bj + kpb, bbv);
+      if constexpr (MODE == 1 && !HW) ld_pairs<QM, KP>(wc + j * LD + kpb, wcv);
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
         p2 bb;
         if constexpr (HB) bb = bcol[c][p];
-        else bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
+        else bb = bbv[p];
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
         if constexpr (MODE == 0) {
           // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
@@ -478,7 +520,7 @@ __device__ __forceinline__ void pair_tile(
         } else {
           p2 w;
           if constexpr (HW) w = rw2[p] + wcol[c][p];
-          else w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
+          else w = rw2[p] + wcv[p];
           const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;
@@ -486,12 +528,13 @@ __device__ __forceinline__ void pair_tile(
         }
       }
       if constexpr (KT) {
-        const float z = at + fmaf(af, dkt, HB ? bcolt[c] : Bj[ktl]);
+        const float z = at + fmaf(af, dkt, HB ? bcolt[c] : ld_tail<QM && (HDG_QTAIL & 1)>(Bj, ktl, grp));
         float e;
         if constexpr (MODE == 0) {
           e = reluf(z);
         } else {
-          const float w = (MODE == 1) ? (rwt + (HW ? wcolt[c] : wc[j * LD + ktl])) : g;
+          const float w =
+              (MODE == 1) ? (rwt + (HW ? wcolt[c] : ld_tail<QM && (HDG_QTAIL & 2)>(wc + j * LD, ktl, grp))) : g;
           e = (z > 0.f) ? w : 0.f;
           yacct = fmaf(af, e, yacct);
         }
@@ -592,8 +635,9 @@ __device__ __forceinline__ void pair_tile32(
   const int grp = k0 / KK;                     // SIMD-balanced rows, as in pair_tile
   const int tj = t & 31, ti = ((t >> 5) + 2 * grp) & 7, lane = t & 63, wv = t >> 6;
   const int wrow = __builtin_amdgcn_readfirstlane(2 * ((wv + grp) & 3));
-  const int kpb = k0 + (k0 & 1);
-  const int ktl = (k0 & 1) ? k0 : k0 + KK - 1;
+  constexpr bool QM = pair_qmap<KK, LD>();     // the quad unit map of pair_tile
+  const int kpb = QM ? 4 * grp : k0 + (k0 & 1);
+  const int ktl = QM ? 16 + grp : ((k0 & 1) ? k0 : k0 + KK - 1);
   auto kof = [&](const int k) { return k < 2 * KP ? kpb + k : ktl; };
   const int nown = (N - radd + rmul - 1) / rmul;
   const int S = (nown + 7) >> 3;
@@ -610,10 +654,8 @@ __device__ __forceinline__ void pair_tile32(
   p2 yacc2[KP > 0 ? KP : 1], dk2[KP > 0 ? KP : 1];
   float yacct = 0.f, dkt = KT ? dl[ktl] : 0.f;
 #pragma unroll
-  for (int p = 0; p < KP; ++p) {
-    yacc2[p] = z2;
-    dk2[p] = *reinterpret_cast<const p2*>(dl + kpb + 2 * p);
-  }
+  for (int p = 0; p < KP; ++p) yacc2[p] = z2;
+  ld_pairs<QM, KP>(dl + kpb, dk2);
 
   for (int s = 0; s < S; ++s) {
     // waves still on an earlier trip get the issue arbiter first (it otherwise favours
@@ -629,11 +671,13 @@ __device__ __forceinline__ void pair_tile32(
     const float* Ai = A + ib * LD;
     const float addm = iv ? 0.f : PADNEG, mulm = iv ? 1.f : 0.f;
     const p2 addm2 = {addm, addm}, mulm2 = {mulm, mulm};
+    ld_pairs<QM, KP>(Ai + kpb, a2);
+    if constexpr (MODE == 1) ld_pairs<QM, KP>(wr + ib * LD + kpb, rw2);
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      a2[p] = *reinterpret_cast<const p2*>(Ai + kpb + 2 * p) + addm2;
+      a2[p] += addm2;
       if constexpr (MODE == 1)
-        rw2[p] = *reinterpret_cast<const p2*>(wr + ib * LD + kpb + 2 * p) * mulm2;
+        rw2[p] *= mulm2;
       else
         rw2[p] = z2;
       racc2[p] = z2;
@@ -661,9 +705,12 @@ __device__ __forceinline__ void pair_tile32(
       }
       const float gy = af * g;             // MODE 2: exact (af is 0 or 1)
       const float* Bj = Bv + j * LD;
+      p2 bbv[KP > 0 ? KP : 1], wcv[KP > 0 ? KP : 1];
+      ld_pairs<QM, KP>(Bj + kpb, bbv);
+      if constexpr (MODE == 1) ld_pairs<QM, KP>(wc + j * LD + kpb, wcv);
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
-        const p2 bb = *reinterpret_cast<const p2*>(Bj + kpb + 2 * p);
+        const p2 bb = bbv[p];
         const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
         if constexpr (MODE == 0) {
           // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
@@ -677,7 +724,7 @@ __device__ __forceinline__ void pair_tile32(
           racc2[p] = __builtin_elementwise_fma(sz, g2, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(sz, g2, cacc2[c][p]);
         } else {
-          const p2 w = rw2[p] + *reinterpret_cast<const p2*>(wc + j * LD + kpb + 2 * p);
+          const p2 w = rw2[p] + wcv[p];
           const p2 e = step2(z) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;
@@ -685,12 +732,12 @@ __device__ __forceinline__ void pair_tile32(
         }
       }
       if constexpr (KT) {
-        const float z = at + fmaf(af, dkt, Bj[ktl]);
+        const float z = at + fmaf(af, dkt, ld_tail<QM && (HDG_QTAIL & 1)>(Bj, ktl, grp));
         float e;
         if constexpr (MODE == 0) {
           e = reluf(z);
         } else {
-          const float w = (MODE == 1) ? (rwt + wc[j * LD + ktl]) : g;
+          const float w = (MODE == 1) ? (rwt + ld_tail<QM && (HDG_QTAIL & 2)>(wc + j * LD, ktl, grp)) : g;
           e = (z > 0.f) ? w : 0.f;
           yacct = fmaf(af, e, yacct);
         }
@@ -1695,11 +1742,21 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   const int NE4 = (Ne + 3) & ~3;
   const int Pc = Nc * (Nc - 1);
   int nstamp = 0;
+  // HDG_STOP_AFTER=n (counter-attribution builds only, tools/lds_phases.sh): every block
+  // returns at the n-th top-level phase boundary, so PMC totals of builds n and n+1 differ
+  // by phase n's work (outputs are void in such a build)
+#ifndef HDG_STOP_AFTER
+#define HDG_STOP_AFTER -1
+#endif
+  int nphase = 0;
 #define MID_STAMP()                                                                     \
   do {                                                                                  \
     if constexpr (STAMPS) {                                                             \
       if (threadIdx.x == 0) stamps[prow * 32 + nstamp] = __builtin_amdgcn_s_memrealtime(); \
       ++nstamp;                                                                         \
+    }                                                                                   \
+    if constexpr (HDG_STOP_AFTER >= 0) {                                                \
+      if (nphase++ == HDG_STOP_AFTER) return;                                           \
     }                                                                                   \
     asm volatile("" : "+v"(t));                                                         \
     lane = t & 63;                                                                      \

@@ -304,18 +304,32 @@ class graph2graph(object):
         done = [torch.cuda.Event() for _ in range(2)]
         hst[2].copy_(eng.state)                          # "after epoch -1": the initial state
         outs = {}
+        pflag = torch.zeros(2, dtype=torch.float32).pin_memory()   # fault-poll slots
+        pdone = [torch.cuda.Event() for _ in range(2)]
 
         def launch(i):
-            """Enqueue epoch i: its steps, then the host copies of its stats and end state."""
+            """Enqueue epoch i: its steps, then the host copies of its stats and end state.
+            Split fused epochs of more than FAULT_POLL steps poll the fault slots every
+            FAULT_POLL steps: the poll at step j copies the fault column so far to pinned
+            memory, and waits only for the previous poll's copy (FAULT_POLL steps older), so
+            the GPU keeps FAULT_POLL steps queued and the host is never in lockstep with it;
+            a fault stops the epoch at the next poll after the one that saw it."""
             rows = es[i % 2]
+            npoll = 0
             for j, db in enumerate(batches):
                 eng.train_step(db, logits=self.fetch_logits, stats=rows[j])
                 if nb > FAULT_POLL and (j + 1) % FAULT_POLL == 0 and j + 1 < nb and \
-                        eng.split and eng.path == _lib.PATH_FUSED and \
-                        bool(rows[:j + 1, 7].any()):     # stop a faulted epoch early
-                    rows[j + 1:].zero_()
-                    rows[j + 1:, 7] = 1.0
-                    break
+                        eng.split and eng.path == _lib.PATH_FUSED:
+                    if npoll:
+                        pdone[(npoll - 1) % 2].synchronize()
+                        if pflag[(npoll - 1) % 2].item() != 0.0:   # stop a faulted epoch early
+                            rows[j + 1:].zero_()
+                            rows[j + 1:, 7] = 1.0
+                            break
+                    pflag[npoll % 2:npoll % 2 + 1].copy_(rows[:j + 1, 7].amax().reshape(1),
+                                                         non_blocking=True)
+                    pdone[npoll % 2].record()
+                    npoll += 1
             if nb:                                       # fresh tensors: stable attributes
                 outs[i] = (eng.probs.clone(), eng.logits.clone() if self.fetch_logits else None)
             hs[i % 2].copy_(rows, non_blocking=True)

@@ -193,3 +193,68 @@ def test_model_train_epoch_retry(monkeypatch, tmp_path):
     assert not got.engine.split
     assert torch.equal(got.engine.params, want.engine.params)
     assert got.loss_Hedge_mse == want.loss_Hedge_mse
+
+
+def test_model_train_late_fault_polls_and_retries(monkeypatch, tmp_path, capsys):
+    """The two paths of graph2graph.train's pipelined loop that a fault in epoch 0 never
+    reaches: a split-mode fault that starts inside epoch 1 of a many-step epoch
+    while epoch 2 is already queued.  The fault poll (every FAULT_POLL steps, lagged one
+    poll) stops the faulted epoch early, the host retries epoch 1 from the state after
+    epoch 0 in one-block mode and drops the stale epoch 2.  Parameters, Adam state, printed
+    lines, result file and every checkpoint equal a clean run that leaves split mode at
+    the same step boundary (epoch 0 split, epochs 1-2 one block per commit)."""
+    import hdgnn.model as hm
+    from hdgnn.engine import Engine
+    monkeypatch.setenv("HDG_FUSED_SPLIT", "1")
+    monkeypatch.setattr(hm, "FAULT_POLL", 4)
+    nb, epochs, mb = 12, 3, B                 # polls at steps 4 and 8 of every epoch
+    cb = synth_commits(nb * mb + mb, NE, NC, 13)
+    tr, te = cb.slice(0, nb * mb), cb.slice(nb * mb, nb * mb + mb)
+    orig = Engine.train_step
+
+    def run(tag, fault_from=None, one_block_from=None):
+        monkeypatch.delenv("HDG_DEBUG_XCH_FAULT", raising=False)
+        count = {"n": 0}
+
+        def step(self, *a, **k):            # enqueue-order hook: the host's step counter
+            n = count["n"]
+            if fault_from is not None and n == fault_from:
+                monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+            if one_block_from is not None and n == one_block_from:
+                self.set_split(False)
+            count["n"] += 1
+            return orig(self, *a, **k)
+
+        monkeypatch.setattr(Engine, "train_step", step)
+        d = tmp_path / tag
+        d.mkdir()
+        monkeypatch.chdir(d)
+
+        class Args:
+            checkpoint_dir, Repo = str(d / "ck"), "glide"
+
+        m = hm.graph2graph(None, 1, NE, NC, NE * (NE - 1), NC * (NC - 1), 2, 20, 20, mb,
+                           Args.checkpoint_dir, epochs, 1, 2, 2, "glide", compact=(tr, te, tr))
+        m.train(Args)
+        monkeypatch.setattr(Engine, "train_step", orig)
+        out = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Epoch")]
+        return m, d, out, count["n"]
+
+    with pytest.warns(RuntimeWarning, match="one-block"):
+        got, gd, gout, gsteps = run("fault", fault_from=nb + 2)
+    want, wd, wout, wsteps = run("clean", one_block_from=nb)
+    assert not got.engine.split and not want.engine.split
+    # the faulted epoch 1 stopped at its second poll (step 8), epoch 2's stale launch too,
+    # then epochs 1 and 2 ran again in full: fewer steps than 3 full epochs twice over
+    assert gsteps == nb + 8 + 8 + 2 * nb, gsteps
+    assert wsteps == epochs * nb
+    assert torch.equal(got.engine.state, want.engine.state)       # params, m, v, beta powers
+    assert gout == wout and len(gout) == epochs
+    rel = "outputSelf/glide/model_2/2/result_2.npy"
+    assert (gd / rel).read_bytes() == (wd / rel).read_bytes()
+    ck = "ck/glide/model_2/2"
+    names = sorted(p.name for p in (wd / ck).iterdir())
+    assert names == sorted(p.name for p in (gd / ck).iterdir()) and len(names) > 3
+    for n in names:
+        if n != "checkpoint":
+            assert (gd / ck / n).read_bytes() == (wd / ck / n).read_bytes(), n
