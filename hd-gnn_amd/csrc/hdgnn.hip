@@ -129,7 +129,7 @@ __device__ __forceinline__ void trip_prio(int s) {
 #define HDG_QMAP 1
 #endif
 #ifndef HDG_QTAIL  // quad map: tail units of the column operands by 8-byte reads (1 B, 2 wc)
-#define HDG_QTAIL 1
+#define HDG_QTAIL 0
 #endif
 // Row sums of 5 values over a 16-lane DPP row as a transposed butterfly: 12 DPP adds
 // instead of 20, no selects -- at the two bank-crossing levels (row_mirror: lanes 0-7 vs
@@ -1480,7 +1480,8 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
                                            const float* rho, const float* Tr, const float* Tx,
                                            const int TL, const int* xoff, const int* coff,
                                            const uint8_t* idl, const float* xlr,
-                                           const int n0, const int n1, float* red2) {
+                                           const int n0, const int n1, float* red2,
+                                           const int ne) {
 #pragma clang fp contract(off)
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
   const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
@@ -1509,8 +1510,9 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
       const float cnt = (float)(cum[hi] - cum[lo]);
       const float sx = (float)(pxd[hi] - pxd[lo]);
       const int bm = cum[q];
-      float rs = fmaf(cnt, ri[h], Tr[k * TL + bm]);            // sum_{j in set} rho_i + rho_j
-      float a0 = xi * rs, a1 = fmaf(ri[h], sx, Tx[k * TL + bm]);
+      const int ts = k * TL + 3 + (ra[h] ? ne - bm : bm);       // the set's scan-order count
+      float rs = fmaf(cnt, ri[h], Tr[ts]);                      // sum_{j in set} rho_i + rho_j
+      float a0 = xi * rs, a1 = fmaf(ri[h], sx, Tx[ts]);
       if ((u[h] + vi[h]) > 0.f) {                                // remove j == i
         const float r2 = 2.f * ri[h];
         rs -= r2;
@@ -2810,42 +2812,57 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   }
   if (t <= Ne) offc[t] = e2off;
   WAVE_STAMP(3);
-  // TB: 1 = the rho table, 2 = the x rho table, 3 = both from one gather of rho
+  // The scan inputs in scan order, unit-major: Tr[k][4 + s] = rho of the node at scan slot
+  // s (sorted slot m = s for the prefix units, w1 < 0; Ne - 1 - s for the suffix units), Tx
+  // likewise x rho -- one block-wide pass over rho's rows (a node's 20 units on 20 lanes),
+  // instead of each unit's wave gathering its column through perm: a column of the 20-word
+  // row pitch lies on 8 of the 32 banks, a 4-way conflict on every gathered read.
+  for (int e = t; e < Ne * HS; e += NT_MID) {
+    const int m = e / HS, k = e - m * HS;
+    const float v = rho[perm[m] * HS + k];
+    const int sl = Ws[E1_W1 + HS + k] >= 0.f ? Ne - 1 - m : m;
+    Tr[k * TL + 4 + sl] = v;
+    Tx[k * TL + 4 + sl] = v * xsrt[m];
+  }
+  __syncthreads();
+  // Per-unit inclusive scans in place: T[k][3 + c] = the sum over the first c scan slots
+  // (T[k][3] = 0), so a suffix unit's set [m, Ne) is c = Ne - m and a prefix unit's [0, m)
+  // is c = m (entity_bwd).  A lane owns 4 consecutive slots: one 16-byte read and write.
+  // TB: 1 = the rho table, 2 = the x rho table, 3 = both
   auto unit_scan = [&](const int k, auto tbc) {
     constexpr int TB = decltype(tbc)::value;
-    const bool suf = Ws[E1_W1 + HS + k] >= 0.f;
     float* T0 = Tr + k * TL;
     float* T1 = Tx + k * TL;
+    const int s0 = 4 * lane;                      // NE4 <= 256: one float4 per lane
+    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+    if (s0 < Ne) {
+      if constexpr (TB & 1) a0 = *reinterpret_cast<const float4*>(T0 + 4 + s0);
+      if constexpr (TB & 2) a1 = *reinterpret_cast<const float4*>(T1 + 4 + s0);
+    }
+    const float v0[4] = {a0.x, a0.y, a0.z, a0.w}, v1[4] = {a1.x, a1.y, a1.z, a1.w};
     float run0[4], run1[4];
     float r0 = 0.f, r1 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int s = 4 * lane + q;                 // scan position
-      float v0 = 0.f, v1 = 0.f;
-      if (s < Ne) {
-        const int m = suf ? Ne - 1 - s : s;
-        v0 = rho[perm[m] * HS + k];
-        if constexpr (TB & 2) v1 = v0 * xsrt[m];
-      }
-      r0 += v0;
-      r1 += v1;
+      const bool in = s0 + q < Ne;                  // slots past Ne hold no node
+      r0 += in ? v0[q] : 0.f;
+      r1 += in ? v1[q] : 0.f;
       run0[q] = r0;
       run1[q] = r1;
     }
     const float off0 = (TB & 1) ? wave_incl_scan_dpp(r0) - r0 : 0.f;
     const float off1 = (TB & 2) ? wave_incl_scan_dpp(r1) - r1 : 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int s = 4 * lane + q;
-      if (s < Ne) {
-        const int o = suf ? Ne - 1 - s : s + 1;    // suffix: slots [m, Ne); prefix: [0, m)
-        if constexpr (TB & 1) T0[o] = off0 + run0[q];
-        if constexpr (TB & 2) T1[o] = off1 + run1[q];
-      }
+    if (s0 < Ne) {
+      if constexpr (TB & 1)
+        *reinterpret_cast<float4*>(T0 + 4 + s0) =
+            make_float4(off0 + run0[0], off0 + run0[1], off0 + run0[2], off0 + run0[3]);
+      if constexpr (TB & 2)
+        *reinterpret_cast<float4*>(T1 + 4 + s0) =
+            make_float4(off1 + run1[0], off1 + run1[1], off1 + run1[2], off1 + run1[3]);
     }
     if (lane == 0) {
-      if constexpr (TB & 1) T0[suf ? Ne : 0] = 0.f;
-      if constexpr (TB & 2) T1[suf ? Ne : 0] = 0.f;
+      if constexpr (TB & 1) T0[3] = 0.f;
+      if constexpr (TB & 2) T1[3] = 0.f;
     }
   };
   // units 0..15: both tables on wave k; units 16.. (HS > 16): one table each on waves
@@ -2863,11 +2880,11 @@ __global__ __launch_bounds__(NT_MID) void k_commit_step(
   MID_STAMP();
   if (rfit)
     entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc,
-               reinterpret_cast<const uint8_t*>(Ps), Ps + xl2o, nlo, nhi, red2);
+               reinterpret_cast<const uint8_t*>(Ps), Ps + xl2o, nlo, nhi, red2, Ne);
   else
     entity_bwd(lane, wv, Ws, xs, cum, pxd, nd, rq, rho, Tr, Tx, TL, offr, offc,
                reinterpret_cast<const uint8_t*>(pp + PL.lists),
-               reinterpret_cast<const float*>(pp + PL.xl), nlo, nhi, red2);
+               reinterpret_cast<const float*>(pp + PL.xl), nlo, nhi, red2, Ne);
   WAVE_STAMP(2);
   __syncthreads();
   if (t < 4 * HS) {
