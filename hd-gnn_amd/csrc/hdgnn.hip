@@ -22,7 +22,11 @@
 //   are prefix/suffix sums over the x-sorted order (O(Ne log nd) per hidden unit)
 //   plus sparse corrections for a = 1.  Hunk pairs run as dense register tiles.
 #include <hip/hip_runtime.h>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <math.h>
@@ -4129,6 +4133,174 @@ int hdg_bundle_write(const char* data_path, const char* index_path, const float*
     remove(itmp.c_str());
   }
   return rc;
+}
+
+// ---- background checkpoint writer -------------------------------------------------
+// saver.save off the training thread: one native thread writes the queued bundles (and the
+// small text files that go with them) in submission order, so the training loop's thread
+// only copies the state into the job.  The first failure is kept for flush().
+struct CkptJob {
+  std::vector<float> state;                  // empty: no bundle in this job
+  std::string data_path, index_path, removes, text_path, text;
+  bool text_append = false;
+};
+struct hdg_ckpt_writer_s {
+  std::vector<int32_t> gather;
+  std::vector<uint8_t> image;
+  std::vector<int64_t> entries, blocks;
+  int64_t n_state = 0;
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<CkptJob> q;
+  bool busy = false, stop = false;
+  int err_code = 0;
+  char err[512] = "";
+  std::thread th;
+};
+
+static int ckpt_run(hdg_ckpt_writer_s* w, CkptJob& j) {
+  if (!j.state.empty()) {
+    std::vector<uint8_t> img = w->image;     // the CRCs are patched into a private copy
+    if (int rc = hdg_bundle_write(j.data_path.c_str(), j.index_path.c_str(), j.state.data(),
+                                  (int64_t)j.state.size(), w->gather.data(),
+                                  (int64_t)w->gather.size(), img.data(), (int64_t)img.size(),
+                                  w->entries.data(), (int32_t)(w->entries.size() / 3),
+                                  w->blocks.data(), (int32_t)(w->blocks.size() / 2)))
+      return rc;
+  }
+  size_t a = 0;                              // '\n'-separated paths: missing ones are fine
+  while (a < j.removes.size()) {
+    size_t e = j.removes.find('\n', a);
+    if (e == std::string::npos) e = j.removes.size();
+    if (e > a) remove(j.removes.substr(a, e - a).c_str());
+    a = e + 1;
+  }
+  if (!j.text_path.empty()) {
+    FILE* f = fopen(j.text_path.c_str(), j.text_append ? "ab" : "wb");
+    if (!f) return fail(HDG_EINVAL, "cannot open %s for writing", j.text_path.c_str());
+    const size_t n = j.text.size(), wr = n ? fwrite(j.text.data(), 1, n, f) : 0;
+    if (fclose(f) != 0 || wr != n) return fail(HDG_EINVAL, "short write to %s", j.text_path.c_str());
+  }
+  return 0;
+}
+
+static void ckpt_loop(hdg_ckpt_writer_s* w) {
+  std::unique_lock<std::mutex> lk(w->mu);
+  for (;;) {
+    w->cv.wait(lk, [&] { return w->stop || !w->q.empty(); });
+    if (w->q.empty()) return;                // stop with nothing queued
+    CkptJob j = std::move(w->q.front());
+    w->q.pop_front();
+    w->busy = true;
+    lk.unlock();
+    const int rc = ckpt_run(w, j);
+    lk.lock();
+    if (rc && !w->err_code) {
+      w->err_code = rc;
+      snprintf(w->err, sizeof(w->err), "%s", hdg::g_err);
+    }
+    w->busy = false;
+    if (w->q.empty()) w->idle.notify_all();
+  }
+}
+
+int hdg_ckpt_writer_create(const int32_t* gather, int64_t n_floats, int64_t n_state,
+                           const uint8_t* index_img, int64_t index_len, const int64_t* entries,
+                           int32_t n_entries, const int64_t* blocks, int32_t n_blocks,
+                           void** writer) {
+  if (!writer || !gather || n_floats < 0 || n_state < 0 || !index_img || index_len < 48 ||
+      (n_entries && !entries) || (n_blocks && !blocks))
+    return fail(HDG_EINVAL, "hdg_ckpt_writer_create: bad arguments");
+  for (int64_t i = 0; i < n_floats; ++i)
+    if (gather[i] < 0 || gather[i] >= n_state)
+      return fail(HDG_EINVAL, "hdg_ckpt_writer_create: gather[%lld] outside the state",
+                  (long long)i);
+  auto* w = new hdg_ckpt_writer_s;
+  w->gather.assign(gather, gather + n_floats);
+  w->image.assign(index_img, index_img + index_len);
+  w->entries.assign(entries, entries + 3 * (size_t)n_entries);
+  w->blocks.assign(blocks, blocks + 2 * (size_t)n_blocks);
+  w->n_state = n_state;
+  w->th = std::thread(ckpt_loop, w);
+  *writer = w;
+  return 0;
+}
+
+int hdg_ckpt_writer_submit(void* writer, const float* state, const char* data_path,
+                           const char* index_path, const char* removes, const char* text_path,
+                           const char* text, int32_t text_append) {
+  auto* w = static_cast<hdg_ckpt_writer_s*>(writer);
+  if (!w || (state && (!data_path || !index_path)) || (text_path && !text))
+    return fail(HDG_EINVAL, "hdg_ckpt_writer_submit: bad arguments");
+  CkptJob j;
+  if (state) {
+    j.state.assign(state, state + w->n_state);
+    j.data_path = data_path;
+    j.index_path = index_path;
+  }
+  if (removes) j.removes = removes;
+  if (text_path) {
+    j.text_path = text_path;
+    j.text = text;
+    j.text_append = text_append != 0;
+  }
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->q.push_back(std::move(j));
+  }
+  w->cv.notify_one();
+  return 0;
+}
+
+int hdg_ckpt_writer_flush(void* writer) {
+  auto* w = static_cast<hdg_ckpt_writer_s*>(writer);
+  if (!w) return fail(HDG_EINVAL, "hdg_ckpt_writer_flush: NULL writer");
+  std::unique_lock<std::mutex> lk(w->mu);
+  w->idle.wait(lk, [&] { return w->q.empty() && !w->busy; });
+  const int rc = w->err_code;
+  if (rc) {
+    snprintf(hdg::g_err, sizeof(hdg::g_err), "%s", w->err);
+    w->err_code = 0;                         // reported once, as a future's exception is
+  }
+  return rc;
+}
+
+int hdg_ckpt_writer_destroy(void* writer) {
+  auto* w = static_cast<hdg_ckpt_writer_s*>(writer);
+  if (!w) return 0;
+  const int rc = hdg_ckpt_writer_flush(w);
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->stop = true;
+  }
+  w->cv.notify_all();
+  w->th.join();
+  delete w;
+  return rc;
+}
+
+// stream-ordered copy and completion events for the training loop's host reads (the same
+// HIP calls torch's copy_ / Event make, without the dispatcher on every epoch)
+int hdg_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream));
+  return 0;
+}
+int hdg_event_create(void** ev) {
+  if (!ev) return fail(HDG_EINVAL, "NULL event pointer");
+  HIP_TRY(hipEventCreateWithFlags((hipEvent_t*)ev, hipEventDisableTiming));
+  return 0;
+}
+int hdg_event_record(void* ev, void* stream) {
+  HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+  return 0;
+}
+int hdg_event_synchronize(void* ev) {
+  HIP_TRY(hipEventSynchronize((hipEvent_t)ev));
+  return 0;
+}
+int hdg_event_destroy(void* ev) {
+  if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
+  return 0;
 }
 
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle) {

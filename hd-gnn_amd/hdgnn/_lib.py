@@ -52,7 +52,7 @@ class Dp(ctypes.Structure):
 
 DP_MAX_WORLD, DP_HANDLE_BYTES, DP_MAX_LEN = 16, 64, 3152
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 # gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
 TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
 STATUS_XCH_TIMEOUT, STATUS_DP_TIMEOUT = 1, 2
@@ -71,7 +71,9 @@ EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count
            "hdg_dp_mailbox_alloc", "hdg_dp_mailbox_open", "hdg_dp_mailbox_close",
            "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce",
            "hdg_pack_classes", "hdg_crc32c", "hdg_fwd_bwd_kernel_events",
-           "hdg_bundle_write"]
+           "hdg_bundle_write", "hdg_ckpt_writer_create", "hdg_ckpt_writer_submit",
+           "hdg_ckpt_writer_flush", "hdg_ckpt_writer_destroy", "hdg_memcpy_async",
+           "hdg_event_create", "hdg_event_record", "hdg_event_synchronize", "hdg_event_destroy"]
 
 _lib = None
 
@@ -123,6 +125,17 @@ def load(path=None):
     lib.hdg_crc32c.restype = ctypes.c_uint32
     lib.hdg_bundle_write.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, ctypes.c_int64, vp,
                                      ctypes.c_int64, vp, ctypes.c_int64, vp, i32, vp, i32]
+    cp = ctypes.c_char_p
+    lib.hdg_ckpt_writer_create.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, ctypes.c_int64,
+                                           vp, i32, vp, i32, P(vp)]
+    lib.hdg_ckpt_writer_submit.argtypes = [vp, vp, cp, cp, cp, cp, cp, i32]
+    lib.hdg_ckpt_writer_flush.argtypes = [vp]
+    lib.hdg_ckpt_writer_destroy.argtypes = [vp]
+    lib.hdg_memcpy_async.argtypes = [vp, vp, ctypes.c_size_t, vp]
+    lib.hdg_event_create.argtypes = [P(vp)]
+    lib.hdg_event_record.argtypes = [vp, vp]
+    lib.hdg_event_synchronize.argtypes = [vp]
+    lib.hdg_event_destroy.argtypes = [vp]
     for name in EXPORTS:
         getattr(lib, name)
     _lib = lib

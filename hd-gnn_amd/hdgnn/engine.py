@@ -308,6 +308,25 @@ class Engine:
                                            ctypes.c_void_p(self.workspace.data_ptr()),
                                            self._stream()))
 
+    def step_call(self, dbatch, stats=None, logits=False):
+        """A zero-argument callable that enqueues train_step(dbatch, logits=logits,
+        stats=stats) on the current stream, its ctypes arguments built once (a training
+        loop's per-step host cost).  Single process only; data parallel: train_step itself."""
+        if self.xgmi or self._distributed():
+            return lambda: self.train_step(dbatch, True, logits, stats)
+        self._check(dbatch)
+        b = dbatch.struct()
+        out = self._outputs(True, logits, stats)
+        fn, check = self.lib.hdg_train_step, _lib.check
+        args = (ctypes.byref(self.shape), ctypes.byref(b), ctypes.byref(self._state),
+                ctypes.c_float(self.lr), ctypes.byref(out),
+                ctypes.c_void_p(self.grad.data_ptr()),
+                ctypes.c_void_p(self.workspace.data_ptr()), self._stream())
+
+        def call():
+            check(fn(*args))
+        return call
+
     # ---- HIP graph of one training step ----------------------------------------
     def capture(self, dbatch, outputs=True, logits=False, steps=1):
         """Capture `steps` consecutive train_step(dbatch) calls (fwd_bwd [+ RCCL all-reduce]

@@ -25,6 +25,7 @@ gradient is all-reduced once per step (Engine.allreduce).  The epoch accuracy's 
 count is computed on the device and travels in the gradient trailer, so the same
 all-reduce sums it.  Outputs written to disk are gathered on rank 0.
 """
+import ctypes
 import os
 import time
 
@@ -80,60 +81,83 @@ class Saver(object):
     max_to_keep bundles (TF's default 5) and rewrites the 'checkpoint' state file, as
     Saver.save does; restore() reads a TF-written bundle too (no Adam slots: the
     optimizer state is then left as it is).  The bundle bytes are assembled and written
-    by libhdgnn (tfckpt.BundleTemplate -> hdg_bundle_write) with the GIL released."""
+    by libhdgnn (tfckpt.BundleTemplate -> hdg_bundle_write); background saves go to its
+    native writer thread (tfckpt.BundleWriter), which also takes the training loop's
+    result-file lines, so their file writes never run on the training thread."""
 
     def __init__(self, model, max_to_keep=5):
         self._model = model
         self.max_to_keep = max_to_keep
         self._last = []              # prefixes saved by this Saver, oldest first
-        self._pool = None            # one writer thread: background saves stay in order
-        self._pending = []
         self._tmpl = None
+        self._writer = None
+        self._dirs = set()           # directories known to exist
+
+    def _template(self):
+        if self._tmpl is None:
+            self._tmpl = tfckpt.BundleTemplate(self._model.variant)
+        return self._tmpl
+
+    def writer(self):
+        """The native background writer (created on first use)."""
+        if self._writer is None:
+            self._writer = tfckpt.BundleWriter(self._template())
+        return self._writer
 
     def _host_state(self):
         """[params | adam_m | adam_v | beta_pow] (layout.state_offsets) in one device->host
         copy."""
         return self._model.engine.state.detach().cpu().numpy().copy()
 
-    def save(self, sess, save_path, global_step=None, background=False, state=None):
-        """background=True: the state is copied to the host now (the bundle holds exactly
-        this step's values), the bundle is written by the writer thread while the caller's
-        next steps run; flush() waits for it and re-raises its error.  state: a host copy of
-        the flat training state the caller already holds (graph2graph.train reads it with
-        the epoch's statistics), instead of a fresh device read."""
-        prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
-        state = self._host_state() if state is None else np.array(state, np.float32)
-        if not background:
-            self.flush()
-            return self._write(prefix, state)
-        if self._pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hdg-saver")
-        self._pending = [f for f in self._pending if not f.done() or f.exception()]
-        self._pending.append(self._pool.submit(self._write, prefix, state))
-        return prefix
+    def _mkdir(self, d):
+        if d not in self._dirs:
+            os.makedirs(d, exist_ok=True)
+            self._dirs.add(d)
 
-    def flush(self):
-        pending, self._pending = self._pending, []
-        for f in pending:
-            f.result()
-
-    def _write(self, prefix, state):
-        if self._tmpl is None:
-            self._tmpl = tfckpt.BundleTemplate(self._model.variant)
+    def _book(self, prefix):
+        """max_to_keep bookkeeping of a save at prefix: (paths to delete, state-file path,
+        state-file text)."""
         d = os.path.dirname(prefix) or "."
-        self._tmpl.write(prefix, state)
         if prefix in self._last:
             self._last.remove(prefix)
         self._last.append(prefix)
+        removes = []
         while self.max_to_keep and len(self._last) > self.max_to_keep:
             old = self._last.pop(0)
-            for f in (old + ".index", old + ".data-00000-of-00001"):
-                if os.path.exists(f):
-                    os.remove(f)
-        tfckpt.write_state_file(d, os.path.basename(prefix),
-                                [os.path.basename(q) for q in self._last
-                                 if (os.path.dirname(q) or ".") == d])
+            removes += [old + ".index", old + ".data-00000-of-00001"]
+        text = tfckpt.state_file_text(os.path.basename(prefix),
+                                      [os.path.basename(q) for q in self._last
+                                       if (os.path.dirname(q) or ".") == d])
+        return removes, os.path.join(d, "checkpoint"), text
+
+    def save(self, sess, save_path, global_step=None, background=False, state=None):
+        """background=True: the writer thread writes the bundle of this state (a host copy
+        taken now, so it holds exactly this step's values) while the caller's next steps
+        run; flush() waits for it and raises its error.  state: a host copy of the flat
+        training state the caller already holds (graph2graph.train reads it with the epoch's
+        statistics), instead of a fresh device read."""
+        prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
+        state = self._host_state() if state is None else state
+        self._mkdir(os.path.dirname(prefix) or ".")
+        if not background:
+            self.flush()
+            return self._write(prefix, state)
+        removes, spath, text = self._book(prefix)
+        self.writer().submit(prefix, state, removes, spath, text)
+        return prefix
+
+    def flush(self):
+        if self._writer is not None:
+            self._writer.flush()
+
+    def _write(self, prefix, state):
+        self._template().write(prefix, state)
+        removes, spath, text = self._book(prefix)
+        for f in removes:
+            if os.path.exists(f):
+                os.remove(f)
+        with open(spath, "w") as f:
+            f.write(text)
         return prefix
 
     def restore(self, sess, save_path):
@@ -301,11 +325,26 @@ class graph2graph(object):
         es = [torch.zeros(nr, _lib.STATS_LEN, dtype=torch.float32, device=dev) for _ in range(2)]
         hs = [torch.zeros(nr, _lib.STATS_LEN, dtype=torch.float32).pin_memory() for _ in range(2)]
         hst = [torch.zeros(S, dtype=torch.float32).pin_memory() for _ in range(3)]
-        done = [torch.cuda.Event() for _ in range(2)]
         hst[2].copy_(eng.state)                          # "after epoch -1": the initial state
         outs = {}
         pflag = torch.zeros(2, dtype=torch.float32).pin_memory()   # fault-poll slots
         pdone = [torch.cuda.Event() for _ in range(2)]
+        # per step row and epoch parity: the step with its ctypes arguments built once; the
+        # epoch's host reads and completion events through libhdgnn (hipMemcpyAsync /
+        # hipEvent: no dispatcher round per epoch)
+        lib = eng.lib
+        steps = [[eng.step_call(db, stats=es[p][j], logits=self.fetch_logits)
+                  for j, db in enumerate(batches)] for p in range(2)]
+        stream = eng._stream()
+        done = [ctypes.c_void_p() for _ in range(2)]
+        for ev in done:
+            _lib.check(lib.hdg_event_create(ctypes.byref(ev)))
+        rows_bytes, state_bytes = nr * _lib.STATS_LEN * 4, S * 4
+        filepath = None
+        if self.rank == 0:
+            filepath = r'outputSelf/{}/model_{}/{}/result_{}.npy'.format(
+                args.Repo, self.variant, self.Step, self.Step)
+            os.makedirs(os.path.dirname(filepath), exist_ok=True)
 
         def launch(i):
             """Enqueue epoch i: its steps, then the host copies of its stats and end state.
@@ -316,8 +355,8 @@ class graph2graph(object):
             a fault stops the epoch at the next poll after the one that saw it."""
             rows = es[i % 2]
             npoll = 0
-            for j, db in enumerate(batches):
-                eng.train_step(db, logits=self.fetch_logits, stats=rows[j])
+            for j, step in enumerate(steps[i % 2]):
+                step()
                 if nb > FAULT_POLL and (j + 1) % FAULT_POLL == 0 and j + 1 < nb and \
                         eng.split and eng.path == _lib.PATH_FUSED:
                     if npoll:
@@ -330,12 +369,28 @@ class graph2graph(object):
                                                          non_blocking=True)
                     pdone[npoll % 2].record()
                     npoll += 1
-            if nb:                                       # fresh tensors: stable attributes
+            if nb and i == self.epoch - 1:              # the fetched outputs of the last step
                 outs[i] = (eng.probs.clone(), eng.logits.clone() if self.fetch_logits else None)
-            hs[i % 2].copy_(rows, non_blocking=True)
-            hst[i % 3].copy_(eng.state, non_blocking=True)
-            done[i % 2].record()
+            _lib.check(lib.hdg_memcpy_async(ctypes.c_void_p(hs[i % 2].data_ptr()),
+                                            ctypes.c_void_p(rows.data_ptr()), rows_bytes, stream))
+            _lib.check(lib.hdg_memcpy_async(ctypes.c_void_p(hst[i % 3].data_ptr()),
+                                            ctypes.c_void_p(eng.state.data_ptr()), state_bytes,
+                                            stream))
+            _lib.check(lib.hdg_event_record(done[i % 2], stream))
 
+        try:
+            self._train_epochs(args, launch, done, hs, hst, outs, nb, th_off, counter, filepath)
+        finally:
+            for ev in done:
+                lib.hdg_event_destroy(ev)
+        end_time1 = time.time()
+        if self.rank == 0:
+            print('test time:' + str(end_time1 - start_time1))
+
+    def _train_epochs(self, args, launch, done, hs, hst, outs, nb, th_off, counter, filepath):
+        """train()'s epoch loop: epoch i+1 enqueued before the host waits for epoch i."""
+        import torch
+        eng, lib, dev = self.engine, self.engine.lib, self.engine.device
         self._barrier()
         if self.epoch > 0:
             launch(0)
@@ -343,7 +398,7 @@ class graph2graph(object):
         while i < self.epoch:
             if i + 1 < self.epoch and self.world == 1:
                 launch(i + 1)
-            done[i % 2].synchronize()
+            _lib.check(lib.hdg_event_synchronize(done[i % 2]))
             host = hs[i % 2].numpy().astype(np.float64)
             if host[:nb, 7].any():                       # a split-mode exchange timed out
                 torch.cuda.synchronize(dev)              # epoch i+1 (if launched) drained
@@ -366,7 +421,8 @@ class graph2graph(object):
                 self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[nb - 1, 0]),
                                                                       float(host[nb - 1, 1]),
                                                                       float(host[nb - 1, 2]))
-                self.C_edge_output2, self.C_edge_output2_logits = outs.pop(i)
+                if i in outs:
+                    self.C_edge_output2, self.C_edge_output2_logits = outs.pop(i)
             acc_top = correct / (nb * self.mini_batch_num * self.Ncr) if nb else 0.0
             # theta (model_2.py:369-371, 392): map_theta2 in the state after epoch i, as
             # self.theta reads it at this point
@@ -377,11 +433,9 @@ class graph2graph(object):
                            " map MSE: " + str(tr_loss_map / nb if nb else 0.0)[0:6] + \
                            " theta: " + str(theta[0]) + ' ' + str(theta[1]) + '\n'
             if self.rank == 0:
-                filepath = r'outputSelf/{}/model_{}/{}/result_{}.npy'.format(
-                    args.Repo, self.variant, self.Step, self.Step)
-                os.makedirs(os.path.dirname(filepath), exist_ok=True)
-                with open(filepath, "a", encoding='utf-8') as f:
-                    f.write(resultString)
+                # appended by the writer thread, in order with the checkpoints (same bytes
+                # as the reference's open(..., "a") + write per epoch)
+                self.saver.writer().submit(text_path=filepath, text=resultString, append=True)
                 print(resultString)
             counter += 1
             self.save(args.checkpoint_dir, counter, background=True, state=state)
@@ -389,10 +443,7 @@ class graph2graph(object):
             if self.world > 1 and i + 1 < self.epoch:   # DP: ranks launch in step after the barrier
                 launch(i + 1)
             i += 1
-        self.saver.flush()          # every epoch's bundle on disk before train() returns
-        end_time1 = time.time()
-        if self.rank == 0:
-            print('test time:' + str(end_time1 - start_time1))
+        self.saver.flush()          # every epoch's files on disk before train() returns
 
     # sess.run's fetched C_edge_output2 / C_edge_output2_logits.  Training keeps the last
     # step's device output as a fresh tensor per epoch (later steps never change it) and

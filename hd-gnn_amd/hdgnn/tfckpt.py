@@ -538,6 +538,66 @@ class BundleTemplate(object):
             len(self.blocks)))
 
 
+class BundleWriter(object):
+    """libhdgnn's background writer (hdg_ckpt_writer_*) over a BundleTemplate: one native
+    thread writes the queued bundles and text files in submission order, so the training
+    loop's thread only hands over a copy of the state (no Python runs on the writer, nothing
+    holds the GIL while it writes).  flush() waits for the queue and raises the first
+    failure since the previous flush."""
+
+    def __init__(self, template):
+        import ctypes
+        from . import _lib
+        self._lib = _lib.load()
+        self._t = template
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.hdg_ckpt_writer_create(
+            template.gather.ctypes.data, template.gather.size, template.n_state,
+            template.image.ctypes.data, template.image.size, template.entries.ctypes.data,
+            len(template.entries), template.blocks.ctypes.data, len(template.blocks),
+            ctypes.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def _b(v):
+        return None if v is None else v.encode("utf-8")
+
+    def submit(self, prefix=None, state=None, removes=(), text_path=None, text=None,
+               append=False):
+        """Queue: the bundle of `state` at `prefix` (if given), then delete `removes`, then
+        write (or append) `text` to `text_path` (if given)."""
+        if state is not None:
+            state = np.ascontiguousarray(state, np.float32)
+            if state.size != self._t.n_state:
+                raise CheckpointError("state has %d floats, the template %d"
+                                      % (state.size, self._t.n_state))
+        rm = "\n".join(removes) if removes else None
+        rc = self._lib.hdg_ckpt_writer_submit(
+            self._h, None if state is None else state.ctypes.data,
+            self._b(None if prefix is None else _shard_name(prefix, 0, 1)),
+            self._b(None if prefix is None else prefix + ".index"), self._b(rm),
+            self._b(text_path), self._b(text), 1 if append else 0)
+        if rc:
+            raise CheckpointError(self._lib.hdg_last_error().decode(errors="replace"))
+
+    def flush(self):
+        if self._h is not None and self._lib.hdg_ckpt_writer_flush(self._h):
+            raise CheckpointError(self._lib.hdg_last_error().decode(errors="replace"))
+
+    def close(self):
+        h, self._h = self._h, None
+        if h is not None and self._lib.hdg_ckpt_writer_destroy(h):
+            raise CheckpointError(self._lib.hdg_last_error().decode(errors="replace"))
+
+    def __del__(self):
+        import sys
+        if not sys.is_finalizing():
+            try:
+                self.close()
+            except Exception:
+                pass
+
+
 def latest(checkpoint_dir):
     """tf.train.get_checkpoint_state(dir).model_checkpoint_path's basename, or None."""
     p = os.path.join(checkpoint_dir, "checkpoint")
@@ -554,13 +614,16 @@ def latest(checkpoint_dir):
     return None
 
 
-def write_state_file(checkpoint_dir, name, all_names=None):
+def state_file_text(name, all_names=None):
     """The CheckpointState text proto tf.train.Saver.save writes next to the bundles:
     the latest prefix and every prefix still kept (max_to_keep), oldest first."""
+    return ('model_checkpoint_path: "%s"\n' % name +
+            "".join('all_model_checkpoint_paths: "%s"\n' % n for n in (all_names or [name])))
+
+
+def write_state_file(checkpoint_dir, name, all_names=None):
     with open(os.path.join(checkpoint_dir, "checkpoint"), "w") as f:
-        f.write('model_checkpoint_path: "%s"\n' % name)
-        for n in (all_names or [name]):
-            f.write('all_model_checkpoint_paths: "%s"\n' % n)
+        f.write(state_file_text(name, all_names))
 
 
 def remove_bundle(prefix):

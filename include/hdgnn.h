@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 7
+#define HDG_ABI_VERSION 8
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -282,6 +282,32 @@ int hdg_bundle_write(const char* data_path, const char* index_path, const float*
                      int64_t n_state, const int32_t* gather, int64_t n_floats,
                      uint8_t* index_img, int64_t index_len, const int64_t* entries,
                      int32_t n_entries, const int64_t* blocks, int32_t n_blocks);
+/* Host utility: background checkpoint writer (saver.save off the training thread).  One
+ * native thread runs the submitted jobs in order; a job writes a bundle of `state` exactly
+ * as hdg_bundle_write does with the writer's template (gather / index image / entries /
+ * blocks, copied at create), then removes the '\n'-separated `removes` paths (bundles that
+ * fell out of max_to_keep; missing files are fine), then writes `text` to `text_path`
+ * (appended when text_append != 0, else replacing it: the 'checkpoint' state file, a
+ * result line).  NULL state / removes / text_path skip that part.  submit copies
+ * everything it is given (n_state floats of state) and returns at once; flush waits for
+ * the queue and returns the first failure since the last flush (HDG_EINVAL, message in
+ * hdg_last_error); destroy flushes, stops the thread and frees the writer.              */
+int hdg_ckpt_writer_create(const int32_t* gather, int64_t n_floats, int64_t n_state,
+                           const uint8_t* index_img, int64_t index_len, const int64_t* entries,
+                           int32_t n_entries, const int64_t* blocks, int32_t n_blocks,
+                           void** writer);
+int hdg_ckpt_writer_submit(void* writer, const float* state, const char* data_path,
+                           const char* index_path, const char* removes, const char* text_path,
+                           const char* text, int32_t text_append);
+int hdg_ckpt_writer_flush(void* writer);
+int hdg_ckpt_writer_destroy(void* writer);
+/* Host utility: hipMemcpyAsync (kind default) and completion events without timing, for
+ * the training loop's stream-ordered reads into pinned host memory.                     */
+int hdg_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
+int hdg_event_create(void** event);
+int hdg_event_record(void* event, void* stream);
+int hdg_event_synchronize(void* event);
+int hdg_event_destroy(void* event);
 /* allocate + zero this rank's mailbox on the current device; handle: 64 bytes out */
 int hdg_dp_mailbox_alloc(void** mailbox, void* handle);
 /* map a peer's mailbox (its handle) into this process; close / free undo the calls */

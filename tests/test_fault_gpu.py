@@ -210,22 +210,26 @@ def test_model_train_late_fault_polls_and_retries(monkeypatch, tmp_path, capsys)
     nb, epochs, mb = 12, 3, B                 # polls at steps 4 and 8 of every epoch
     cb = synth_commits(nb * mb + mb, NE, NC, 13)
     tr, te = cb.slice(0, nb * mb), cb.slice(nb * mb, nb * mb + mb)
-    orig = Engine.train_step
+    orig = Engine.step_call
 
     def run(tag, fault_from=None, one_block_from=None):
         monkeypatch.delenv("HDG_DEBUG_XCH_FAULT", raising=False)
         count = {"n": 0}
 
-        def step(self, *a, **k):            # enqueue-order hook: the host's step counter
-            n = count["n"]
-            if fault_from is not None and n == fault_from:
-                monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
-            if one_block_from is not None and n == one_block_from:
-                self.set_split(False)
-            count["n"] += 1
-            return orig(self, *a, **k)
+        def step_call(self, *a, **k):       # enqueue-order hook: the host's step counter
+            call = orig(self, *a, **k)
 
-        monkeypatch.setattr(Engine, "train_step", step)
+            def step():
+                n = count["n"]
+                if fault_from is not None and n == fault_from:
+                    monkeypatch.setenv("HDG_DEBUG_XCH_FAULT", "1")
+                if one_block_from is not None and n == one_block_from:
+                    self.set_split(False)
+                count["n"] += 1
+                return call()
+            return step
+
+        monkeypatch.setattr(Engine, "step_call", step_call)
         d = tmp_path / tag
         d.mkdir()
         monkeypatch.chdir(d)
@@ -236,7 +240,7 @@ def test_model_train_late_fault_polls_and_retries(monkeypatch, tmp_path, capsys)
         m = hm.graph2graph(None, 1, NE, NC, NE * (NE - 1), NC * (NC - 1), 2, 20, 20, mb,
                            Args.checkpoint_dir, epochs, 1, 2, 2, "glide", compact=(tr, te, tr))
         m.train(Args)
-        monkeypatch.setattr(Engine, "train_step", orig)
+        monkeypatch.setattr(Engine, "step_call", orig)
         out = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Epoch")]
         return m, d, out, count["n"]
 

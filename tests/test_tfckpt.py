@@ -265,3 +265,33 @@ def test_native_bundle_write_checks_gather_bounds(tmp_path):
     assert rc == 1000                          # HDG_EINVAL
     assert b"gather" in lib.hdg_last_error()
     assert not list(tmp_path.iterdir())
+
+
+def test_native_writer_order_text_and_errors(tmp_path):
+    """tfckpt.BundleWriter (libhdgnn's writer thread): jobs run in submission order (a
+    bundle, then its removals, then the state file; appended text accumulates), and a
+    failure surfaces at the next flush() -- once -- without stopping later jobs."""
+    t = tfckpt.BundleTemplate(2)
+    w = tfckpt.BundleWriter(t)
+    st = np.arange(t.n_state, dtype=np.float32)
+    res = str(tmp_path / "result_2.npy")
+    for k in range(3):
+        w.submit(str(tmp_path / ("m-%d" % k)), st + k,
+                 removes=[str(tmp_path / ("m-%d.index" % (k - 2)))] if k >= 2 else (),
+                 text_path=str(tmp_path / "checkpoint"), text="latest %d\n" % k)
+        w.submit(text_path=res, text="Epoch %d\n" % (k + 1), append=True)
+    w.flush()
+    assert open(res).read() == "Epoch 1\nEpoch 2\nEpoch 3\n"
+    assert open(tmp_path / "checkpoint").read() == "latest 2\n"
+    assert not (tmp_path / "m-0.index").exists() and (tmp_path / "m-1.index").exists()
+    fl, m, v, bp = tfckpt.engine_state(tfckpt.read(str(tmp_path / "m-2")), 2)
+    P, so = layout.n_params(2), layout.state_offsets(2)
+    np.testing.assert_array_equal(fl, (st + 2)[:P])
+    np.testing.assert_array_equal(m, (st + 2)[so["m"]:so["m"] + P])
+    w.submit(str(tmp_path / "missing_dir" / "x"), st)       # cannot be written
+    w.submit(text_path=res, text="after\n", append=True)     # still runs
+    with pytest.raises(tfckpt.CheckpointError, match="missing_dir"):
+        w.flush()
+    w.flush()                                                 # reported once
+    assert open(res).read().endswith("Epoch 3\nafter\n")
+    w.close()
