@@ -1703,9 +1703,11 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   // grid read a clamped address and store 0
   const int tr = threadIdx.x >> 5, tc4 = (threadIdx.x & 31) * 4;
   const bool al4 = (Nc & 3) == 0;                 // rows 16-byte aligned: float4 loads
+  WSTAMP(11, 0);
   for (int c0 = 0; c0 < Nc; c0 += CHM) {   // gamma's diagonal is 0: no self pair to remove
     const int c1 = c0 + CHM < Nc ? c0 + CHM : Nc;
     __syncthreads();
+    if (c0 == 0) WSTAMP(11, 1);
     stage_rows(os_, oth, c0, c1);
     for (int e = threadIdx.x; e < (c1 - c0) * H; e += NTP)
       ose[e] = oth[(size_t)c0 * H + e] + D[D_EPS + e % H];
@@ -1739,6 +1741,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
     }
     __syncthreads();
+    if (c0 == 0) WSTAMP(11, 2);
     int lo, hi;
     wave_share(c0, c1, lo, hi);
     // one loop per pass (block-uniform): gamma from the LDS tile (row pass) or global
@@ -1771,12 +1774,16 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     };
     if (z == 0) sweep(std::true_type{});
     else sweep(std::false_type{});
+    if (c0 == 0) WSTAMP(11, 3);
   }
+  WSTAMP(11, 4);
   __syncthreads();                       // every wave is done with os_ / gt (= buf)
   combine8(acc, buf, res);
   if (z == 0) combine8(ya, buf, yres);
+  WSTAMP(11, 5);
   clsb_epilogue(z, b, t0, tc, Nc, W, o, D, G, Hh, Dsig, Dtau, dG, dH, part, sg, res, yres, Gt, X,
                 sumD, ysum, Wl, kzh, blockIdx.x);
+  WSTAMP(11, 6);
 }
 
 // kw_hunk_mlpb's epilogue: the tile's D alpha / D beta rows out, the partial rows of dV1

@@ -30,6 +30,8 @@ ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--variant", type=int, default=2)
 ap.add_argument("--hunk", default="sorted")
 ap.add_argument("--path", type=int, default=2, help="0 auto, 1 fused (model_4: hybrid), 2 general")
+ap.add_argument("--groups", type=int, default=1,
+                help="report the stamped waves as this many contiguous groups (grid z slices)")
 a = ap.parse_args()
 flags = {"dense": _lib.FLAG_HUNK_DENSE, "sorted": _lib.FLAG_HUNK_SORTED,
          "tiled": _lib.FLAG_HUNK_TILED}[a.hunk]
@@ -45,21 +47,22 @@ for _ in range(3):
     eng.fwd_bwd(db)
 torch.cuda.synchronize()
 lib.hdg_wstamp_set(ctypes.c_void_p(0))
-s = st.view(N, 8).cpu().numpy()[:, :a.slots].astype(np.int64)
-s = s[s[:, 0] > 0]
-done = (s > 0).all(1)
-print("waves stamped %d (complete %d)" % (len(s), int(done.sum())))
-s = s[done]
-d = np.diff(s, axis=1) * 1e-2               # 100 MHz ticks -> us
-for i in range(a.slots - 1):
-    print("stamp %d->%d  median %7.2f  p90 %7.2f  max %7.2f us" % (
-        i, i + 1, np.median(d[:, i]), np.percentile(d[:, i], 90), d[:, i].max()))
-tot = (s[:, -1] - s[:, 0]) * 1e-2
-print("per wave total: median %.2f p90 %.2f max %.2f us" % (np.median(tot), np.percentile(tot, 90),
-                                                              tot.max()))
-t0 = (s[:, 0] - s[:, 0].min()) * 1e-2
-print("wave starts: p10 %.2f median %.2f p90 %.2f max %.2f us; kernel span %.2f us" % (
-    np.percentile(t0, 10), np.median(t0), np.percentile(t0, 90), t0.max(),
-    (s[:, -1].max() - s[:, 0].min()) * 1e-2))
-h, edges = np.histogram(t0, bins=np.arange(0, t0.max() + 1.0, 1.0))
-print("wave starts per us: " + " ".join("%d" % c for c in h))
+s_all = st.view(N, 8).cpu().numpy()[:, :a.slots].astype(np.int64)
+s_all = s_all[s_all[:, 0] > 0]
+for gi, s in enumerate(np.array_split(s_all, a.groups)):
+    if a.groups > 1:
+        print("-- group %d of %d" % (gi, a.groups))
+    done = (s > 0).all(1)
+    print("waves stamped %d (complete %d)" % (len(s), int(done.sum())))
+    s = s[done]
+    d = np.diff(s, axis=1) * 1e-2               # 100 MHz ticks -> us
+    for i in range(a.slots - 1):
+        print("stamp %d->%d  median %7.2f  p90 %7.2f  max %7.2f us" % (
+            i, i + 1, np.median(d[:, i]), np.percentile(d[:, i], 90), d[:, i].max()))
+    tot = (s[:, -1] - s[:, 0]) * 1e-2
+    print("per wave total: median %.2f p90 %.2f max %.2f us" % (
+        np.median(tot), np.percentile(tot, 90), tot.max()))
+    t0 = (s[:, 0] - s_all[:, 0].min()) * 1e-2
+    print("wave starts: p10 %.2f median %.2f p90 %.2f max %.2f us; span %.2f us" % (
+        np.percentile(t0, 10), np.median(t0), np.percentile(t0, 90), t0.max(),
+        (s[:, -1].max() - s_all[:, 0].min()) * 1e-2))
