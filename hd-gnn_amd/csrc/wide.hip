@@ -1659,6 +1659,10 @@ __device__ __forceinline__ void clsb_epilogue(
 //   global loads, no index division).
 // ---------------------------------------------------------------------------------
 constexpr int GTP = CHM + 1;   // gamma tile pitch
+#ifndef HDG_CLSB_CTILE        // kw_hunk_clsb column pass: gamma staged through LDS (1) or
+#define HDG_CLSB_CTILE 1      // read from global memory per swept row (0)
+#endif
+static_assert(CHM * TN <= TN * GTP, "the column pass's gamma tile fits the row pass's");
 __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void kw_hunk_clsb(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Nc,
@@ -1739,6 +1743,28 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
           d[3] = rin ? gv[i].w : 0.f;
         }
       }
+    } else if (HDG_CLSB_CTILE) {
+      // column pass: the chunk's gamma rows over the tile's 64 columns, staged as they lie
+      // ([m - c0][lane], pitch TN): coalesced 16-byte loads instead of one dependent global
+      // load per swept row; columns past the grid 0 (their lanes' sums are not used)
+      float4 gv[CHM * TN / (4 * NTP)];
+      const int rr = threadIdx.x >> 4, cc4 = (threadIdx.x & 15) * 4, cg = t0 + cc4;
+#pragma unroll
+      for (int i = 0; i < CHM * TN / (4 * NTP); ++i) {
+        const int r = c0 + rr + (NTP / 16) * i;
+        const float* src = gb + (size_t)(r < c1 ? r : c1 - 1) * Nc;
+        if (al4 && cg + 3 < Nc) {
+          gv[i] = *reinterpret_cast<const float4*>(src + cg);
+        } else {
+          gv[i].x = cg < Nc ? src[cg] : 0.f;
+          gv[i].y = cg + 1 < Nc ? src[cg + 1] : 0.f;
+          gv[i].z = cg + 2 < Nc ? src[cg + 2] : 0.f;
+          gv[i].w = cg + 3 < Nc ? src[cg + 3] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CHM * TN / (4 * NTP); ++i)
+        *reinterpret_cast<float4*>(gt + (rr + (NTP / 16) * i) * TN + cc4) = gv[i];
     }
     __syncthreads();
     if (c0 == 0) WSTAMP(11, 2);
@@ -1754,7 +1780,8 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
       for (int m = lo; m < hi; ++m) {
         if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
         const bool y1 = (word >> (m & 31)) & 1u;
-        const float g = ROW ? gt[lane * GTP + (m - c0)] : gb[(size_t)m * Nc + ncl];
+        const float g = ROW ? gt[lane * GTP + (m - c0)]
+                            : (HDG_CLSB_CTILE ? gt[(m - c0) * TN + lane] : gb[(size_t)m * Nc + ncl]);
         const f2 g2 = {g, g}, gy2 = y1 ? g2 : (f2){0.f, 0.f};
         // [kappa > 0] g and [kappa > 0] y g as one fma each (the products are exact)
         const float4* o4 = reinterpret_cast<const float4*>((y1 ? ose : os_) + (m - c0) * H);
