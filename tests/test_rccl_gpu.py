@@ -88,8 +88,12 @@ def test_bench_gpus2_starts_two_ranks():
         assert "ranks_share_device" in d["config"]
 
 
-def test_bench_under_torchrun_uses_rccl():
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+@pytest.mark.parametrize("mode", ["rccl", "auto"])
+def test_bench_under_torchrun(mode):
+    """bench.py under torch.distributed.run (world 1): HDG_DP_ALLREDUCE=rccl must run the
+    RCCL all-reduce of the flat gradient (nccl backend = RCCL); auto picks the xGMI
+    mailboxes when their self-test passes, else RCCL."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HDG_DP_ALLREDUCE=mode)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5", "--warmup", "2",
@@ -103,5 +107,7 @@ def test_bench_under_torchrun_uses_rccl():
     # verdict (world 1: the mailbox exchange with itself), the tail time per step
     dp = d["dp"]
     assert dp["allreduce"] in ("xgmi", "rccl") and dp["selftest"]
+    if mode == "rccl":
+        assert dp["allreduce"] == "rccl" and "not tried" in dp["selftest"]
     assert dp["allreduce"] != "xgmi" or dp["selftest"].startswith("passed")
     assert dp["tail_ms_per_step"] > 0
