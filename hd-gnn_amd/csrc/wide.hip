@@ -75,6 +75,9 @@ __device__ unsigned long long* g_wst;
 #else
 #define WSTAMP(kid, k) do {} while (0)
 #endif
+#ifndef HDG_ABL_XJ    // ablation builds only: neighbour x reads at conflict-free addresses
+#define HDG_ABL_XJ 0  // (wrong sums; for timing the LDS gathers of the walks)
+#endif
 
 
 template <int CTRL>
@@ -825,6 +828,7 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
       dense2[kk] = acc;
     }
   }
+  WSTAMP(7, 1);
   // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i)), one clamped
   // packed fma per two hidden units and neighbour (clamp_coef); KPW = 5: two packed
   // pairs + one scalar unit
@@ -851,13 +855,13 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
     f2 sr[2] = {(f2){0.f, 0.f}, (f2){0.f, 0.f}}, sc[2] = {sr[0], sr[1]};
     float srt = 0.f, sct = 0.f;
     for_list<2>(prep, 0, b, i, Ne, Nc, [&](int j) {   // xb[Ne] = NaN: clamps to 0
-      const float xj = xb[j];
+      const float xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
       sr[0] += clamp_fma2(xj, ra[0], rb2[0]);
       sr[1] += clamp_fma2(xj, ra[1], rb2[1]);
       srt += clamp_fma1(xj, rat, rbt);
     });
     for_list<2>(prep, 1, b, i, Ne, Nc, [&](int j) {
-      const float xj = xb[j];
+      const float xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
       sc[0] += clamp_fma2(xj, ca[0], cb[0]);
       sc[1] += clamp_fma2(xj, ca[1], cb[1]);
       sct += clamp_fma1(xj, cat, cbt);
@@ -1012,11 +1016,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
     ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
   // the per-node products on the tile (node_fwd_tile): its inputs are this block's outputs
   // (global writes made visible to the block by the barrier)
-  WSTAMP(7, 1);
-  __syncthreads();
   WSTAMP(7, 2);
-  node_fwd_tile(x, W, o, Ne, ent_part, P, R1, C1, no);
+  __syncthreads();
   WSTAMP(7, 3);
+  node_fwd_tile(x, W, o, Ne, ent_part, P, R1, C1, no);
+  WSTAMP(7, 4);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1559,6 +1563,9 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
 // the y-weighted sums yres, row pass), D = c (.) sums out, dG = D M^T (dH), and the partial
 // rows of dU1 / dd1 / dV2 / dc2 through X = sum_n G_n (x) D_n (model_2.py:265-275, 304-321).
 // LDS: res, yres, Gt [TN][HP]; X [H][H]; sumD, ysum [H]; Wl the staged M | V2 | c2 | U1e.
+// Every product is a 16x16 MFMA tile on its own wave (8 waves): X (with sum_n D_n as the row
+// of Gt's padding column set to 1) and dG, then dU1e and dV2 -- no serial 20- or 64-term
+// LDS loops.
 __device__ __forceinline__ void clsb_epilogue(
     const int z, const int b, const int t0, const int tc, const int Nc, const float* __restrict__ W,
     const Off& o, const float* __restrict__ D, const float* __restrict__ G,
@@ -1566,6 +1573,7 @@ __device__ __forceinline__ void clsb_epilogue(
     float* __restrict__ dG, float* __restrict__ dH, float* __restrict__ part, const Segs& sg,
     float* res, float* yres, float* Gt, float* X, float* sumD, float* ysum, const float* Wl,
     const float* kzh, const int tile) {
+  static_assert(NTP == 512, "clsb_epilogue maps its 16 product tiles onto 8 waves");
   const float *Ml = Wl, *V2 = Wl + H * H, *c2 = Wl + 2 * H * H, *U1e = Wl + 2 * H * H + H;
   (void)W;
   const float* gsrc = (z ? Hh : G) + (size_t)b * Nc * H;
@@ -1577,73 +1585,89 @@ __device__ __forceinline__ void clsb_epilogue(
     const float d = in ? res[n * HP + k] * D[D_CV + k] : 0.f;
     res[n * HP + k] = d;
     Gt[n * HP + k] = in ? gsrc[(t0 + n) * H + k] : 0.f;
+    if (k == 0) Gt[n * HP + H] = in ? 1.f : 0.f;             // X's row H: sum_n D_n
     if (z == 0 && !in) yres[n * HP + k] = 0.f;
     if (in) dout[(t0 + n) * H + k] = d;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < TN * H; e += blockDim.x) {   // dG_n[l] = sum_k M[l][k] D_n[k]
-    const int n = e / H, l = e - n * H;
-    if (t0 + n >= Nc) continue;
-    float sacc = 0.f;
-    for (int k = 0; k < H; ++k) sacc = fmaf(Ml[l * H + k], res[n * HP + k], sacc);
-    gout[(t0 + n) * H + l] = sacc;
-  }
-  if (threadIdx.x < 256) {   // X_blk = sum_n G_n (x) D_n: 2 x 2 16x16 MFMA tiles, K = 64 nodes
-    const int lane = threadIdx.x & 63, tq = threadIdx.x >> 6;   // wave-uniform
-    const int rl = (tq >> 1) * 16 + (lane & 15), kc = (tq & 1) * 16 + (lane & 15);
-    const bool rv = rl < H, cv = kc < H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r16 = lane & 15;
+  if (wv < 4) {   // X_blk = sum_n [G_n; 1] (x) D_n: 2 x 2 tiles, K = 64 nodes
+    const int rl = (wv >> 1) * 16 + r16, kc = (wv & 1) * 16 + r16;
+    const bool rv = rl <= H, cv = kc < H;
     const f4v c = mfma_tile16_p(rv ? Gt + rl : kzh, rv ? HP : 0, cv ? res + kc : kzh,
                                 cv ? HP : 0, TN, lane);
     if (cv)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int rr = (tq >> 1) * 16 + 4 * (lane >> 4) + j;
+        const int rr = (wv >> 1) * 16 + 4 * (lane >> 4) + j;
         if (rr < H) X[rr * H + kc] = c[j];
+        else if (rr == H) sumD[kc] = c[j];
       }
-  }
-  if (threadIdx.x < H) {
-    const int k = threadIdx.x;
-    float sd = 0.f, y = 0.f;
-    for (int n = 0; n < TN; ++n) {
-      sd += res[n * HP + k];
-      if (z == 0) y += yres[n * HP + k];
+    if (z == 0) {   // ysum[k] = sum_n yres[n][k]: units 5 wv .. 5 wv + 4, one wave sum each
+#pragma unroll
+      for (int q = 0; q < H / 4; ++q) {
+        const int k = (H / 4) * wv + q;
+        const float v = wsum(yres[lane * HP + k]);
+        if (lane == 0) ysum[k] = v;
+      }
+    } else if (lane < H / 4) {
+      ysum[(H / 4) * wv + lane] = 0.f;
     }
-    sumD[k] = sd;
-    ysum[k] = y;
+  } else {        // dG_n[l] = sum_k D_n[k] M[l][k]: 4 x 2 tiles, K = 20, two per wave
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tl = 2 * (wv - 4) + u, n0 = (tl >> 1) * 16, lc = (tl & 1) * 16 + r16;
+      const bool cv = lc < H;
+      const f4v c = mfma_tile16_p(res + (n0 + r16) * HP, 1, cv ? Ml + lc * H : kzh, cv ? 1 : 0,
+                                  H, lane);
+      if (cv)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + 4 * (lane >> 4) + j;
+          if (t0 + n < Nc) gout[(t0 + n) * H + lc] = c[j];
+        }
+    }
   }
   __syncthreads();
   const int row = (b * tc + tile) * 2 + z;
   const float Nc1 = (float)(Nc - 1);
   const Seg& s2 = sg.s[SG_CLSB_H2];
   const Seg& s1 = sg.s[SG_CLSB_H1];
-  for (int e = threadIdx.x; e < 2 * H * H + 3 * H; e += blockDim.x) {
-    if (e < H * H) {              // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]
-      const int m = e / H, k = e - m * H;
-      float a = Nc1 * c2[m] * sumD[k];
-      for (int l = 0; l < H; ++l) a = fmaf(V2[l * H + m], X[l * H + k], a);
-      put(part, s2, (2 + m) * H + k, row, a);
-    } else if (e < 2 * H * H) {   // dV2[l][m] = sum_k X[l][k] U1e[m][k]
-      const int f = e - H * H, l = f / H, m = f - l * H;
-      float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(X[l * H + k], U1e[m * H + k], a);
-      put(part, s1, f, row, a);
-    } else if (e < 2 * H * H + H) {   // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
-      const int m = e - 2 * H * H;
-      float a = 0.f;
-      for (int k = 0; k < H; ++k) a = fmaf(U1e[m * H + k], sumD[k], a);
-      put(part, s1, H * H + m, row, Nc1 * a);
-    } else {                      // dU1[0], dU1[1], dd1 (row pass only)
-      const int f = e - 2 * H * H - H;   // 0 .. 2H-1
-      const int k = f % H;
-      const float dd1 = z == 0 ? sumD[k] : 0.f;
-      const float dy1 = z == 0 ? D[D_CV + k] * ysum[k] : 0.f;
-      if (f < H) {
-        put(part, s2, k, row, dd1 - dy1);
-        put(part, s2, H + k, row, dy1);
-      } else {
-        put(part, s2, 22 * H + k, row, dd1);
+  if (wv < 4) {   // dU1e[m][k] = sum_l V2[l][m] X[l][k] + (Nc-1) c2[m] sumD[k]: 2 x 2 tiles
+    const int m0 = (wv >> 1) * 16, kc = (wv & 1) * 16 + r16, mr = m0 + r16;
+    const bool mv = mr < H, cv = kc < H;
+    const f4v c = mfma_tile16_p(mv ? V2 + mr : kzh, mv ? H : 0, cv ? X + kc : kzh, cv ? H : 0, H,
+                                lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + 4 * (lane >> 4) + j;
+        if (m < H) put(part, s2, (2 + m) * H + kc, row, fmaf(Nc1 * c2[m], sumD[kc], c[j]));
       }
-    }
+  } else {        // dV2[l][m] = sum_k X[l][k] U1e[m][k]: 2 x 2 tiles
+    const int tl = wv - 4, l0 = (tl >> 1) * 16, mc = (tl & 1) * 16 + r16, lr = l0 + r16;
+    const bool lv = lr < H, cv = mc < H;
+    const f4v c = mfma_tile16_p(lv ? X + lr * H : kzh, lv ? 1 : 0, cv ? U1e + mc * H : kzh,
+                                cv ? 1 : 0, H, lane);
+    if (cv)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int l = l0 + 4 * (lane >> 4) + j;
+        if (l < H) put(part, s1, l * H + mc, row, c[j]);
+      }
+  }
+  if (threadIdx.x < H) {            // dc2[m] = (Nc-1) sum_k U1e[m][k] sumD[k]
+    const int m = threadIdx.x;
+    float a = 0.f;
+    for (int k = 0; k < H; ++k) a = fmaf(U1e[m * H + k], sumD[k], a);
+    put(part, s1, H * H + m, row, Nc1 * a);
+  } else if (threadIdx.x >= 64 && threadIdx.x < 64 + H) {   // dU1[0], dU1[1], dd1 (row pass)
+    const int k = threadIdx.x - 64;
+    const float dd1 = z == 0 ? sumD[k] : 0.f;
+    const float dy1 = z == 0 ? D[D_CV + k] * ysum[k] : 0.f;
+    put(part, s2, k, row, dd1 - dy1);
+    put(part, s2, H + k, row, dy1);
+    put(part, s2, 22 * H + k, row, dd1);
   }
 }
 
@@ -3168,7 +3192,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       const bool ok = j0 < Ne;
       const int j = ok ? j0 : 0;
       const float vm = ok ? 1.f : 0.f;
-      const float xj = xb[j];
+      const float xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
       const float* qj = rbb + (size_t)j * H + g * KPW;
       const f2 xx = {xj, xj};
 #pragma unroll
