@@ -1981,16 +1981,21 @@ __host__ __device__ inline size_t hsort_tab(int b, int side, int k, int len) {
 }
 
 // XCD-aware block map of a (T, B, 2) grid: blocks are dealt to the 8 XCDs round robin by
-// linear id, so the blocks of commit b all land on XCD b % 8 when B % 8 == 0 -- the sorted
-// tables one kernel writes are then read by the next from the same L2 (else identity)
+// linear id, so the blocks of commit b all land on XCD b % 8 (the last B % 8 commits' blocks
+// in id order) -- the sorted tables one kernel writes are then read by the next from the
+// same L2
 __device__ __forceinline__ void xcd_commit_map(int& t, int& b, int& z) {
-  const int T = gridDim.x, B = gridDim.y;
-  if (B & 7) {
-    t = blockIdx.x; b = blockIdx.y; z = blockIdx.z;
+  const int T = gridDim.x, B = gridDim.y, Z = gridDim.z;
+  const int L = blockIdx.x + T * (blockIdx.y + B * blockIdx.z);
+  const int Bq = B & ~7, per = Z * T;              // commits [0, Bq): commit b on XCD b % 8
+  if (L >= per * Bq) {                              // the last B % 8 commits: in id order
+    const int r = L - per * Bq, rem = r % per;
+    b = Bq + r / per;
+    z = rem / T;
+    t = rem - z * T;
     return;
   }
-  const int L = blockIdx.x + T * (blockIdx.y + B * blockIdx.z);
-  const int s = L >> 3, per = 2 * T, bq = s / per, r = s - bq * per;
+  const int s = L >> 3, bq = s / per, r = s - bq * per;
   b = 8 * bq + (L & 7);
   z = r / T;
   t = r - z * T;
@@ -3045,7 +3050,11 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
                                               double* __restrict__ tab) {
   __shared__ double c1[NT], c2[NT];
   const GenPrep GP = gen_prep(Ne, Nc);
-  const int k = blockIdx.x, b = blockIdx.y, mode = mode0 + blockIdx.z, t = threadIdx.x;
+  // the 20 unit blocks of commit b on one XCD (B % 8 == 0): the commit's rho / phi rows and
+  // sorted tables are fetched into that L2 once instead of once per unit from every XCD
+  int k, b, zz;
+  xcd_commit_map(k, b, zz);
+  const int mode = mode0 + zz, t = threadIdx.x;
   const int B = gridDim.y;
   const uint32_t* pp = prep + (size_t)b * GP.words;
   const float* xsrt = reinterpret_cast<const float*>(pp + GP.xsrt);
@@ -3101,10 +3110,10 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
                                                const float* __restrict__ rb,
                                                const double* __restrict__ tab,
                                                float* __restrict__ part, const Segs& sg,
-                                               float* hand) {
+                                               float* hand, const int tx, const int b) {
 #pragma clang fp contract(off)
   const GenPrep GP = gen_prep(Ne, Nc);
-  const int b = blockIdx.y, t0 = blockIdx.x * TN, te = gridDim.x, B = gridDim.y;
+  const int t0 = tx * TN, te = gridDim.x, B = gridDim.y;
   // 8 waves: wave g + 4 hw takes hidden units g; the halves hw split each lane's neighbour
   // list (hw 1 hands its partial sums over through LDS), hw 0 also does the dense part
   const int lane = threadIdx.x & 63, g = uni((threadIdx.x >> 6) & 3), hw = uni(threadIdx.x >> 8);
@@ -3249,7 +3258,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     v[2 * KPW + kk] = s2;
     v[3 * KPW + kk] = live ? S3[kk] : 0.f;
   }
-  const int row = b * te + blockIdx.x;
+  const int row = b * te + tx;
 #pragma unroll
   for (int q = 0; q < 4 * KPW; ++q) v[q] = wsum(v[q]);
   if (lane == 0) {
@@ -3287,10 +3296,12 @@ __global__ __launch_bounds__(NTP) void kw_first_bwd(const float* __restrict__ x,
                                                    const double* __restrict__ tab,
                                                    float* __restrict__ part, Segs sg) {
   __shared__ float hand[NW * 3 * KPW * TN];        // hw 1's walk sums [g][3 KPW][lane]
-  if (mode0 + (int)blockIdx.z == 0)
-    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg, hand);
+  int tx, b, zz;                                   // commit b's tiles on XCD b % 8, as kw_scan's
+  xcd_commit_map(tx, b, zz);                       // blocks that wrote its tables
+  if (mode0 + zz == 0)
+    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg, hand, tx, b);
   else
-    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg, hand);
+    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg, hand, tx, b);
 }
 
 // ---------------------------------------------------------------------------------
