@@ -1428,8 +1428,11 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
     const uint32_t* __restrict__ yT, const float* __restrict__ W, Off o,
     const float* __restrict__ D, int Nc, const float* __restrict__ sig,
     const float* __restrict__ tau, float* __restrict__ probs, float* __restrict__ logits,
-    float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg) {
+    float* __restrict__ gam, float ce_scale, float* __restrict__ part, Segs sg,
+    const int gam_out) {
 #pragma clang fp contract(off)
+  // gam_out = 0: gamma is not stored -- kw_hunk_clsb rebuilds it from the stored p1
+  // (probs) and y, the same float ops on the same bits
   // sigma rows | 4 pad words | sigma + eps (the y = 1 rows): a lane's row is picked by its
   // y bit, and the pad puts the two tables' rows on different banks (the b128 reads of a
   // wave hit two addresses, else 2-way conflicts: the tables are 2560 words apart)
@@ -1525,12 +1528,12 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
         corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
         if constexpr (TRAIN) {
           const float g = ce_scale * (p1 - yf);
-          gam[((size_t)b * Nc + p) * Nc + q] = g;
+          if (gam_out) gam[((size_t)b * Nc + p) * Nc + q] = g;
           gs += g;
 #pragma unroll
           for (int kk = 0; kk < H2; ++kk) za[kk] = fma2(kap[kk], (f2){g, g}, za[kk]);
         }
-      } else if (TRAIN && live) {
+      } else if (TRAIN && live && gam_out) {
         gam[((size_t)b * Nc + p) * Nc + q] = 0.f;   // defined diagonal, read by the passes
       }
     }
@@ -1683,6 +1686,9 @@ __device__ __forceinline__ void clsb_epilogue(
 //   global loads, no index division).
 // ---------------------------------------------------------------------------------
 constexpr int GTP = CHM + 1;   // gamma tile pitch
+#ifndef HDG_GAM_FROM_PROBS    // training steps that write probs: kw_hunk_clsb rebuilds gamma
+#define HDG_GAM_FROM_PROBS 1  // from them (kw_hunk_cls stores no gamma)
+#endif
 #ifndef HDG_CLSB_CTILE        // kw_hunk_clsb column pass: gamma staged through LDS (1) or
 #define HDG_CLSB_CTILE 1      // read from global memory per swept row (0)
 #endif
@@ -1693,7 +1699,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
     const float* __restrict__ sig, const float* __restrict__ tau, const float* __restrict__ gam,
     const float* __restrict__ G, const float* __restrict__ Hh, float* __restrict__ Dsig,
     float* __restrict__ Dtau, float* __restrict__ dG, float* __restrict__ dH,
-    float* __restrict__ part, Segs sg) {
+    float* __restrict__ part, Segs sg, const float* __restrict__ probs, const float ce_scale) {
 #pragma clang fp contract(off)
   // the swept rows and the gamma tile are dead once the sweep ends: combine8's buffer
   // overlays them (76 KB of LDS: two blocks per CU)
@@ -1720,6 +1726,19 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   const float* oth = (z ? sig : tau) + (size_t)b * Nc * H;
   const uint32_t* brow = (z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC;
   const float* gb = gam + (size_t)b * Nc * Nc;
+  // probs != NULL (kw_hunk_cls stored no gamma): gamma_pq = ce_scale (p1_pq - y_pq) from the
+  // stored p1 (off-diagonal layout, model_2.py:321) and the y bits, 0 on the diagonal --
+  // the forward's float ops on its bits
+  const size_t Pc = (size_t)Nc * (Nc - 1);
+  const float* p1b = probs ? probs + (size_t)b * 2 * Pc + Pc : nullptr;
+  const uint32_t* ybb = ybits + (size_t)b * Nc * WC;
+  auto gamma_at = [&](const int r, const int q) -> float {   // r, q < Nc
+    if (!p1b) return gb[(size_t)r * Nc + q];
+    if (q == r) return 0.f;
+    const float p1 = p1b[(size_t)r * (Nc - 1) + q - (q > r ? 1 : 0)];
+    const float yf = ((ybb[r * WC + (q >> 5)] >> (q & 31)) & 1u) ? 1.f : 0.f;
+    return ce_scale * (p1 - yf);
+  };
   f2 ow[H2], acc[H2], ya[H2];
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
@@ -1744,15 +1763,15 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
       const int cg = c0 + tc4;
 #pragma unroll
       for (int i = 0; i < TN / 16; ++i) {
-        const int r = t0 + tr + 16 * i;
-        const float* src = gb + (size_t)(r < Nc ? r : Nc - 1) * Nc;
-        if (al4 && cg + 3 < c1) {
+        const int r = t0 + tr + 16 * i, rc = r < Nc ? r : Nc - 1;
+        const float* src = gb + (size_t)rc * Nc;
+        if (!p1b && al4 && cg + 3 < c1) {
           gv[i] = *reinterpret_cast<const float4*>(src + cg);
         } else {
-          gv[i].x = cg < c1 ? src[cg] : 0.f;
-          gv[i].y = cg + 1 < c1 ? src[cg + 1] : 0.f;
-          gv[i].z = cg + 2 < c1 ? src[cg + 2] : 0.f;
-          gv[i].w = cg + 3 < c1 ? src[cg + 3] : 0.f;
+          gv[i].x = cg < c1 ? gamma_at(rc, cg) : 0.f;
+          gv[i].y = cg + 1 < c1 ? gamma_at(rc, cg + 1) : 0.f;
+          gv[i].z = cg + 2 < c1 ? gamma_at(rc, cg + 2) : 0.f;
+          gv[i].w = cg + 3 < c1 ? gamma_at(rc, cg + 3) : 0.f;
         }
       }
 #pragma unroll
@@ -1775,15 +1794,15 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
       const int rr = threadIdx.x >> 4, cc4 = (threadIdx.x & 15) * 4, cg = t0 + cc4;
 #pragma unroll
       for (int i = 0; i < CHM * TN / (4 * NTP); ++i) {
-        const int r = c0 + rr + (NTP / 16) * i;
-        const float* src = gb + (size_t)(r < c1 ? r : c1 - 1) * Nc;
-        if (al4 && cg + 3 < Nc) {
+        const int r = c0 + rr + (NTP / 16) * i, rc = r < c1 ? r : c1 - 1;
+        const float* src = gb + (size_t)rc * Nc;
+        if (!p1b && al4 && cg + 3 < Nc) {
           gv[i] = *reinterpret_cast<const float4*>(src + cg);
         } else {
-          gv[i].x = cg < Nc ? src[cg] : 0.f;
-          gv[i].y = cg + 1 < Nc ? src[cg + 1] : 0.f;
-          gv[i].z = cg + 2 < Nc ? src[cg + 2] : 0.f;
-          gv[i].w = cg + 3 < Nc ? src[cg + 3] : 0.f;
+          gv[i].x = cg < Nc ? gamma_at(rc, cg) : 0.f;
+          gv[i].y = cg + 1 < Nc ? gamma_at(rc, cg + 1) : 0.f;
+          gv[i].z = cg + 2 < Nc ? gamma_at(rc, cg + 2) : 0.f;
+          gv[i].w = cg + 3 < Nc ? gamma_at(rc, cg + 3) : 0.f;
         }
       }
 #pragma unroll
@@ -1805,7 +1824,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
         if ((m >> 5) != wi) { wi = m >> 5; word = brow[wi]; }
         const bool y1 = (word >> (m & 31)) & 1u;
         const float g = ROW ? gt[lane * GTP + (m - c0)]
-                            : (HDG_CLSB_CTILE ? gt[(m - c0) * TN + lane] : gb[(size_t)m * Nc + ncl]);
+                            : (HDG_CLSB_CTILE ? gt[(m - c0) * TN + lane] : gamma_at(m, ncl));
         const f2 g2 = {g, g}, gy2 = y1 ? g2 : (f2){0.f, 0.f};
         // [kappa > 0] g and [kappa > 0] y g as one fma each (the products are exact)
         const float4* o4 = reinterpret_cast<const float4*>((y1 ? ose : os_) + (m - c0) * H);
@@ -4498,7 +4517,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   if (!train) {
     hipLaunchKernelGGL(kw_hunk_cls<false>, dim3(tc, B, CLS_SPLIT), dim3(NTP), 0, st, yT, params,
                        o, D,
-                       Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
+                       Nc, F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs, 0);
     WTRY(kmark("kw_hunk_cls", st));
     if (ce_sum) {
       hipLaunchKernelGGL(kw_grad_reduce, dim3(1), dim3(64), 0, st, part, w.segs, o.NP, o.NP,
@@ -4510,9 +4529,13 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
     return 0;
   }
+  // the two-pass classifier backward rebuilds gamma from the probabilities when the step
+  // writes them (a training sess.run fetches C_edge_output2): 4 B per pair not stored
+  const float* gprobs = (!ht && HDG_GAM_FROM_PROBS) ? probs : nullptr;
   hipLaunchKernelGGL(kw_hunk_cls<true>, dim3(tc, B, CLS_SPLIT), dim3(NTP), 0, st, yT, params,
                      o, D, Nc,
-                     F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs);
+                     F(w.sig), F(w.tau), probs, logits, F(w.gam), ce_scale, part, w.segs,
+                     gprobs ? 0 : 1);
   WTRY(kmark("kw_hunk_cls", st));
   if (ht) {
     HTileArgs ha{Nc, F(w.sig), F(w.tau), nullptr, nullptr, F(w.gam), D + D_EPS, bt->ybits,
@@ -4524,7 +4547,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   } else {
     hipLaunchKernelGGL(kw_hunk_clsb, dim3(tc, B, 2), dim3(NTP), 0, st, bt->ybits, yT, params, o,
                        D, Nc, F(w.sig), F(w.tau), F(w.gam), F(w.G), F(w.Hh), F(w.Dsig),
-                       F(w.Dtau), F(w.dG), F(w.dH), part, w.segs);
+                       F(w.Dtau), F(w.dG), F(w.dH), part, w.segs, gprobs, ce_scale);
     WTRY(kmark("kw_hunk_clsb", st));
   }
   if (hs) {
