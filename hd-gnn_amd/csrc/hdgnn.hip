@@ -278,6 +278,22 @@ __device__ __forceinline__ f2 step2(f2 z) {
   return r;
 }
 
+// [x + c > 0] for a packed pair in ONE op where only the step of the sum is used (the
+// backward passes' masks): clamp(fma(x, 2^64, c 2^64)).  The fma rounds the exact
+// (x + c) 2^64 once: 0 for x + c <= 0 (-0, NaN: 0), 1 for every x + c >= 2^-64, so it
+// differs from step2(fl(x + c)) only for 0 < x + c < 2^-64.  cs = c 2^64 (exact and finite
+// for |c| < 2^63; PADNEG 2^64 = -inf masks the pair).
+#ifndef HDG_STEPF
+#define HDG_STEPF 1
+#endif
+constexpr float STEP_S = 0x1p64f;
+__device__ __forceinline__ f2 stepf2(f2 x, f2 cs) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 clamp"
+      : "=v"(r) : "v"(x), "s"((f2){STEP_S, STEP_S}), "v"(cs));
+  return r;
+}
+
 // q = r / d, rem = r % d for 0 <= r < 2^22, 1 <= d < 2^12: float estimate + one select
 // correction, 24-bit multiplies, no branches (keeps unrolled loads in flight)
 __device__ __forceinline__ void divmod_bf(int r, int d, float inv, int& q, int& rem) {
@@ -470,6 +486,7 @@ __device__ __forceinline__ void pair_tile(
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
       a2[p] += addm2;
+      if constexpr (MODE != 0 && HDG_STEPF) a2[p] *= (p2){STEP_S, STEP_S};   // stepf2's c
       if constexpr (MODE == 1)
         rw2[p] *= mulm2;
       else
@@ -507,7 +524,8 @@ __device__ __forceinline__ void pair_tile(
         p2 bb;
         if constexpr (HB) bb = bcol[c][p];
         else bb = bbv[p];
-        const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
+        const p2 zb = __builtin_elementwise_fma(af2, dk2[p], bb);
+        const p2 z = a2[p] + zb;          // used by MODE 0 (MODE 1, 2: stepf2(zb, a 2^64))
         if constexpr (MODE == 0) {
           // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
           // max on gfx950: relu was two scalar v_max plus two packed adds)
@@ -517,7 +535,7 @@ __device__ __forceinline__ void pair_tile(
         } else if constexpr (MODE == 2) {
           // w = g is one value per pair: [z > 0] g and [z > 0] a g as one fma each (the
           // products are exact: the same bits as multiply, then add)
-          const p2 sz = step2(z), g2 = {g, g}, gy2 = {gy, gy};
+          const p2 sz = HDG_STEPF ? stepf2(zb, a2[p]) : step2(z), g2 = {g, g}, gy2 = {gy, gy};
           yacc2[p] = __builtin_elementwise_fma(sz, gy2, yacc2[p]);
           racc2[p] = __builtin_elementwise_fma(sz, g2, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(sz, g2, cacc2[c][p]);
@@ -525,7 +543,7 @@ __device__ __forceinline__ void pair_tile(
           p2 w;
           if constexpr (HW) w = rw2[p] + wcol[c][p];
           else w = rw2[p] + wcv[p];
-          const p2 e = step2(z) * w;
+          const p2 e = (HDG_STEPF ? stepf2(zb, a2[p]) : step2(z)) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;
           cacc2[c][p] += e;
@@ -680,6 +698,7 @@ __device__ __forceinline__ void pair_tile32(
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
       a2[p] += addm2;
+      if constexpr (MODE != 0 && HDG_STEPF) a2[p] *= (p2){STEP_S, STEP_S};   // stepf2's c
       if constexpr (MODE == 1)
         rw2[p] *= mulm2;
       else
@@ -715,7 +734,8 @@ __device__ __forceinline__ void pair_tile32(
 #pragma unroll
       for (int p = 0; p < KP; ++p) {
         const p2 bb = bbv[p];
-        const p2 z = a2[p] + __builtin_elementwise_fma(af2, dk2[p], bb);
+        const p2 zb = __builtin_elementwise_fma(af2, dk2[p], bb);
+        const p2 z = a2[p] + zb;          // used by MODE 0 (MODE 1, 2: stepf2(zb, a 2^64))
         if constexpr (MODE == 0) {
           // relu(z) accumulated as z [z > 0]: one packed step and two packed fma (no packed
           // max on gfx950: relu was two scalar v_max plus two packed adds)
@@ -723,13 +743,13 @@ __device__ __forceinline__ void pair_tile32(
           racc2[p] = __builtin_elementwise_fma(z, sz, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(z, sz, cacc2[c][p]);
         } else if constexpr (MODE == 2) {   // as pair_tile: one exact fma per sum
-          const p2 sz = step2(z), g2 = {g, g}, gy2 = {gy, gy};
+          const p2 sz = HDG_STEPF ? stepf2(zb, a2[p]) : step2(z), g2 = {g, g}, gy2 = {gy, gy};
           yacc2[p] = __builtin_elementwise_fma(sz, gy2, yacc2[p]);
           racc2[p] = __builtin_elementwise_fma(sz, g2, racc2[p]);
           cacc2[c][p] = __builtin_elementwise_fma(sz, g2, cacc2[c][p]);
         } else {
           const p2 w = rw2[p] + wcv[p];
-          const p2 e = step2(z) * w;
+          const p2 e = (HDG_STEPF ? stepf2(zb, a2[p]) : step2(z)) * w;
           yacc2[p] = __builtin_elementwise_fma(af2, e, yacc2[p]);
           racc2[p] += e;
           cacc2[c][p] += e;

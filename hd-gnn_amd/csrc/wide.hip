@@ -512,6 +512,21 @@ __device__ __forceinline__ f2 step2(f2 z) {
   return r;
 }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// [x + c > 0] for a packed pair in ONE op where only the step of the sum is used (not the
+// sum): clamp(fma(x, 2^64, c 2^64)).  The fma rounds the exact (x + c) 2^64 once, so the
+// result is 0 for x + c <= 0 (-0, NaN: 0) and 1 for every x + c >= 2^-64; it differs from
+// step2(fl(x + c)) only for 0 < x + c < 2^-64.  cs = c 2^64 (exact and finite for |c| <
+// 2^63; -inf masks the pair).
+#ifndef HDG_STEPF
+#define HDG_STEPF 1
+#endif
+constexpr float STEP_S = 0x1p64f;
+__device__ __forceinline__ f2 stepf2(f2 x, f2 cs) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 clamp"
+      : "=v"(r) : "v"(x), "s"((f2){STEP_S, STEP_S}), "v"(cs));
+  return r;
+}
 __device__ __forceinline__ f2 ld2(const float* p) { return (f2){p[0], p[1]}; }
 
 // rows [c0, c1) of a [N][H] array -> LDS (float4 copies; rows are 80 B, 16-B aligned)
@@ -1686,9 +1701,9 @@ __device__ __forceinline__ void clsb_epilogue(
 //   global loads, no index division).
 // ---------------------------------------------------------------------------------
 constexpr int GTP = CHM + 1;   // gamma tile pitch
-#ifndef HDG_GAM_FROM_PROBS    // training steps that write probs: kw_hunk_clsb rebuilds gamma
-#define HDG_GAM_FROM_PROBS 1  // from them (kw_hunk_cls stores no gamma)
-#endif
+#ifndef HDG_GAM_FROM_PROBS    // 1: training steps that write probs have kw_hunk_clsb rebuild
+#define HDG_GAM_FROM_PROBS 0  // gamma from them, kw_hunk_cls storing none.  Measured at stress:
+#endif                        // cls 42.0 -> 40.2 us but clsb 49.3 -> 90.6 us (scalar staging)
 #ifndef HDG_CLSB_CTILE        // kw_hunk_clsb column pass: gamma staged through LDS (1) or
 #define HDG_CLSB_CTILE 1      // read from global memory per swept row (0)
 #endif
@@ -1743,6 +1758,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) {
     ow[kk] = ld2(own + ncl * H + 2 * kk);
+    if (HDG_STEPF) ow[kk] *= (f2){STEP_S, STEP_S};   // stepf2's c 2^64 (exact)
     acc[kk] = (f2){0.f, 0.f};
     ya[kk] = (f2){0.f, 0.f};
   }
@@ -1831,8 +1847,10 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int v = 0; v < H / 4; ++v) {
           const float4 q = o4[v];
-          const f2 sa = step2(ow[2 * v] + (f2){q.x, q.y});
-          const f2 sb = step2(ow[2 * v + 1] + (f2){q.z, q.w});
+          const f2 sa = HDG_STEPF ? stepf2((f2){q.x, q.y}, ow[2 * v])
+                                  : step2(ow[2 * v] + (f2){q.x, q.y});
+          const f2 sb = HDG_STEPF ? stepf2((f2){q.z, q.w}, ow[2 * v + 1])
+                                  : step2(ow[2 * v + 1] + (f2){q.z, q.w});
           acc[2 * v] = fma2(sa, g2, acc[2 * v]);   // gamma finite, 0 on the diagonal
           acc[2 * v + 1] = fma2(sb, g2, acc[2 * v + 1]);
           if constexpr (ROW) {
