@@ -512,6 +512,10 @@ __device__ __forceinline__ f2 step2(f2 z) {
   return r;
 }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// ln x for x in [1, 2] (the two-class CE's log(1 + e^-|d|) and log(e0 + e1)): v_log_f32
+// (log2, ~1 ulp, no denormal range to guard) times ln 2 -- 2 VALU ops where logf expands to
+// a denormal-scaled, split-constant sequence of ~11
+__device__ __forceinline__ float ln_1to2(float x) { return __builtin_amdgcn_logf(x) * 0.693147182f; }
 // [x + c > 0] for a packed pair in ONE op where only the step of the sum is used (not the
 // sum): clamp(fma(x, 2^64, c 2^64)).  The fma rounds the exact (x + c) 2^64 once, so the
 // result is 0 for x + c <= 0 (-0, NaN: 0) and 1 for every x + c >= 2^-64; it differs from
@@ -1471,6 +1475,17 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
 #pragma unroll
   for (int kk = 0; kk < H2; ++kk) tq[kk] = ld2(tau + ((size_t)b * Nc + qc) * H + 2 * kk);
   const f2 bb = ld2(W + o.H2_B2);
+  // the d form's classifier column c and the CE scale pinned in VGPRs: as uniform values
+  // the compiler re-issued their scalar loads every pair, each with an lgkmcnt(0) wait that
+  // also drained the pair's LDS reads
+  f2 cvr[H2];
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) {
+    cvr[kk] = ld2(D + D_CV + 2 * kk);
+    asm volatile("" : "+v"(cvr[kk]));
+  }
+  float ces = ce_scale;
+  asm volatile("" : "+v"(ces));
   float* prb = probs ? probs + (size_t)b * 2 * Pc : nullptr;
   float* lgb = logits ? logits + (size_t)b * 2 * Pc : nullptr;
   float ce = 0.f, gs = 0.f, corr = 0.f;
@@ -1517,7 +1532,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
         const float ssum = e0 + e1, inv = __builtin_amdgcn_rcpf(ssum);   // [1, 2]: 1-ulp rcp
         p0 = e0 * inv;
         p1 = e1 * inv;
-        cep = (__logf(ssum) + mx) - (yf > 0.f ? z1 : z0);
+        cep = (ln_1to2(ssum) + mx) - (yf > 0.f ? z1 : z0);
         if (live && q != p) {
           const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
           lgb[r] = z0;
@@ -1527,14 +1542,14 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
                    // fused kernel's M7: p1 = 1 / (1 + e^-d), CE = softplus(-+d)
         f2 dd = {bb.y - bb.x, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < H2; ++kk) dd = fma2(kap[kk], ld2(D + D_CV + 2 * kk), dd);
+        for (int kk = 0; kk < H2; ++kk) dd = fma2(kap[kk], cvr[kk], dd);
         const float d = dd.x + dd.y;
         const float ex = __expf(-fabsf(d));
         const float inv = __builtin_amdgcn_rcpf(1.f + ex);   // 1 + e in (1, 2]: 1-ulp rcp
         const float ps = ex * inv;
         p1 = d >= 0.f ? inv : ps;
         p0 = d >= 0.f ? ps : inv;
-        cep = __logf(1.f + ex) + relu(yf > 0.f ? -d : d);
+        cep = ln_1to2(1.f + ex) + relu(yf > 0.f ? -d : d);
       }
       if (live && q != p) {
         const int r = p * (Nc - 1) + q - (q > p ? 1 : 0);
@@ -1542,7 +1557,7 @@ __global__ __launch_bounds__(NTP) void kw_hunk_cls(
         ce += cep;
         corr += ((p1 > p0) == (yf > 0.f)) ? 1.f : 0.f;   // top_ACC: np.argmax, ties -> 0
         if constexpr (TRAIN) {
-          const float g = ce_scale * (p1 - yf);
+          const float g = ces * (p1 - yf);
           if (gam_out) gam[((size_t)b * Nc + p) * Nc + q] = g;
           gs += g;
 #pragma unroll
