@@ -1308,10 +1308,37 @@ __global__ __launch_bounds__(NT) void kw_cross_fwd(
   const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt) + (size_t)c * Ne;
   const float* xb = xv + (size_t)b * Ne;
   float a0 = 0.f, a1 = 0.f;
-  for (int I = lane; I < Ne; I += 64) {
-    const float xi = xb[I];
-    a0 = fmaf((float)ks[I], xi, a0);
-    a1 = fmaf((float)kt[I], xi, a1);
+  if ((Ne & 3) == 0) {   // rows 8-byte aligned: 4 nodes per lane and load, 4 trips in flight
+    constexpr int U = 4;
+    for (int I0 = 4 * lane; I0 < Ne; I0 += 256 * U) {
+      uint2 vs[U], vt[U];
+      float4 xx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int I = I0 + 256 * u < Ne ? I0 + 256 * u : I0;   // clamped load, value unused
+        vs[u] = *reinterpret_cast<const uint2*>(ks + I);
+        vt[u] = *reinterpret_cast<const uint2*>(kt + I);
+        xx[u] = *reinterpret_cast<const float4*>(xb + I);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (I0 + 256 * u >= Ne) break;
+        const float x4[4] = {xx[u].x, xx[u].y, xx[u].z, xx[u].w};
+        const uint32_t s4[4] = {vs[u].x & 0xffffu, vs[u].x >> 16, vs[u].y & 0xffffu, vs[u].y >> 16};
+        const uint32_t t4[4] = {vt[u].x & 0xffffu, vt[u].x >> 16, vt[u].y & 0xffffu, vt[u].y >> 16};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a0 = fmaf((float)s4[q], x4[q], a0);
+          a1 = fmaf((float)t4[q], x4[q], a1);
+        }
+      }
+    }
+  } else {
+    for (int I = lane; I < Ne; I += 64) {
+      const float xi = xb[I];
+      a0 = fmaf((float)ks[I], xi, a0);
+      a1 = fmaf((float)kt[I], xi, a1);
+    }
   }
   float nv[4];
   nv[0] = wsum(a0);
@@ -2960,6 +2987,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   const int lane = t & 63, w = t >> 6;
   const int I = t0 + lane;
   const uint32_t* pp = prep + (size_t)b * PL.words;
+  WSTAMP(12, 0);
   stage_w(Wl, W + o.E3_W1, 461);
   stage_w(Wl + 464, W + o.E1_W5, 400);
   {
@@ -3008,6 +3036,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     }
     dxq[w * TN + lane] = a;
   }
+  WSTAMP(12, 1);
   const size_t base = ((size_t)b * Ne + t0) * H;
   for (int e = t; e < TN * H; e += NT) {
     const int n = e / H, k = e - n * H;
@@ -3030,11 +3059,13 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   }
   __syncthreads();
   // dE = dq W1'[1:]^T, rho_E = dE W5^T as MFMA tiles (transposed weights: SM = 1, SK = H)
+  WSTAMP(12, 2);
   rows_x_w<1, H>(dq, W1e + H, kzr, [&](int n, int m, float c) { dE[n * HP + m] = c; });
   __syncthreads();
   rows_x_w<1, H>(dE, W5, kzr, [&](int n, int l, float c) {
     if (t0 + n < Ne) rhoE[base + n * H + l] = c;
   });
+  WSTAMP(12, 3);
   const int row = b * te + blockIdx.x;
   const Seg& s3 = sg.s[SG_E3];
   const Seg& s5 = sg.s[SG_E1W5];
@@ -3082,6 +3113,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
       put(part, s5, f, row, a);
     }
   }
+  WSTAMP(12, 4);
 }
 
 // ---------------------------------------------------------------------------------
@@ -3173,7 +3205,9 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
+  WSTAMP(13, 0);
   const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
+  WSTAMP(13, 1);
   const float* xb = T.xs;
   const float xi = xb[ic];
   const float* rbb = rb + (size_t)b * Ne * H;
@@ -3234,6 +3268,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
   float cs[KPW];                                  // sum of the corrections' dm
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) cs[kk] = 0.f;
+  WSTAMP(13, 2);
   if (live) {   // units (0,1), (2,3) as packed pairs, unit 4 scalar; [z > 0] g as step2(z) g
     static_assert(KPW == 5, "packed correction layout");
     f2 u2[2], wb2[2], dd2[2], ri2[2], cs2[2], s12[2], s32[2];
@@ -3284,6 +3319,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     }
     cs[4] = cst; S1[4] = s1t; S3[4] = s3t;
   }
+  WSTAMP(13, 3);
   float* hd = hand + g * 3 * KPW * TN + lane;     // hw 1's sums, added in a fixed order
   if (hw) {
 #pragma unroll
@@ -3294,6 +3330,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     }
   }
   __syncthreads();
+  WSTAMP(13, 4);
   if (hw) return;                                 // no barriers below
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
