@@ -75,6 +75,9 @@ __device__ unsigned long long* g_wst;
 #else
 #define WSTAMP(kid, k) do {} while (0)
 #endif
+#ifndef HDG_ABL_DX    // ablation builds only: kw_node_bwd's count-phase loads (1 counts, 2 dn)
+#define HDG_ABL_DX 0
+#endif
 #ifndef HDG_ABL_XJ    // ablation builds only: neighbour x reads at conflict-free addresses
 #define HDG_ABL_XJ 0  // (wrong sums; for timing the LDS gathers of the walks)
 #endif
@@ -2977,6 +2980,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     const float* __restrict__ P, const float* __restrict__ Eb, const float* __restrict__ hE,
     float* __restrict__ rhoE, float* __restrict__ part, Segs sg) {
   __shared__ float dxq[NW * TN], xs[TN], dov[TN];
+  __shared__ float2 dnl[HS_NC_MAX];               // (dn_c[0], dn_c[1]) of the commit
   __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
   __shared__ float Wl[864];
   __shared__ float kzr[1];                        // 0.f: stride-0 operand of padding tiles
@@ -2988,12 +2992,36 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   const int I = t0 + lane;
   const uint32_t* pp = prep + (size_t)b * PL.words;
   WSTAMP(12, 0);
+  // the tile's P / E_bar / h rows and its ov / x values are loaded first (registers), so their
+  // latency hides behind the count loop instead of costing two round trips after it
+  constexpr int NPE = TN * H / NT;
+  static_assert(TN * H % NT == 0, "kw_node_bwd row staging");
+  const size_t base = ((size_t)b * Ne + t0) * H;
+  float pv[NPE], ev[NPE], hv[NPE];
+#pragma unroll
+  for (int it = 0; it < NPE; ++it) {
+    const int e = t + it * NT, n = e / H;
+    const size_t a = t0 + n < Ne ? base + e : base;           // clamped load, value dropped
+    pv[it] = P[a];
+    ev[it] = Eb[a];
+    hv[it] = hE[a];
+  }
+  const int tnode = t0 + (t < TN ? t : 0) < Ne ? t0 + (t < TN ? t : 0) : Ne - 1;
+  const float ovt = ov[(size_t)b * Ne + tnode], xt = x[(size_t)b * Ne + tnode];
   stage_w(Wl, W + o.E3_W1, 461);
   stage_w(Wl + 464, W + o.E1_W5, 400);
+  // the commit's (dn_c[0], dn_c[1]) in LDS: the count loop's per-hunk factors are the same
+  // for every lane, and as scalar loads (one s_load and lgkmcnt wait per hunk pair) they
+  // cost a third of the loop (wave stamps: 16.9 -> 11.9 us without them at stress)
+  {
+    const float* dnb = dn + (size_t)b * Nc * 4;
+    for (int c = t; c < Nc; c += NT) dnl[c] = *reinterpret_cast<const float2*>(dnb + 4 * c);
+  }
+  __syncthreads();
+  WSTAMP(12, 1);
   {
     const uint16_t* ks = reinterpret_cast<const uint16_t*>(pp + PL.ks);
     const uint16_t* kt = reinterpret_cast<const uint16_t*>(pp + PL.kt);
-    const float* dnb = dn + (size_t)b * Nc * 4;
     const int c0 = (Nc * w) / NW, c1 = (Nc * (w + 1)) / NW;
     float a = 0.f;
     if (I < Ne) {                  // NB_U hunks' counts in flight per step, same fma order
@@ -3003,10 +3031,21 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
         float vs[NB_U], vt[NB_U], d0[NB_U], d1[NB_U];
 #pragma unroll
         for (int u = 0; u < NB_U; ++u) {
-          vs[u] = (float)ks[(size_t)(c + u) * Ne + I];
-          vt[u] = (float)kt[(size_t)(c + u) * Ne + I];
-          d0[u] = dnb[4 * (c + u)];
-          d1[u] = dnb[4 * (c + u) + 1];
+          if (HDG_ABL_DX & 1) {      // ablation builds only (wrong sums): no count loads
+            vs[u] = (float)((c + u + I) & 3);
+            vt[u] = (float)((c + u + I) & 1);
+          } else {
+            vs[u] = (float)ks[(size_t)(c + u) * Ne + I];
+            vt[u] = (float)kt[(size_t)(c + u) * Ne + I];
+          }
+          if (HDG_ABL_DX & 2) {      // ... no dn loads
+            d0[u] = (float)(c + u);
+            d1[u] = (float)(c - u);
+          } else {
+            const float2 dv = dnl[c + u];
+            d0[u] = dv.x;
+            d1[u] = dv.y;
+          }
         }
 #pragma unroll
         for (int u = 0; u < NB_U; ++u) {
@@ -3020,8 +3059,8 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
         for (int u = 0; u < 4; ++u) {
           vs[u] = (float)ks[(size_t)(c + u) * Ne + I];
           vt[u] = (float)kt[(size_t)(c + u) * Ne + I];
-          d0[u] = dnb[4 * (c + u)];
-          d1[u] = dnb[4 * (c + u) + 1];
+          d0[u] = dnl[c + u].x;
+          d1[u] = dnl[c + u].y;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -3030,27 +3069,27 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
         }
       }
       for (; c < c1; ++c) {
-        a = fmaf(dnb[4 * c], (float)ks[(size_t)c * Ne + I], a);
-        a = fmaf(dnb[4 * c + 1], (float)kt[(size_t)c * Ne + I], a);
+        a = fmaf(dnl[c].x, (float)ks[(size_t)c * Ne + I], a);
+        a = fmaf(dnl[c].y, (float)kt[(size_t)c * Ne + I], a);
       }
     }
     dxq[w * TN + lane] = a;
   }
-  WSTAMP(12, 1);
-  const size_t base = ((size_t)b * Ne + t0) * H;
-  for (int e = t; e < TN * H; e += NT) {
-    const int n = e / H, k = e - n * H;
+  WSTAMP(12, 2);
+#pragma unroll
+  for (int it = 0; it < NPE; ++it) {
+    const int e = t + it * NT, n = e / H, k = e - n * H;
     const bool in = t0 + n < Ne;
-    Pt[n * HP + k] = in ? P[base + e] : 0.f;
-    Et[n * HP + k] = in ? Eb[base + e] : 0.f;
-    ht[n * HP + k] = in ? hE[base + e] : 0.f;
+    Pt[n * HP + k] = in ? pv[it] : 0.f;
+    Et[n * HP + k] = in ? ev[it] : 0.f;
+    ht[n * HP + k] = in ? hv[it] : 0.f;
   }
   __syncthreads();
   if (t < TN) {
     const bool in = t0 + t < Ne;
     const float d = ((dxq[t] + dxq[TN + t]) + dxq[2 * TN + t]) + dxq[3 * TN + t];
-    dov[t] = (in && ov[(size_t)b * Ne + t0 + t] > 0.f) ? d : 0.f;
-    xs[t] = in ? x[(size_t)b * Ne + t0 + t] : 0.f;
+    dov[t] = (in && ovt > 0.f) ? d : 0.f;
+    xs[t] = in ? xt : 0.f;
   }
   __syncthreads();
   for (int e = t; e < TN * H; e += NT) {
@@ -3059,13 +3098,13 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   }
   __syncthreads();
   // dE = dq W1'[1:]^T, rho_E = dE W5^T as MFMA tiles (transposed weights: SM = 1, SK = H)
-  WSTAMP(12, 2);
+  WSTAMP(12, 3);
   rows_x_w<1, H>(dq, W1e + H, kzr, [&](int n, int m, float c) { dE[n * HP + m] = c; });
   __syncthreads();
   rows_x_w<1, H>(dE, W5, kzr, [&](int n, int l, float c) {
     if (t0 + n < Ne) rhoE[base + n * H + l] = c;
   });
-  WSTAMP(12, 3);
+  WSTAMP(12, 4);
   const int row = b * te + blockIdx.x;
   const Seg& s3 = sg.s[SG_E3];
   const Seg& s5 = sg.s[SG_E1W5];
@@ -3113,7 +3152,7 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
       put(part, s5, f, row, a);
     }
   }
-  WSTAMP(12, 4);
+  WSTAMP(12, 5);
 }
 
 // ---------------------------------------------------------------------------------
