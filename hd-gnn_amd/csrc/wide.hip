@@ -75,6 +75,9 @@ __device__ unsigned long long* g_wst;
 #else
 #define WSTAMP(kid, k) do {} while (0)
 #endif
+#ifndef HDG_ABL_QJ    // ablation builds only: kw_first_bwd's neighbour rows read from the own
+#define HDG_ABL_QJ 0  // row (cache-hot, wrong sums)
+#endif
 #ifndef HDG_ABL_DX    // ablation builds only: kw_node_bwd's count-phase loads (1 counts, 2 dn)
 #define HDG_ABL_DX 0
 #endif
@@ -2459,11 +2462,12 @@ __device__ __forceinline__ void walk_row(const float* rows, int q, int g, float 
 // LB groups of four ids loaded before any is used
 template <int LB = HS_LB, class F>
 __device__ __forceinline__ void for_ylist(const uint32_t* __restrict__ prep, const ListLayout& Y,
-                                          size_t r, int Nc, F f) {
-  const int ng = ((int)prep[Y.cnt + r] + 3) >> 2;
+                                          size_t r, int Nc, F f, int part = 0, int nparts = 1) {
+  const int ngt = ((int)prep[Y.cnt + r] + 3) >> 2;
   const uint2* ids = reinterpret_cast<const uint2*>(
       reinterpret_cast<const uint16_t*>(prep + Y.ids) + r * list_stride(Nc));
-  for (int g0 = 0; g0 < ng; g0 += LB) {
+  const int ng = (ngt * (part + 1)) / nparts;    // this caller's share of the 4-id groups
+  for (int g0 = (ngt * part) / nparts; g0 < ng; g0 += LB) {
     uint2 q[LB];
 #pragma unroll
     for (int u = 0; u < LB; ++u) q[u] = ids[g0 + u < ng ? g0 + u : g0];
@@ -2497,24 +2501,31 @@ __device__ __forceinline__ void hs_search(const float* svl, int NcP, int Nc,
 }
 
 // The per-lane core of the forward sorted pass: node ncl's sums over the swept side for the
-// five units of group g: the dense part from the search and the f64 suffix table, the self
-// pair removed, the y = 1 pairs' relu(z1) replacing relu(z0) (the sentinel ids: a zero term)
+// five units of group g: the dense part from the search and the f64 suffix table (dsum), the
+// self pair removed, the y = 1 pairs' relu(z1) replacing relu(z0) (the sentinel ids: a zero
+// term) in acc.  part / nparts: this lane's share of the label list; part 0 alone does the
+// dense part and the self pair (the others' dsum and acc start at 0).  The node's sums are
+// dsum + the parts' acc summed in part order.
 template <int RS, int GS>
 __device__ __forceinline__ void fwd_s_lane(const float* svl, const float* rows, int NcP, int Nc,
                                            int b, int z, int g, int ncl, bool ys,
                                            const float (&ow)[KPW], const float (&dl)[KPW],
                                            const double* __restrict__ sx,
                                            const uint32_t* __restrict__ prep,
-                                           const ListLayout& Y, size_t yrow, float (&out)[KPW]) {
-  int m[KPW];
-  hs_search(svl, NcP, Nc, ow, m);
-  double dense[KPW];
-  float acc[KPW];
+                                           const ListLayout& Y, size_t yrow, float (&dsum)[KPW],
+                                           float (&acc)[KPW], int part = 0, int nparts = 1) {
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk)
-    dense[kk] = (double)(Nc - m[kk]) * (double)ow[kk] +
-                sx[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]];
-  {
+  for (int kk = 0; kk < KPW; ++kk) {
+    dsum[kk] = 0.f;
+    acc[kk] = 0.f;
+  }
+  if (part == 0) {
+    int m[KPW];
+    hs_search(svl, NcP, Nc, ow, m);
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk)
+      dsum[kk] = (float)((double)(Nc - m[kk]) * (double)ow[kk] +
+                         sx[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]]);
     float os[KPW], unused[KPW];
     walk_row<1, RS, GS>(rows, ncl, g, os, unused);
 #pragma unroll
@@ -2532,12 +2543,11 @@ __device__ __forceinline__ void fwd_s_lane(const float* svl, const float* rows, 
       const float z0 = ow[kk] + oq[kk];
       acc[kk] += vm * (relu(z0 + dl[kk]) - relu(z0));
     }
-  });
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) out[kk] = (float)dense[kk] + acc[kk];
+  }, part, nparts);
 }
 
-// ... and of the backward one: Dalpha / Dbeta sums (out) and the y-weighted sums (yout)
+// ... and of the backward one: Dalpha / Dbeta sums (dsum + acc) and the y-weighted sums (ya),
+// parts as in fwd_s_lane
 template <int RS, int GS>
 __device__ __forceinline__ void mlpb_s_lane(const float* svl, const float* rows, int NcP, int Nc,
                                             int b, int z, int g, int ncl, bool ys,
@@ -2545,17 +2555,22 @@ __device__ __forceinline__ void mlpb_s_lane(const float* svl, const float* rows,
                                             const float (&dl)[KPW],
                                             const double* __restrict__ sw,
                                             const uint32_t* __restrict__ prep,
-                                            const ListLayout& Y, size_t yrow, float (&out)[KPW],
-                                            float (&yout)[KPW]) {
-  int m[KPW];
-  hs_search(svl, NcP, Nc, ow, m);
-  double dense[KPW];
-  float acc[KPW], ya[KPW];
+                                            const ListLayout& Y, size_t yrow, float (&dsum)[KPW],
+                                            float (&acc)[KPW], float (&ya)[KPW], int part = 0,
+                                            int nparts = 1) {
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk)
-    dense[kk] = (double)(Nc - m[kk]) * (double)wo[kk] +
-                sw[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]];
-  {
+  for (int kk = 0; kk < KPW; ++kk) {
+    dsum[kk] = 0.f;
+    acc[kk] = 0.f;
+    ya[kk] = 0.f;
+  }
+  if (part == 0) {
+    int m[KPW];
+    hs_search(svl, NcP, Nc, ow, m);
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk)
+      dsum[kk] = (float)((double)(Nc - m[kk]) * (double)wo[kk] +
+                         sw[hsort_tab(b, z, g * KPW + kk, NcP + 1) + m[kk]]);
     float os[KPW], ws[KPW];
     walk_row<2, RS, GS>(rows, ncl, g, os, ws);
 #pragma unroll
@@ -2579,17 +2594,16 @@ __device__ __forceinline__ void mlpb_s_lane(const float* svl, const float* rows,
       acc[kk] += m1 - (z0 > 0.f ? gq : 0.f);
       ya[kk] += m1;
     }
-  });
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    out[kk] = (float)dense[kk] + acc[kk];
-    yout[kk] = ya[kk];
-  }
+  }, part, nparts);
 }
 
-// kw_hunk_fwd_s  grid (ceil(Nc / 128), B, 2), NTP threads, Nc <= HS_ALL_MAX: kw_hunk_fwd's
-// results (G / H, sigma / tau) from the sorted tables
-__global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
+// kw_hunk_fwd_s  grid (ceil(Nc / 128), B, 2), HS_NT threads, Nc <= HS_ALL_MAX: kw_hunk_fwd's
+// results (G / H, sigma / tau) from the sorted tables.  Waves 8 h + w: h the half of every
+// node's label list (the walks are latency-bound and the LDS tables allow one block per
+// CU: the halves give each SIMD four waves instead of two), w as the 8-wave shape (node half
+// w >> 2, unit group w & 3); half 1 hands its partial sums to half 0 through res
+constexpr int HS_NT = 2 * NTP;
+__global__ __launch_bounds__(HS_NT) void kw_hunk_fwd_s(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ sv, const double* __restrict__ sx,
@@ -2602,13 +2616,14 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
   int tile, b, z;
   xcd_commit_map(tile, b, z);
   const int t0 = tile * HSN, B = gridDim.y, NcP = (Nc + 3) & ~3;
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
+  const int lane = threadIdx.x & 63, wl = uni(threadIdx.x >> 6), w = wl & 7, lh = wl >> 3;
+  const int g = w & 3, hw = w >> 2;
   const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
   WSTAMP(2, 0);
   stage_w(Ml, D + D_M, H * H);
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
-  float ow[KPW], dl[KPW], out[KPW];
+  float ow[KPW], dl[KPW], dsum[KPW], acc[KPW];
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     ow[kk] = own[(size_t)ncl * H + g * KPW + kk];
@@ -2618,15 +2633,25 @@ __global__ __launch_bounds__(NTP) void kw_hunk_fwd_s(
   hs_stage_all<1>(z, b, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H, nullptr, hs_lds);
   WSTAMP(2, 1);
   fwd_s_lane<HS_OSF, 6>(hs_lds + g * KPW * NcP, hs_lds + H * NcP, NcP, Nc, b, z, g, ncl, ys, ow,
-                        dl, sx, prep, Y, ((size_t)z * B + b) * Nc + ncl, out);
+                        dl, sx, prep, Y, ((size_t)z * B + b) * Nc + ncl, dsum, acc, lh, 2);
   WSTAMP(2, 2);
+  if (lh) {
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) res[nl * HP + g * KPW + kk] = out[kk];
+    for (int kk = 0; kk < KPW; ++kk) res[nl * HP + g * KPW + kk] = acc[kk];
+  }
+  __syncthreads();
+  if (!lh) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      float* r = res + nl * HP + g * KPW + kk;
+      *r = dsum[kk] + (acc[kk] + *r);
+    }
+  }
   __syncthreads();
   float* gout = (z ? Hh : G) + (size_t)b * Nc * H;
   float* sout = (z ? tau : sig) + (size_t)b * Nc * H;
   const float* off = D + (z ? D_T0 : D_S0);
-  for (int e = threadIdx.x; e < HSN * H; e += NTP) {
+  for (int e = threadIdx.x; e < HSN * H; e += HS_NT) {
     const int n = e / H, k = e - n * H;
     if (t0 + n >= Nc) continue;
     float sacc = 0.f;
@@ -2653,7 +2678,7 @@ __global__ __launch_bounds__(NT) void kw_hunk_fwd_g(
   const int nd = t0 + threadIdx.x, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H + g * KPW;
-  float ow[KPW], dl[KPW], out[KPW];
+  float ow[KPW], dl[KPW], dsum[KPW], acc[KPW];
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     ow[kk] = own[(size_t)ncl * H + kk];
@@ -2662,11 +2687,11 @@ __global__ __launch_bounds__(NT) void kw_hunk_fwd_g(
   const bool ys = bitf((z ? yT : ybits) + ((size_t)b * Nc + ncl) * WC, ncl) > 0.f;
   hs_stage_g<1>(z, b, g, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H, nullptr, hs_lds);
   fwd_s_lane<HS_RSF, 0>(hs_lds, hs_lds + KPW * NcP, NcP, Nc, b, z, g, ncl, ys, ow, dl, sx, prep,
-                        Y, ((size_t)z * B + b) * Nc + ncl, out);
+                        Y, ((size_t)z * B + b) * Nc + ncl, dsum, acc);
   if (nd < Nc) {
     float* gout = (z ? Hh : G) + ((size_t)b * Nc + nd) * H + g * KPW;
 #pragma unroll
-    for (int kk = 0; kk < KPW; ++kk) gout[kk] = out[kk];
+    for (int kk = 0; kk < KPW; ++kk) gout[kk] = dsum[kk] + acc[kk];
   }
 }
 
@@ -2705,7 +2730,7 @@ __global__ __launch_bounds__(NT) void kw_hunk_sig(const float* __restrict__ D, i
 // alpha's order and dG; then the y = 1 pairs' mask changes, ysum = sum y dz, and the self
 // pair removed.  The epilogue (partial gradient rows) per 64-node half, as kw_hunk_mlpb's
 // tiles write them.
-__global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
+__global__ __launch_bounds__(HS_NT) void kw_hunk_mlpb_s(
     const uint32_t* __restrict__ ybits, const uint32_t* __restrict__ yT,
     const float* __restrict__ D, int Nc, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ dG, const float* __restrict__ dH,
@@ -2719,13 +2744,14 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
   xcd_commit_map(btile, b, z);
   const int t0 = btile * HSN, B = gridDim.y, NcP = (Nc + 3) & ~3;
   const int tc = (Nc + TN - 1) / TN;
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6), g = w & 3, hw = w >> 2;
+  const int lane = threadIdx.x & 63, wl = uni(threadIdx.x >> 6), w = wl & 7, lh = wl >> 3;
+  const int g = w & 3, hw = w >> 2;                // waves 8 lh + w: as kw_hunk_fwd_s
   const int nl = hw * TN + lane, nd = t0 + nl, ncl = nd < Nc ? nd : Nc - 1;
   const int WC = (Nc + 31) >> 5;
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H;
   const float* wown = (z ? dH : dG) + (size_t)b * Nc * H;
   WSTAMP(3, 0);
-  float ow[KPW], wo[KPW], dl[KPW], out[KPW], yout[KPW];
+  float ow[KPW], wo[KPW], dl[KPW], dsum[KPW], acc[KPW], ya[KPW];
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     ow[kk] = own[(size_t)ncl * H + g * KPW + kk];
@@ -2737,12 +2763,25 @@ __global__ __launch_bounds__(NTP) void kw_hunk_mlpb_s(
                   (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
   WSTAMP(3, 1);
   mlpb_s_lane<HS_OSB, 10>(hs_lds + g * KPW * NcP, hs_lds + H * NcP, NcP, Nc, b, z, g, ncl, ys,
-                          ow, wo, dl, sw, prep, Y, ((size_t)z * B + b) * Nc + ncl, out, yout);
+                          ow, wo, dl, sw, prep, Y, ((size_t)z * B + b) * Nc + ncl, dsum, acc, ya,
+                          lh, 2);
   WSTAMP(3, 2);
+  if (lh) {                                        // list half 1's partial sums -> half 0
 #pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    res[nl * HP + g * KPW + kk] = out[kk];
-    yres[nl * HP + g * KPW + kk] = yout[kk];
+    for (int kk = 0; kk < KPW; ++kk) {
+      res[nl * HP + g * KPW + kk] = acc[kk];
+      yres[nl * HP + g * KPW + kk] = ya[kk];
+    }
+  }
+  __syncthreads();
+  if (!lh) {
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      float* r = res + nl * HP + g * KPW + kk;
+      float* yr = yres + nl * HP + g * KPW + kk;
+      *r = dsum[kk] + (acc[kk] + *r);
+      *yr = ya[kk] + *yr;
+    }
   }
   __syncthreads();
   for (int half = 0; half < 2; ++half) {        // kw_hunk_mlpb's rows, one per 64-node tile
@@ -2776,7 +2815,7 @@ __global__ __launch_bounds__(NT) void kw_hunk_mlpb_g(
   const int WC = (Nc + 31) >> 5;
   const float* own = (z ? beta : alpha) + (size_t)b * Nc * H + g * KPW;
   const float* wown = (z ? dH : dG) + (size_t)b * Nc * H + g * KPW;
-  float ow[KPW], wo[KPW], dl[KPW], out[KPW], yout[KPW];
+  float ow[KPW], wo[KPW], dl[KPW], dsum[KPW], acc[KPW], ya[KPW], out[KPW];
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     ow[kk] = own[(size_t)ncl * H + kk];
@@ -2787,12 +2826,14 @@ __global__ __launch_bounds__(NT) void kw_hunk_mlpb_g(
   hs_stage_g<2>(z, b, g, Nc, sv, (z ? alpha : beta) + (size_t)b * Nc * H,
                 (z ? dG : dH) + (size_t)b * Nc * H, hs_lds);
   mlpb_s_lane<HS_RSB, 0>(hs_lds, hs_lds + KPW * NcP, NcP, Nc, b, z, g, ncl, ys, ow, wo, dl, sw,
-                         prep, Y, ((size_t)z * B + b) * Nc + ncl, out, yout);
+                         prep, Y, ((size_t)z * B + b) * Nc + ncl, dsum, acc, ya);
+#pragma unroll
+  for (int kk = 0; kk < KPW; ++kk) out[kk] = dsum[kk] + acc[kk];
   const bool in = nd < Nc;
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     res[nl * RS5 + kk] = in ? out[kk] : 0.f;
-    yres[nl * RS5 + kk] = in ? yout[kk] : 0.f;
+    yres[nl * RS5 + kk] = in ? ya[kk] : 0.f;
   }
   float* dout = (z ? Dbe : Dal) + (size_t)b * Nc * H + g * KPW;
   if (in) {
@@ -3322,19 +3363,32 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       s32[h] = (f2){0.f, 0.f};
     }
     float cst = 0.f, s1t = S1[4], s3t = 0.f;
-    for_list(prep, 0, b, i, Ne, Nc, [&](int j0) {
-      // the sentinel Ne reads node 0's row with gg = 0: every term below vanishes
+    // neighbour j's row of the group's 5 units and its x (the sentinel Ne reads node 0's
+    // row with gg = 0: every term below vanishes)
+    struct NbrRow {
+      f2 q[2];
+      float q4, xj;
+    };
+    auto ldr = [&](const int j0) -> NbrRow {
+      const int j = j0 < Ne ? j0 : 0;
+      const float* qj = rbb + (size_t)(HDG_ABL_QJ ? ic : j) * H + g * KPW;
+      NbrRow v;
+      v.q[0] = (f2){qj[0], qj[1]};
+      v.q[1] = (f2){qj[2], qj[3]};
+      v.q4 = qj[4];
+      v.xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
+      return v;
+    };
+    auto use = [&](const int j0, const NbrRow& v) {
       const bool ok = j0 < Ne;
-      const int j = ok ? j0 : 0;
       const float vm = ok ? 1.f : 0.f;
-      const float xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
-      const float* qj = rbb + (size_t)j * H + g * KPW;
+      const float xj = v.xj;
       const f2 xx = {xj, xj};
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f2 z0 = MODE == 0 ? u2[h] + xx * wb2[h] : fma2(xx, wb2[h], u2[h]);
         const f2 z1 = z0 + dd2[h];
-        const f2 gg = (ri2[h] + (f2){qj[2 * h], qj[2 * h + 1]}) * vm;   // finite
+        const f2 gg = (ri2[h] + v.q[h]) * vm;   // finite
         const f2 m1 = step2(z1) * gg, m0 = step2(z0) * gg;
         const f2 dm = m1 - m0;
         cs2[h] += dm;
@@ -3343,13 +3397,17 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
       }
       const float z0 = MODE == 0 ? u[4] + xj * wb[4] : fmaf(xj, wb[4], u[4]);
       const float z1 = z0 + dd[4];
-      const float gg = ok ? ri[4] + qj[4] : 0.f;
+      const float gg = ok ? ri[4] + v.q4 : 0.f;
       const float m1 = z1 > 0.f ? gg : 0.f, m0 = z0 > 0.f ? gg : 0.f;
       const float dm = m1 - m0;
       cst += dm;
       s1t = fmaf(xj, dm, s1t);
       s3t += m1;
-    }, hw, 2);
+    };
+    // (one neighbour's loads then its use: 74 VGPRs, 6 waves per SIMD -- batching the row
+    // loads of 4 / 8 / 16 neighbours ahead of their use measured 35.8 / 36.2 / 44.0 us
+    // against 32.8 at stress, the walk wanting waves more than loads in flight)
+    for_list(prep, 0, b, i, Ne, Nc, [&](int j0) { use(j0, ldr(j0)); }, hw, 2);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       cs[2 * h] = cs2[h].x; cs[2 * h + 1] = cs2[h].y;
@@ -4595,7 +4653,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
 #undef HDG_SORT
     WTRY(kmark("kw_hunk_sort", st));
     if (Nc <= HS_ALL_MAX) {
-      hipLaunchKernelGGL(kw_hunk_fwd_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(NTP),
+      hipLaunchKernelGGL(kw_hunk_fwd_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(HS_NT),
                          hs_lds_bytes(Nc, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.hsv), (const double*)F(w.hsx), prep, YL, F(w.G), F(w.Hh),
                          F(w.sig), F(w.tau));
@@ -4673,7 +4731,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
 #undef HDG_WSUM
     WTRY(kmark("kw_hunk_wsum", st));
     if (Nc <= HS_ALL_MAX) {
-      hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(NTP),
+      hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(HS_NT),
                          hs_lds_bytes(Nc, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.dG), F(w.dH), F(w.nvec), F(w.hsv), (const double*)F(w.hsw), prep,
                          YL, F(w.Dal), F(w.Dbe), part, w.segs);
