@@ -3019,7 +3019,8 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     const uint32_t* __restrict__ prep, const float* __restrict__ x, const float* __restrict__ W,
     Off o, int Ne, int Nc, const float* __restrict__ dn, const float* __restrict__ ov,
     const float* __restrict__ P, const float* __restrict__ Eb, const float* __restrict__ hE,
-    float* __restrict__ rhoE, float* __restrict__ part, Segs sg) {
+    float* __restrict__ rhoE, float* __restrict__ part, Segs sg, const float* __restrict__ Dal,
+    const float* __restrict__ Dbe) {
   __shared__ float dxq[NW * TN], xs[TN], dov[TN];
   __shared__ float2 dnl[HS_NC_MAX];               // (dn_c[0], dn_c[1]) of the commit
   __shared__ float Pt[TN * HP], Et[TN * HP], ht[TN * HP], dq[TN * HP], dE[TN * HP];
@@ -3054,9 +3055,29 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
   // the commit's (dn_c[0], dn_c[1]) in LDS: the count loop's per-hunk factors are the same
   // for every lane, and as scalar loads (one s_load and lgkmcnt wait per hunk pair) they
   // cost a third of the loop (wave stamps: 16.9 -> 11.9 us without them at stress)
-  {
+  if (dn) {
     const float* dnb = dn + (size_t)b * Nc * 4;
     for (int c = t; c < Nc; c += NT) dnl[c] = *reinterpret_cast<const float2*>(dnb + 4 * c);
+  } else {   // dn = NULL (no entity-edge stage reads it): kw_dn's m = 0, 1 values computed
+             // here, the same fma order, from the commit's Dalpha / Dbeta rows
+    for (int c = t; c < Nc; c += NT) {
+      const float4* da = reinterpret_cast<const float4*>(Dal + ((size_t)b * Nc + c) * H);
+      const float4* db = reinterpret_cast<const float4*>(Dbe + ((size_t)b * Nc + c) * H);
+      float va[H], vb[H];
+#pragma unroll
+      for (int v = 0; v < H / 4; ++v) {
+        const float4 x4 = da[v], y4 = db[v];
+        va[4 * v] = x4.x; va[4 * v + 1] = x4.y; va[4 * v + 2] = x4.z; va[4 * v + 3] = x4.w;
+        vb[4 * v] = y4.x; vb[4 * v + 1] = y4.y; vb[4 * v + 2] = y4.z; vb[4 * v + 3] = y4.w;
+      }
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        a0 = fmaf(W[o.H1_W1 + k], va[k], fmaf(W[o.H1_W1 + 4 * H + k], vb[k], a0));
+        a1 = fmaf(W[o.H1_W1 + H + k], va[k], fmaf(W[o.H1_W1 + 5 * H + k], vb[k], a1));
+      }
+      dnl[c] = make_float2(a0, a1);
+    }
   }
   __syncthreads();
   WSTAMP(12, 1);
@@ -3229,12 +3250,42 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
   double* T = tab + (((size_t)mode * B + b) * H + k) * 2 * (Ne + 1);
   const int C = (Ne + NT - 1) / NT;
   const int p0 = t * C, p1 = p0 + C < Ne ? p0 + C : Ne;
+  // C <= CR (Ne <= 1024): the thread's chunk loaded once, every load issued before the first
+  // use (perm, then the gathered q and x), kept in registers for the second pass -- the
+  // kernel was a chain of dependent loads per element, twice
+  constexpr int CR = 4;
+  const bool reg = C <= CR;
+  float qv[CR], xv[CR];
+  int mv[CR];
   double a1 = 0.0, a2 = 0.0;
-  for (int p = p0; p < p1; ++p) {            // p = position in scan order
-    const int m = suf ? Ne - 1 - p : p;
-    const double val = (double)q[(size_t)perm[m] * H + k];
-    a1 += val;
-    a2 += val * (double)xsrt[m];
+  if (reg) {
+    int pm[CR];
+#pragma unroll
+    for (int u = 0; u < CR; ++u) {
+      const int p = p0 + u < p1 ? p0 + u : p0;           // clamped, unused past the chunk
+      mv[u] = suf ? Ne - 1 - p : p;
+      pm[u] = p < Ne ? perm[mv[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < CR; ++u) {
+      qv[u] = q[(size_t)pm[u] * H + k];
+      xv[u] = xsrt[p0 + u < Ne ? mv[u] : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < CR; ++u) {
+      if (p0 + u < p1) {
+        const double val = (double)qv[u];
+        a1 += val;
+        a2 += val * (double)xv[u];
+      }
+    }
+  } else {
+    for (int p = p0; p < p1; ++p) {            // p = position in scan order
+      const int m = suf ? Ne - 1 - p : p;
+      const double val = (double)q[(size_t)perm[m] * H + k];
+      a1 += val;
+      a2 += val * (double)xsrt[m];
+    }
   }
   // exclusive scan of the per-thread chunk sums: wave shuffles, then the 4 wave totals
   const int lane = t & 63, w = t >> 6;
@@ -3253,6 +3304,20 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
   if (t == 0) {
     T[suf ? Ne : 0] = 0.0;
     T[Ne + 1 + (suf ? Ne : 0)] = 0.0;
+  }
+  if (reg) {
+#pragma unroll
+    for (int u = 0; u < CR; ++u) {
+      if (p0 + u < p1) {
+        const double val = (double)qv[u];
+        a1 += val;
+        a2 += val * (double)xv[u];
+        const int e = suf ? mv[u] : mv[u] + 1;
+        T[e] = a1;
+        T[Ne + 1 + e] = a2;
+      }
+    }
+    return;
   }
   for (int p = p0; p < p1; ++p) {
     const int m = suf ? Ne - 1 - p : p;
@@ -4756,14 +4821,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        part, w.segs);
     WTRY(kmark("kw_hunk_mlpb", st));
   }
-  if (ent || ee) {
+  if (ee) {   // kw_ee_clsb reads dn; with the entity stage alone kw_node_bwd forms it itself
     hipLaunchKernelGGL(kw_dn, dim3(tc, B), dim3(NT), 0, st, params, o, Nc, F(w.Dal), F(w.Dbe),
                        F(w.dn));
     WTRY(kmark("kw_dn", st));
   }
   if (ent) {
     hipLaunchKernelGGL(kw_node_bwd, dim3(te, B), dim3(NT), 0, st, prep, bt->x, params, o, Ne, Nc,
-                       F(w.dn), F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part, w.segs);
+                       ee ? F(w.dn) : nullptr, F(w.ov), F(w.P), F(w.Eb), F(w.hE), F(w.rhoE), part,
+                       w.segs, F(w.Dal), F(w.Dbe));
     WTRY(kmark("kw_node_bwd", st));
   }
   if (ee) {
