@@ -3060,23 +3060,33 @@ __global__ __launch_bounds__(NT) void kw_node_bwd(
     for (int c = t; c < Nc; c += NT) dnl[c] = *reinterpret_cast<const float2*>(dnb + 4 * c);
   } else {   // dn = NULL (no entity-edge stage reads it): kw_dn's m = 0, 1 values computed
              // here, the same fma order, from the commit's Dalpha / Dbeta rows
-    for (int c = t; c < Nc; c += NT) {
-      const float4* da = reinterpret_cast<const float4*>(Dal + ((size_t)b * Nc + c) * H);
-      const float4* db = reinterpret_cast<const float4*>(Dbe + ((size_t)b * Nc + c) * H);
-      float va[H], vb[H];
+    constexpr int DU = 2;                          // hunks per thread and round trip
+    for (int c0 = t; c0 < Nc; c0 += DU * NT) {
+      float4 va[DU][H / 4], vb[DU][H / 4];
 #pragma unroll
-      for (int v = 0; v < H / 4; ++v) {
-        const float4 x4 = da[v], y4 = db[v];
-        va[4 * v] = x4.x; va[4 * v + 1] = x4.y; va[4 * v + 2] = x4.z; va[4 * v + 3] = x4.w;
-        vb[4 * v] = y4.x; vb[4 * v + 1] = y4.y; vb[4 * v + 2] = y4.z; vb[4 * v + 3] = y4.w;
-      }
-      float a0 = 0.f, a1 = 0.f;
+      for (int u = 0; u < DU; ++u) {
+        const int c = c0 + u * NT < Nc ? c0 + u * NT : c0;   // clamped load, unused
+        const float4* da = reinterpret_cast<const float4*>(Dal + ((size_t)b * Nc + c) * H);
+        const float4* db = reinterpret_cast<const float4*>(Dbe + ((size_t)b * Nc + c) * H);
 #pragma unroll
-      for (int k = 0; k < H; ++k) {
-        a0 = fmaf(W[o.H1_W1 + k], va[k], fmaf(W[o.H1_W1 + 4 * H + k], vb[k], a0));
-        a1 = fmaf(W[o.H1_W1 + H + k], va[k], fmaf(W[o.H1_W1 + 5 * H + k], vb[k], a1));
+        for (int v = 0; v < H / 4; ++v) {
+          va[u][v] = da[v];
+          vb[u][v] = db[v];
+        }
       }
-      dnl[c] = make_float2(a0, a1);
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        if (c0 + u * NT >= Nc) break;
+        const float* fa = reinterpret_cast<const float*>(va[u]);
+        const float* fb = reinterpret_cast<const float*>(vb[u]);
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+          a0 = fmaf(W[o.H1_W1 + k], fa[k], fmaf(W[o.H1_W1 + 4 * H + k], fb[k], a0));
+          a1 = fmaf(W[o.H1_W1 + H + k], fa[k], fmaf(W[o.H1_W1 + 5 * H + k], fb[k], a1));
+        }
+        dnl[c0 + u * NT] = make_float2(a0, a1);
+      }
     }
   }
   __syncthreads();
@@ -4004,10 +4014,19 @@ __global__ __launch_bounds__(64) void kw_grad_reduce(const float* __restrict__ p
     const Seg& g = sg.s[s];
     if (g.n > 0 && p >= g.p0 && p < g.p0 + g.n) {
       const float* src = part + g.off + (long long)(p - g.p0) * g.rows;
-      if (p == pc)
-        for (int r = lane; r < g.rows; r += 64) c += (unsigned long long)src[r];
-      else
-        for (int r = lane; r < g.rows; r += 64) a += src[r];
+      constexpr int RU = 8;                      // rows in flight per lane (same sum order)
+      for (int r0 = lane; r0 < g.rows; r0 += 64 * RU) {
+        float v[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) v[u] = r0 + 64 * u < g.rows ? src[r0 + 64 * u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          if (r0 + 64 * u < g.rows) {
+            if (p == pc) c += (unsigned long long)v[u];
+            else a += v[u];
+          }
+        }
+      }
       break;
     }
   }
