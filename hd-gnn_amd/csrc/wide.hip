@@ -1793,7 +1793,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(4))) void k
   // stored p1 (off-diagonal layout, model_2.py:321) and the y bits, 0 on the diagonal --
   // the forward's float ops on its bits
   const size_t Pc = (size_t)Nc * (Nc - 1);
-  const float* p1b = probs ? probs + (size_t)b * 2 * Pc + Pc : nullptr;
+  const float* p1b = (HDG_GAM_FROM_PROBS && probs) ? probs + (size_t)b * 2 * Pc + Pc : nullptr;
   const uint32_t* ybb = ybits + (size_t)b * Nc * WC;
   auto gamma_at = [&](const int r, const int q) -> float {   // r, q < Nc
     if (!p1b) return gb[(size_t)r * Nc + q];
