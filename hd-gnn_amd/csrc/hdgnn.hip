@@ -1514,6 +1514,7 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
   const int sub = lane / EG_L, kp = lane - sub * EG_L, k0 = 2 * kp;
   const EntUnit ea = ent_unit(Ws, k0 < HS ? k0 : 0), eb = ent_unit(Ws, k0 < HS ? k0 + 1 : 1);
   const f2 w0 = {ea.w0, eb.w0}, w1 = {ea.w1, eb.w1}, c0 = {ea.c0, eb.c0}, dd = {ea.d, eb.d};
+  const f2 ddS = dd * (f2){STEP_S, STEP_S};       // stepf2's c for [z0 + d > 0]
   const bool ra[2] = {ea.w1 >= 0.f, eb.w1 >= 0.f};
   f2 S0 = {0.f, 0.f}, S1 = S0, S2 = S0, S3 = S0;
   // rounds of 96 nodes; wave w takes nodes w + 16 s (s < 6) of a round, so the last,
@@ -1555,17 +1556,18 @@ __device__ __forceinline__ void entity_bwd(const int lane, const int wv, const f
     f2 sd = {0.f, 0.f}, sx = sd;                     // sum dm, sum x_j dm
     // row neighbours from the padded (id, x) lists: 4 ids in one u32 and 4 x values in one
     // 16-byte read per step, identical across the node group's lanes (LDS broadcast)
+    // [z1 > 0] as stepf2(z0, d 2^64) (no z1 add); dm = ([z1 > 0] - [z0 > 0]) gs and s3 += [z1 > 0] gs
+    // as one fma: the same values as m1 gs - m0 gs and s3 + m1 gs (the steps are 0 or 1)
     auto nbr = [&](const int j, const float xj) {
       const f2 rj = *reinterpret_cast<const f2*>(rho + j * HS + k0);
       const f2 z0 = u + xj * w1;
-      const f2 z1 = z0 + dd;
       const f2 gs = ri + rj;                 // finite: step2(z) * gs == [z > 0] gs
-      const f2 m1g = step2(z1) * gs;
-      const f2 m0g = step2(z0) * gs;
-      const f2 dm = m1g - m0g;
+      const f2 st0 = step2(z0);
+      const f2 st1 = HDG_STEPF ? stepf2(z0, ddS) : step2(z0 + dd);
+      const f2 dm = (st1 - st0) * gs;
       sd += dm;
       sx = __builtin_elementwise_fma((f2){xj, xj}, dm, sx);
-      s3 += m1g;
+      s3 = __builtin_elementwise_fma(st1, gs, s3);
     };
     const int o0 = live ? xoff[ic] : 0;
     const int d = live ? coff[ic + 1] - coff[ic] : 0;

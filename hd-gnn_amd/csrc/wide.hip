@@ -3462,13 +3462,15 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f2 z0 = MODE == 0 ? u2[h] + xx * wb2[h] : fma2(xx, wb2[h], u2[h]);
-        const f2 z1 = z0 + dd2[h];
         const f2 gg = (ri2[h] + v.q[h]) * vm;   // finite
-        const f2 m1 = step2(z1) * gg, m0 = step2(z0) * gg;
-        const f2 dm = m1 - m0;
+        // dm and s3 from the two masks (same values as m1 - m0 and += m1); stepf2 for st1
+        // is one op fewer but raises this walk to 125 VGPRs (spills at 6 waves)
+        const f2 st0 = step2(z0);
+        const f2 st1 = step2(z0 + dd2[h]);
+        const f2 dm = (st1 - st0) * gg;
         cs2[h] += dm;
         s12[h] = fma2(xx, dm, s12[h]);
-        s32[h] += m1;
+        s32[h] = fma2(st1, gg, s32[h]);
       }
       const float z0 = MODE == 0 ? u[4] + xj * wb[4] : fmaf(xj, wb[4], u[4]);
       const float z1 = z0 + dd[4];
