@@ -3608,6 +3608,12 @@ __device__ __forceinline__ void ee_clsb_rows_q(
     float& sdl, float (&zr)[2], int (&kst)[2]) {
   const int lane = threadIdx.x & 63, qr = lane >> 4, cq = lane & 15;
   const float bq = D[D_EEBQ];
+  // the classifier's prescaled weight differences read once (uniform: SGPRs); read in the
+  // trip they were refetched every trip (the rowp stores may alias D for the compiler),
+  // and the scalar wait drained the trip's LDS reads with them
+  f2 cqs[H2];
+#pragma unroll
+  for (int kk = 0; kk < H2; ++kk) cqs[kk] = ld2(D + D_EECQ + 2 * kk);
   const int trips = (hi - lo + 3) >> 2;
   const int jn0 = t0 + cq, jn1 = t0 + cq + 16;
   const bool live0 = jn0 < Ne, live1 = jn1 < Ne;
@@ -3655,9 +3661,9 @@ __device__ __forceinline__ void ee_clsb_rows_q(
       for (int kk = 0; kk < H2; ++kk) {  // relu(kappa) = kappa [kappa > 0]
         st[kk] = step2(pre[kk]);
         if (kk & 1)
-          dzb = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dzb);
+          dzb = fma2(pre[kk] * st[kk], cqs[kk], dzb);
         else
-          dz = fma2(pre[kk] * st[kk], ld2(D + D_EECQ + 2 * kk), dz);
+          dz = fma2(pre[kk] * st[kk], cqs[kk], dz);
       }
       dz += dzb;
       const float e = __builtin_amdgcn_exp2f(fminf(dz.x + dz.y, 64.f));
