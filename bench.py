@@ -17,6 +17,7 @@ the CPU baseline is oracle/literal.py (the TF graph's op sequence on torch-CPU).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -29,6 +30,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "training-step commits/sec, glide Ne=200 Nc=74 batch=100; 1/2/4/8 GPU"
+WARM_S = 0.03      # seconds of back-to-back warm-up steps before the timed region
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
 HBM_PEAK_GBS = 8000.0
 CLOCK_HZ = 2.4e9              # gfx950 peak engine clock (MI355X_MICROARCH.md)
@@ -361,8 +363,27 @@ def main():
     else:
         eng.capture(db, steps=gsteps)            # one HIP graph per gsteps training steps
         step = eng.replay
-    for _ in range(max(1, args.warmup // gsteps)):
+    nwarm = max(1, args.warmup // gsteps)
+    for _ in range(nwarm):
         step()
+    torch.cuda.synchronize(dev)
+    # Clock ramp: the device reaches its steady clocks only after a few ms of back-to-back
+    # steps (20-step regions right after start-up: 0.0576, 0.0565, 0.0560, 0.0554, then
+    # 0.0548 ms/step; tools/sync_overhead.py), so beyond the requested W steps the warm-up
+    # keeps the device busy for WARM_S of steps.  The replay count is agreed across ranks
+    # (every rank replays the same graphs: their collectives must pair up).
+    t_w = time.perf_counter()
+    step()
+    torch.cuda.synchronize(dev)
+    nwarm += 1
+    extra = int(math.ceil(WARM_S / max(time.perf_counter() - t_w, 1e-6)))
+    if launched:
+        te = torch.tensor([float(extra)], device="cpu" if shared else dev)
+        torch.distributed.all_reduce(te, op=torch.distributed.ReduceOp.MAX)
+        extra = int(te.item())
+    for _ in range(extra):
+        step()
+    nwarm += extra
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
@@ -436,7 +457,11 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(cb, args.cpu_steps, threads)
     line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "steps": args.steps, "warmup": nwarm * gsteps, "warmup_requested": args.warmup,
+            "warmup_note": "untimed steps run before the timed region: at least the requested "
+                           "W and %g ms of back-to-back steps (the device's clock ramp)" % (
+                               1e3 * WARM_S),
+            "ms_per_step": round(ms_per_step, 5),
             "allreduce": {"xgmi": "in-kernel xGMI exchange of the flat gradient per step "
                                   "(hdg_train_step_dp: tagged words into every peer's "
                                   "mailbox, rank-order sum, TF Adam in the same kernel)",
