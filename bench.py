@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "training-step commits/sec, glide Ne=200 Nc=74 batch=100; 1/2/4/8 GPU"
-WARM_S = 0.03      # seconds of back-to-back warm-up steps before the timed region
+WARM_S = 0.03      # seconds of back-to-back steps before the steady-state re-timing
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak (spec)
 HBM_PEAK_GBS = 8000.0
 CLOCK_HZ = 2.4e9              # gfx950 peak engine clock (MI355X_MICROARCH.md)
@@ -277,6 +277,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly")
+    ap.add_argument("--no-steady", action="store_true",
+                    help="skip the steady-state re-timing after the clock-ramp warm-up")
     ap.add_argument("--graph-steps", type=int, default=50,
                     help="training steps captured per HIP graph (a divisor of --steps)")
     ap.add_argument("--variant", type=int, default=2, choices=(1, 2, 3, 4),
@@ -363,43 +365,58 @@ def main():
     else:
         eng.capture(db, steps=gsteps)            # one HIP graph per gsteps training steps
         step = eng.replay
-    nwarm = max(1, args.warmup // gsteps)
-    for _ in range(nwarm):
-        step()
+    # Warm-up: exactly the requested W training steps (eager launches of the same kernels;
+    # the graph capture's own warm step restores the state it changed and is not counted),
+    # then the timed region of exactly K steps: this is the headline `value`.
+    for _ in range(args.warmup):
+        eng.train_step(db)
     torch.cuda.synchronize(dev)
-    # Clock ramp: the device reaches its steady clocks only after a few ms of back-to-back
-    # steps (20-step regions right after start-up: 0.0576, 0.0565, 0.0560, 0.0554, then
-    # 0.0548 ms/step; tools/sync_overhead.py), so beyond the requested W steps the warm-up
-    # keeps the device busy for WARM_S of steps.  The replay count is agreed across ranks
-    # (every rank replays the same graphs: their collectives must pair up).
-    t_w = time.perf_counter()
-    step()
-    torch.cuda.synchronize(dev)
-    nwarm += 1
-    extra = int(math.ceil(WARM_S / max(time.perf_counter() - t_w, 1e-6)))
-    if launched:
-        te = torch.tensor([float(extra)], device="cpu" if shared else dev)
-        torch.distributed.all_reduce(te, op=torch.distributed.ReduceOp.MAX)
-        extra = int(te.item())
-    for _ in range(extra):
-        step()
-    nwarm += extra
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps // gsteps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    eng.check_status()             # a failed launch (exchange timeout) voids the run: raise
-    if launched:
-        t = torch.tensor([elapsed], device="cpu" if shared else dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+
+    def timed():
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps // gsteps):
+            step()
+        torch.cuda.synchronize(dev)
+        barrier()
+        el = time.perf_counter() - t0
+        eng.check_status()         # a failed launch (exchange timeout) voids the run: raise
+        if launched:
+            t = torch.tensor([el], device="cpu" if shared else dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = t.item()
+        return el
+
+    elapsed = timed()
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
+
+    # Steady state, reported beside the headline: the device reaches its steady clocks only
+    # after a few ms of back-to-back steps (20-step regions right after start-up: 0.0576,
+    # 0.0565, 0.0560, 0.0554, then 0.0548 ms/step; tools/sync_overhead.py), so after WARM_S
+    # more seconds of steps the same K steps are timed again.  The replay count is agreed
+    # across ranks (every rank replays the same graphs: their exchanges must pair up).
+    steady = None
+    if not args.no_steady:
+        t_w = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        extra = int(math.ceil(WARM_S / max(time.perf_counter() - t_w, 1e-6)))
+        if launched:
+            te = torch.tensor([float(extra)], device="cpu" if shared else dev)
+            torch.distributed.all_reduce(te, op=torch.distributed.ReduceOp.MAX)
+            extra = int(te.item())
+        for _ in range(extra):
+            step()
+        torch.cuda.synchronize(dev)
+        el2 = timed()
+        steady = {"warmup": args.warmup + args.steps + (1 + extra) * gsteps,
+                  "value": round(world * B * args.steps / el2, 2),
+                  "ms_per_step": round(1e3 * el2 / args.steps, 5),
+                  "note": "the same %d timed steps again after %g ms more of back-to-back "
+                          "steps (the device's clock ramp); not the headline" % (
+                              args.steps, 1e3 * WARM_S)}
 
     # per-kernel durations: HIP events on the launch stream after every kernel launch of
     # the step (hdg_fwd_bwd_kernel_events), eager launches, a separate instrumented pass
@@ -456,12 +473,16 @@ def main():
     if world == 1 and not args.no_cpu and v == 2:
         threads = min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(cb, args.cpu_steps, threads)
-    line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": world,
-            "steps": args.steps, "warmup": nwarm * gsteps, "warmup_requested": args.warmup,
-            "warmup_note": "untimed steps run before the timed region: at least the requested "
-                           "W and %g ms of back-to-back steps (the device's clock ramp)" % (
-                               1e3 * WARM_S),
+    ndev = min(world, torch.cuda.device_count()) if launched else 1
+    line = {"metric": METRIC, "value": round(value, 2), "unit": "commits/s", "n_gpus": ndev,
+            "n_ranks": world,
+            "steps": args.steps, "warmup": args.warmup, "warmup_requested": args.warmup,
+            "warmup_note": "exactly the requested W untimed training steps before the timed "
+                           "region (plus the HIP-graph capture's state-neutral warm step)",
             "ms_per_step": round(ms_per_step, 5),
+            "steady_state": steady,
+            **({"rehearsal": "%d ranks share %d device(s): not a %d-GPU measurement" % (
+                world, ndev, world)} if shared else {}),
             "allreduce": {"xgmi": "in-kernel xGMI exchange of the flat gradient per step "
                                   "(hdg_train_step_dp: tagged words into every peer's "
                                   "mailbox, rank-order sum, TF Adam in the same kernel)",

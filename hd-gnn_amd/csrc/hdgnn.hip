@@ -3336,6 +3336,107 @@ __global__ __launch_bounds__(1024) void k_dp_tail(const float* __restrict__ src,
   }
 }
 
+// k_dp_tail's SUM / GRAD modes for ranks that share a device (hdg_dp.flags HDG_DP_SHARED):
+// HDG_DP_SHARED_BLOCKS blocks per rank, block b owning the slot groups b, b + G, ... .  A
+// block first sends the words of all its groups (the values are src[p], the epoch of group
+// k is ep[k] + 1 as in k_dp_tail), then receives, sums and updates its groups in order:
+// the same words, tags, rank-order sums and Adam arithmetic as one k_dp_tail block per
+// group, so the two kernels give the same bits and keep the same per-group launch counters.
+// Only G blocks per rank spin, so the W-1 ranks waiting for the last one cover at most
+// (W-1)*G CUs and the last rank's step kernel always finds CUs to run on.
+template <int MODE>
+__global__ __launch_bounds__(DP_NT_LIGHT) void k_dp_tail_shared(
+    const float* __restrict__ src, const int np, const int glen, float* __restrict__ gout,
+    float* __restrict__ params, float* __restrict__ mm, float* __restrict__ vv,
+    float* __restrict__ bpow, const float* __restrict__ aux, const float lr,
+    const float inv_pairs, float* __restrict__ stats, uint32_t* __restrict__ status,
+    const DpArgs d) {
+  static_assert(MODE != dpk::PART, "the shared-device tail exchanges a reduced gradient");
+  __shared__ float vals[dpk::MAXW][RED_P];
+  const int t = threadIdx.x, l = t & (RED_P - 1), r = t / RED_P;
+  const int ngrp = (glen + RED_P - 1) / RED_P;
+  uint32_t* own = d.box[d.rank];
+  uint32_t* ep = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(own) + dpk::OFF_EPOCH);
+  const bool bad = MODE == dpk::GRAD && src[np + HDG_TR_FAULT] != 0.f;
+  // 1. every word of this block's groups to every peer
+  if (r < d.world && r != d.rank) {
+    for (int k = blockIdx.x; k < ngrp; k += gridDim.x) {
+      const int p = k * RED_P + l;
+      const uint32_t e = ep[k] + 1u;
+      if (p < glen)
+        dstore2(dp_slot(d.box[r], e & 1u, d.rank, p),
+                (xu2){__float_as_uint(src[p]), (e << 1) | (bad ? 1u : 0u)});
+    }
+  }
+  // 2. per group: the peers' words, the rank-order sum, TF Adam
+  for (int k = blockIdx.x; k < ngrp; k += gridDim.x) {
+    const int p = k * RED_P + l;
+    const uint32_t e = ep[k] + 1u, par = e & 1u;
+    bool upd = MODE != dpk::SUM && t < RED_P && p < np;
+    const float w = upd ? params[p] : 0.f, m0 = upd ? mm[p] : 0.f, v0 = upd ? vv[p] : 0.f;
+    bool late = false, rbad = false;
+    if (r < d.world && p < glen) {
+      float v;
+      if (r != d.rank) {
+        const uint32_t* in = dp_slot(own, par, r, p);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        xu2 wd = dload2(in);
+        while ((wd.y >> 1) != (e & 0x7FFFFFFFu)) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > d.wait) { late = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+          wd = dload2(in);
+        }
+        v = __uint_as_float(wd.x);
+        rbad = (wd.y & 1u) != 0u;
+      } else {
+        v = src[p];
+      }
+      vals[r][l] = v;
+    }
+    const bool anylate = __syncthreads_or(late);
+    const bool anybad = __syncthreads_or(rbad) || bad;
+    if (t == 0) ep[k] = e;                      // this group's launch is consumed
+    if (t < RED_P && p < glen) {
+      float tot = 0.f;
+      for (int q = 0; q < d.world; ++q) tot += vals[q][l];
+      if (MODE != dpk::SUM && p == np + HDG_TR_CE && anylate) tot = __builtin_nanf("");
+      gout[p] = tot;
+      if (anylate && t == 0 && status) xstore1(status, HDG_STATUS_DP_TIMEOUT);
+      if constexpr (MODE == dpk::GRAD) {
+        const int TH1 = np - 4, TH2 = np - 2;
+        if (stats && p >= np + HDG_TR_COUNT && p <= np + HDG_TR_FAULT)
+          stats[4 + (p - np - HDG_TR_COUNT)] = tot;
+        if (p == np + HDG_TR_CE && stats) {
+          const float ce = tot * inv_pairs;
+          stats[0] = ce;
+          stats[1] = aux[1];
+          stats[2] = aux[0];
+          stats[3] = 10.f * ce + 0.1f * aux[1] + aux[0];
+        }
+        if (anylate || anybad) upd = false;
+        if (upd) {
+          const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+          const float lr_t = lr * aux[4], n1 = aux[2], n2 = aux[3];
+          float gg = tot + 0.001f * w;
+          if (p >= TH1 && p < TH1 + 2) gg += 0.001f * w / n1;
+          if (p >= TH2 && p < TH2 + 2) gg += 0.001f * w / n2;
+          float m = m0, v = v0;
+          m += (gg - m) * (1.f - b1);
+          v += (gg * gg - v) * (1.f - b2);
+          mm[p] = m;
+          vv[p] = v;
+          params[p] = w - lr_t * m / (sqrtf(v) + eps);
+        }
+        if (k == 0 && t == 0 && upd) {
+          bpow[0] = aux[5];
+          bpow[1] = aux[6];
+        }
+      }
+    }
+    __syncthreads();                            // vals is rewritten by the next group
+  }
+}
+
 // aux for MODE GRAD (k_commit_step's block 0 writes it on the fused path): loss terms of
 // the pre-update parameters (model_2.py:123-130, 326-333) and TF ApplyAdam's lr factor,
 // in k_adam_tf's summation order
@@ -4374,6 +4475,7 @@ int dp_args(const hdg_dp* dp, DpArgs& a) {
   if (dp->world < 1 || dp->world > HDG_DP_MAX_WORLD || dp->rank < 0 || dp->rank >= dp->world)
     return fail(HDG_EINVAL, "hdg_dp: rank %d / world %d out of range (world <= %d)", dp->rank,
                 dp->world, HDG_DP_MAX_WORLD);
+  if (dp->flags & ~HDG_DP_SHARED) return fail(HDG_EINVAL, "hdg_dp: unknown flags 0x%x", dp->flags);
   memset(&a, 0, sizeof(a));
   for (int r = 0; r < dp->world; ++r) {
     if (!dp->mailbox[r]) return fail(HDG_EINVAL, "hdg_dp: mailbox of rank %d is NULL", r);
@@ -4383,6 +4485,11 @@ int dp_args(const hdg_dp* dp, DpArgs& a) {
   a.world = dp->world;
   a.wait = dp->wait_ticks ? dp->wait_ticks : dpk::WAIT_DEFAULT;
   return 0;
+}
+bool dp_shared(const hdg_dp* dp) { return (dp->flags & HDG_DP_SHARED) != 0; }
+unsigned dp_shared_grid(int n) {
+  const int groups = (n + RED_P - 1) / RED_P;
+  return (unsigned)(groups < HDG_DP_SHARED_BLOCKS ? groups : HDG_DP_SHARED_BLOCKS);
 }
 float* dp_aux(const hdg_dp* dp) {
   return (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_AUX);
@@ -4398,9 +4505,14 @@ int hdg_dp_allreduce(const hdg_dp* dp, const float* in, float* out, int32_t n, u
   if (!in || !out || n < 1 || n > HDG_DP_MAX_LEN)
     return fail(HDG_EINVAL, "hdg_dp_allreduce: NULL buffer or n=%d outside [1, %d]", n,
                 HDG_DP_MAX_LEN);
-  hipLaunchKernelGGL(k_dp_tail<dpk::SUM>, dim3((n + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT), 0,
-                     (hipStream_t)stream, in, 1, 0, n, out, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, 0.f, 0.f, nullptr, status, 0, a);
+  if (dp_shared(dp))
+    hipLaunchKernelGGL(k_dp_tail_shared<dpk::SUM>, dim3(dp_shared_grid(n)), dim3(DP_NT_LIGHT), 0,
+                       (hipStream_t)stream, in, 0, n, out, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0.f, 0.f, nullptr, status, a);
+  else
+    hipLaunchKernelGGL(k_dp_tail<dpk::SUM>, dim3((n + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT), 0,
+                       (hipStream_t)stream, in, 1, 0, n, out, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0.f, 0.f, nullptr, status, 0, a);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -4419,10 +4531,16 @@ int hdg_adam_dp(const hdg_shape* s, hdg_state* state, const float* grad_local, f
   float* aux = dp_aux(dp);
   hipLaunchKernelGGL(k_dp_aux, dim3(1), dim3(1024), 0, st, state->params, np, state->beta_pow,
                      aux);
-  hipLaunchKernelGGL(k_dp_tail<dpk::GRAD>, dim3((glen + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT), 0, st,
-                     grad_local, 1, np, glen, grad_out, state->params, state->adam_m,
-                     state->adam_v, state->beta_pow, aux, lr, 1.f / pair_count(s), stats, status,
-                     0, a);
+  if (dp_shared(dp))
+    hipLaunchKernelGGL(k_dp_tail_shared<dpk::GRAD>, dim3(dp_shared_grid(glen)), dim3(DP_NT_LIGHT),
+                       0, st, grad_local, np, glen, grad_out, state->params, state->adam_m,
+                       state->adam_v, state->beta_pow, aux, lr, 1.f / pair_count(s), stats,
+                       status, a);
+  else
+    hipLaunchKernelGGL(k_dp_tail<dpk::GRAD>, dim3((glen + RED_P - 1) / RED_P), dim3(DP_NT_LIGHT),
+                       0, st, grad_local, 1, np, glen, grad_out, state->params, state->adam_m,
+                       state->adam_v, state->beta_pow, aux, lr, 1.f / pair_count(s), stats,
+                       status, 0, a);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -4440,13 +4558,17 @@ int hdg_train_step_dp(const hdg_shape* s, const hdg_batch* bt, hdg_state* state,
   hipStream_t st = (hipStream_t)stream;
   uint32_t* status = out ? out->status : nullptr;
   float* stats = out ? out->stats : nullptr;
-  if (path == HDG_PATH_GENERAL || is_hybrid(s, path)) {
+  if (path == HDG_PATH_GENERAL || is_hybrid(s, path) || dp_shared(dp)) {
     // the rank's own reduced gradient lands in the mailbox's local scratch (the tail
-    // reads it while other blocks already write the world sums into grad)
+    // reads it while other blocks already write the world sums into grad).  Ranks that
+    // share a device take this route on the fused path too: the partial rows are reduced
+    // by the non-spinning k_grad_reduce, and only the light tail waits for the peers
     float* local = (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_GLOC);
     const int rc = path == HDG_PATH_GENERAL
         ? hdg::wide_run(s, bt, state->params, local, out, nullptr, workspace, true, st)
-        : hybrid_run(s, bt, state->params, local, out, nullptr, workspace, true, st, nullptr);
+        : is_hybrid(s, path)
+        ? hybrid_run(s, bt, state->params, local, out, nullptr, workspace, true, st, nullptr)
+        : hdg_fwd_bwd(s, bt, state->params, local, out, workspace, stream);
     if (rc) return rc;
     return hdg_adam_dp(s, state, local, grad, lr, stats, status, dp, stream);
   }

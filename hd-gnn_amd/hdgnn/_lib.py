@@ -47,12 +47,14 @@ class Outputs(ctypes.Structure):
 class Dp(ctypes.Structure):
     """hdg_dp: this rank's view of the node's xGMI mailboxes (include/hdgnn.h)."""
     _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32),
-                ("wait_ticks", ctypes.c_uint64), ("mailbox", ctypes.c_void_p * 16)]
+                ("wait_ticks", ctypes.c_uint64), ("mailbox", ctypes.c_void_p * 16),
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 DP_MAX_WORLD, DP_HANDLE_BYTES, DP_MAX_LEN = 16, 64, 3152
+DP_SHARED, DP_SHARED_BLOCKS = 1, 8      # hdg_dp.flags: ranks share a device (include/hdgnn.h)
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 # gradient trailer (include/hdgnn.h): grad = [P parameter gradients | TRAILER slots]
 TRAILER, TR_CE, TR_COUNT, TR_FAULT = 8, 0, 1, 4
 STATUS_XCH_TIMEOUT, STATUS_DP_TIMEOUT = 1, 2

@@ -21,11 +21,13 @@ from .layout import n_params, state_offsets
 
 class Engine:
     def __init__(self, ne, nc, batch, variant=2, device="cuda", batch_global=None, lr=3e-4,
-                 process_group=None, path=_lib.PATH_AUTO, allreduce=None, flags=0):
+                 process_group=None, path=_lib.PATH_AUTO, allreduce=None, flags=0,
+                 dp_shared=None):
         """variant: model_<variant>.py (1 HD-GNN/ES, 2 HD-GNN/S, 3 HD-GNN/E, 4 HD-GNN).
         path: PATH_AUTO (fused kernel when it applies, else the general path),
         PATH_FUSED or PATH_GENERAL (include/hdgnn.h).  flags: HDG_FLAG_* bits
-        (FLAG_HUNK_DENSE / FLAG_HUNK_SORTED force the general path's hunk-sum form)."""
+        (FLAG_HUNK_DENSE / FLAG_HUNK_SORTED force the general path's hunk-sum form).
+        dp_shared: the xGMI ranks share devices (HDG_DP_SHARED); None detects it."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -88,7 +90,7 @@ class Engine:
             if mode != "rccl":
                 from .xgmi import XgmiGroup
                 self.xgmi = XgmiGroup.create(self.lib, self.pg or torch.distributed.group.WORLD,
-                                             dev, required=mode == "xgmi")
+                                             dev, required=mode == "xgmi", shared=dp_shared)
                 self.allreduce_selftest = XgmiGroup.verdict
             else:
                 self.allreduce_selftest = "xGMI not tried (HDG_DP_ALLREDUCE=rccl)"

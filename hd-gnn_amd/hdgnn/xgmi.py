@@ -17,6 +17,7 @@ through torch.distributed / RCCL) or raises (mode "xgmi").
 """
 import contextlib
 import ctypes
+import os
 import socket
 import sys
 
@@ -27,6 +28,21 @@ from . import _lib
 
 TICKS_PER_S = 100_000_000           # s_memrealtime
 SELFTEST_WAIT_S = 5.0
+
+
+def device_identity(device):
+    """A string naming the physical GPU behind `device` (its UUID when torch reports one,
+    else the PCI location, else the index): equal for two ranks on the same GPU.  A CPU
+    device (the set-up protocol's tests) names the process: never shared."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return "%s:pid%d" % (device.type, os.getpid())
+    p = torch.cuda.get_device_properties(device)
+    for attr in ("uuid", "pci_bus_id"):
+        v = getattr(p, attr, None)
+        if v is not None and str(v):
+            return "%s:%s:%s" % (attr, getattr(p, "pci_domain_id", ""), v)
+    return "index:%d" % device.index
 
 
 class XgmiGroup:
@@ -43,10 +59,18 @@ class XgmiGroup:
 
     # ------------------------------------------------------------------ setup
     @classmethod
-    def create(cls, lib, pg, device, required=False, wait_s=10.0):
+    def create(cls, lib, pg, device, required=False, wait_s=10.0, shared=None):
+        """shared: the ranks share devices (hdg_dp.flags HDG_DP_SHARED: light capped tails
+        that cannot starve a peer's step kernel of CUs); None = detect it from the ranks'
+        device identities (one GPU box: every rank on device 0)."""
         dist = torch.distributed
         world, rank = dist.get_world_size(pg), dist.get_rank(pg)
         tdev = device if dist.get_backend(pg) == "nccl" else torch.device("cpu")
+        if shared is None:
+            devs = [None] * world
+            dist.all_gather_object(devs, (socket.gethostname(), device_identity(device)),
+                                   group=pg)
+            shared = len(set(devs)) < world
 
         def agree(ok):
             t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=tdev)
@@ -89,6 +113,8 @@ class XgmiGroup:
                     break
                 peers[r] = p
             grp = cls(lib, rank, world, own, peers, device) if ok else None
+            if grp:
+                grp.dp.flags = _lib.DP_SHARED if shared else 0
             if not agree(ok):
                 if grp:
                     grp.close()
@@ -103,7 +129,10 @@ class XgmiGroup:
                 return give_up("self-test failed on some rank (%s)" % (why or "peer"))
             grp.dp.wait_ticks = int(wait_s * TICKS_PER_S)
             cls.verdict = ("passed: exact rank-order sums of %d floats over %d ranks through "
-                           "the mailboxes" % (_lib.DP_MAX_LEN, world))
+                           "the mailboxes%s" % (_lib.DP_MAX_LEN, world,
+                                                " (ranks share a device: %d light tail blocks "
+                                                "per rank)" % _lib.DP_SHARED_BLOCKS
+                                                if shared else ""))
             return grp
 
     def selftest(self, n=_lib.DP_MAX_LEN):

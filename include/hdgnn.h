@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HDG_ABI_VERSION 8
+#define HDG_ABI_VERSION 9
 #define HDG_EINVAL 1000
 
 /* Per-launch problem shape (one rank's share of the commit batch). */
@@ -261,7 +261,22 @@ typedef struct hdg_dp {
     int32_t  world;       /* ranks on this node, 1 <= world <= HDG_DP_MAX_WORLD          */
     uint64_t wait_ticks;  /* 100 MHz ticks a block waits for a peer (0: 10 s)            */
     void*    mailbox[HDG_DP_MAX_WORLD];  /* rank r's mailbox as mapped in this process   */
+    int32_t  flags;       /* HDG_DP_* bits (ABI 9), 0 for one rank per device            */
+    int32_t  reserved;    /* 0                                                            */
 } hdg_dp;
+/* HDG_DP_SHARED: several ranks share one device (a rehearsal of the node's DP step on a
+ * box with fewer GPUs).  A waiting tail block spins on a CU; with one rank per device
+ * nothing else needs that CU, but a peer rank on the SAME device still has to place its
+ * step kernel, whose 1024-thread blocks each take a whole CU (all VGPRs, up to all of the
+ * LDS).  The tails of W-1 waiting ranks must therefore never cover every CU: with this
+ * flag every exchange runs as HDG_DP_SHARED_BLOCKS light blocks per rank that loop over
+ * the slot groups (all of a block's words sent first, then its groups received in order),
+ * and the fused path reduces its partial rows with the non-spinning k_grad_reduce before
+ * the exchange (hdg_fwd_bwd -> hdg_adam_dp) instead of inside the spinning tail.  At most
+ * (HDG_DP_MAX_WORLD - 1) * HDG_DP_SHARED_BLOCKS = 120 spinning blocks per device.  Same
+ * bits as the one-rank-per-device calls.                                               */
+#define HDG_DP_SHARED 1
+#define HDG_DP_SHARED_BLOCKS 8
 
 size_t hdg_dp_mailbox_bytes(void);
 /* Host utility: CRC-32C (Castagnoli) of n bytes, continuing from crc (0 to start) -- the

@@ -151,15 +151,21 @@ def test_header_trailer_constants_match_binding():
     assert val["HDG_STATUS_DP_TIMEOUT"] == _lib.STATUS_DP_TIMEOUT
     assert (val["HDG_DP_MAX_WORLD"], val["HDG_DP_HANDLE_BYTES"], val["HDG_DP_MAX_LEN"]) == (
         _lib.DP_MAX_WORLD, _lib.DP_HANDLE_BYTES, _lib.DP_MAX_LEN)
+    assert (val["HDG_DP_SHARED"], val["HDG_DP_SHARED_BLOCKS"]) == (
+        _lib.DP_SHARED, _lib.DP_SHARED_BLOCKS)
 
 
 def test_dp_struct_and_mailbox_size():
-    """hdg_dp's ctypes mirror has the C layout (int32 rank, world; u64 wait; 16 pointers)
-    and the mailbox holds two parities x 16 senders x DP_MAX_LEN tagged words."""
+    """hdg_dp's ctypes mirror has the C layout (int32 rank, world; u64 wait; 16 pointers;
+    int32 flags, reserved) and the mailbox holds two parities x 16 senders x DP_MAX_LEN
+    tagged words."""
     import ctypes
     from hdgnn import _lib
-    assert ctypes.sizeof(_lib.Dp) == 4 + 4 + 8 + 8 * _lib.DP_MAX_WORLD
+    assert ctypes.sizeof(_lib.Dp) == 4 + 4 + 8 + 8 * _lib.DP_MAX_WORLD + 4 + 4
     assert _lib.Dp.mailbox.offset == 16
+    assert _lib.Dp.flags.offset == 16 + 8 * _lib.DP_MAX_WORLD
+    # the shared-device tails: the waiting ranks' spinning blocks never cover the CUs
+    assert (_lib.DP_MAX_WORLD - 1) * _lib.DP_SHARED_BLOCKS < 256
     lib = _lib.load()
     assert lib.hdg_dp_mailbox_bytes() >= 2 * _lib.DP_MAX_WORLD * _lib.DP_MAX_LEN * 8
     assert _lib.DP_MAX_LEN >= lib.hdg_grad_len(4) and _lib.DP_MAX_LEN % 16 == 0

@@ -10,8 +10,14 @@ Per workload (variant x Ne x Nc x batch per GPU, the engine path bench.py picks)
   * bitwise determinism of fwd_bwd (gradient and probabilities) on the full grid;
   * the data-parallel decomposition at full size: the two halves of the batch, each with
     the CE normalised by the whole batch, sum to the full batch's gradient (8e-5 |g| +
-    8e-6 max|g| per variable: fp32 reduction order differs between the grids).
-Reference shapes: main.py:11-15 (steps 2 / 3 / 5), SURVEY 8(d) stress.
+    8e-6 max|g| per variable: fp32 reduction order differs between the grids);
+  * the full batch's gradient against the float64 oracle's, the oracle run over chunks of
+    commits (its CE mean re-weighted by chunk / B and summed: the DP decomposition of
+    tests/test_dp.py) at test_gpu_parity.py's gradient tolerances, and one TF-Adam step's
+    weights at atol 2e-6 -- the whole grid the bench launches (split mode, 2B blocks, every
+    block-pair exchange and the 2B-row reduction), not a few commits.
+Reference shapes: main.py:11-15 (steps 2 / 3 / 5), SURVEY 8(d) stress; gradient and
+update: model_2.py:115-130, 336-338.
 """
 import numpy as np
 import pytest
@@ -20,7 +26,67 @@ import torch
 from hdgnn import _lib, layout
 from hdgnn.data import pair_index
 from hdgnn.synth import synth_commits
-from tests.test_general_gpu import _check_outputs, _oracle
+from oracle import model_ref
+from tests import _errlog
+from tests.test_general_gpu import _check_outputs, _oracle, _reg_grad
+
+GRAD_RTOL, GRAD_ATOL = 1.5e-4, 3e-6      # test_gpu_parity.py: x |ref|, x max|ref| per variable
+
+
+def oracle_batch_grad(flat, cb, v, chunk):
+    """The float64 oracle's gradient of the whole batch's train_loss (model_2.py:336),
+    computed over chunks of `chunk` commits: each chunk's data gradient (its gradient minus
+    the parameter-only loss_para / loss_map terms) weighted by its share of the batch, plus
+    those terms once.  Returns (gradient, CE of the batch)."""
+    B = cb.B
+    reg = _reg_grad(flat)
+    g, ce = np.zeros(len(flat)), 0.0
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        out, gc = _oracle(flat, cb.slice(lo, hi), v)
+        g += (gc - reg) * ((hi - lo) / B)
+        ce += float(out["ce"]) * ((hi - lo) / B)
+    return g + reg, ce
+
+
+def grad_close(g_eng, g_ref, v, what):
+    bad = []
+    for name, (o, shape) in layout.offsets(v).items():
+        n = int(np.prod(shape))
+        a, r = g_eng[o:o + n], g_ref[o:o + n]
+        scale = max(np.abs(r).max(), 1e-12)
+        tol = GRAD_RTOL * np.abs(r) + GRAD_ATOL * scale + 1e-9
+        err = np.abs(a - r)
+        _errlog.record("%s:%s" % (what, name), err.max() / scale, (err / tol).max())
+        if not np.all(err <= tol):
+            bad.append("%s: max err %.3g, scale %.3g, %d/%d bad" % (
+                name, np.nanmax(err) if np.isfinite(err).any() else np.nan, scale,
+                int((~(err <= tol)).sum()), n))
+    assert not bad, "%s mismatch:\n  " % what + "\n  ".join(bad)
+
+
+def check_full_batch_vs_oracle(eng, db, cb, flat, v, chunk=10):
+    """eng (parameters = flat) on the full batch: fwd_bwd's gradient and one training step's
+    weights against the oracle.  Leaves eng's parameters updated by one step."""
+    B, nc = cb.B, cb.Nc
+    eng.set_params(flat)
+    eng.fwd_bwd(db)
+    torch.cuda.synchronize()
+    eng.check_status()
+    g = eng.grad.cpu().numpy().astype(np.float64)
+    P = len(flat)
+    g_ref, ce_ref = oracle_batch_grad(flat, cb, v, chunk)
+    grad_close(g[:P] + _reg_grad(flat), g_ref, v, "fullgrad")
+    np.testing.assert_allclose(g[P] / (B * nc * (nc - 1)), ce_ref, rtol=1e-5)
+    eng.set_params(flat)                      # Adam moments and beta powers reset too
+    eng.train_step(db)
+    torch.cuda.synchronize()
+    eng.check_status()
+    want = model_ref.AdamTF(P).step(flat.astype(np.float64), g_ref)
+    err = np.abs(eng.get_params() - want)
+    _errlog.record("weights@1:full", err.max(), err.max() / 2e-6)
+    np.testing.assert_allclose(eng.get_params(), want, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(eng.stats[0].item(), ce_ref, rtol=1e-5)
 
 pytestmark = pytest.mark.gpu
 
@@ -93,3 +159,6 @@ def test_full_size_workload(w):
         tol = 8e-5 * np.abs(r) + 8e-6 * max(np.abs(r).max(), 1e-12) + 1e-9
         assert np.all(np.abs(a - r) <= tol), "%s: max err %.3g" % (name, np.abs(a - r).max())
     np.testing.assert_allclose(gsum[P], g[P], rtol=1e-5)          # CE sum trailer
+
+    # the full grid's gradient and one TF-Adam step against the float64 oracle
+    check_full_batch_vs_oracle(eng, db, cb, flat, v, chunk=10 if ne <= 256 else 4)

@@ -202,8 +202,10 @@ def test_deterministic_bitwise():
 
 
 def test_full_size_properties():
-    """BASELINE config 2 (glide, B=100): probabilities normalised, CE equals the mean
-    -log p_label of the returned probabilities, a few commits match the oracle."""
+    """BASELINE config 2 (glide, B=100, the bench's split grid of 200 blocks): probabilities
+    normalised, CE equals the mean -log p_label of the returned probabilities, a few
+    commits' outputs match the oracle, and the full batch's gradient and one TF-Adam step
+    match the oracle's (summed over chunks of 10 commits; tests/test_fullsize_gpu.py)."""
     B, ne, nc = 100, 200, 74
     cb = synth_commits(B, ne, nc, 20250301)
     eng = _engine(B, ne, nc)
@@ -223,6 +225,9 @@ def test_full_size_properties():
     sub = cb.slice(0, 3)
     out, _ = _oracle(flat, sub)
     _check_outputs(eng.logits.cpu().numpy()[:3], probs[:3], out)
+    from tests.test_fullsize_gpu import check_full_batch_vs_oracle
+    assert eng.split                           # 2B <= CUs: the bench's grid
+    check_full_batch_vs_oracle(eng, cb.to_device(), cb, flat, 2)
 
 
 def test_shape_errors_are_reported():

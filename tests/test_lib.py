@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from hdgnn import _lib
     lib = _lib.load()
-    assert lib.hdg_version() == _lib.ABI_VERSION == 8
+    assert lib.hdg_version() == _lib.ABI_VERSION == 9
     for v, n in ((1, 1146), (2, 2127), (3, 2148), (4, 3129)):
         assert lib.hdg_param_count(v) == n
         assert lib.hdg_grad_len(v) == n + _lib.TRAILER

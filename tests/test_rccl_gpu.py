@@ -64,28 +64,34 @@ def test_rccl_step_matches_single_process(world1, v):
     np.testing.assert_allclose(dp.stats.cpu().numpy(), single.stats.cpu().numpy(), rtol=1e-6)
 
 
-def test_bench_gpus2_starts_two_ranks():
-    """`bench.py --gpus 2` without a launcher starts the two ranks itself (the driver's
-    scaling command shape).  On the one-GPU box both ranks share device 0: gloo control
-    plane, the gradient over the xGMI mailboxes (IPC between the two processes), one block
-    per commit."""
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_gpus_n_starts_n_ranks(n):
+    """`bench.py --gpus N` without a launcher starts the N ranks itself (the driver's
+    scaling command shape).  On the one-GPU box the ranks share device 0: gloo control
+    plane, the gradient over the xGMI mailboxes (IPC between the processes) with the
+    shared-device tails (HDG_DP_SHARED: 8 light blocks per rank, so the waiting ranks can
+    never hold every CU while the last rank's step kernel still needs one), one block per
+    commit.  The line then counts the one device in n_gpus and the ranks in n_ranks."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
-           "--warmup", "2", "--no-cpu", "--e2e", "0"]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "20",
+           "--warmup", "5", "--no-cpu", "--e2e", "0"]
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]          # rank 0 alone prints
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
-    assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert d["n_ranks"] == n and d["n_gpus"] == min(n, torch.cuda.device_count())
+    assert d["config"]["global_batch"] == n * d["config"]["batch_per_gpu"]
+    assert d["config"]["parallelism"] == "dp%d" % n and d["value"] > 0
+    assert d["warmup"] == d["warmup_requested"] == 5 and d["steps"] == 20
     dp = d["dp"]
     assert dp["allreduce"] == "xgmi" and dp["selftest"].startswith("passed")
-    assert "over 2 ranks" in dp["selftest"] and dp["tail_ms_per_step"] > 0
-    if torch.cuda.device_count() < 2:
-        assert "ranks_share_device" in d["config"]
+    assert "over %d ranks" % n in dp["selftest"] and dp["tail_ms_per_step"] > 0
+    if torch.cuda.device_count() < n:
+        assert "ranks_share_device" in d["config"] and "rehearsal" in d
+        assert "share a device" in dp["selftest"]
 
 
 @pytest.mark.parametrize("mode", ["rccl", "auto"])

@@ -6,7 +6,8 @@ memory -- the same protocol the 8-GPU node runs over xGMI links.  The handles go
 gloo group (RCCL refuses two ranks on one GPU).
 
 Checks: the DP step (fused and general path; eager, HIP-graph replay, and the split
-fwd_bwd / adam calls) equals the single-process step on the whole batch and keeps the
+fwd_bwd / adam calls; world 2 and 4; the one-rank-per-device tails and the shared-device
+tails of HDG_DP_SHARED) equals the single-process step on the whole batch and keeps the
 replicas bitwise equal; the plain all-reduce sums in rank order bit for bit (world 4);
 a rank that stops exchanging makes its peer fail loudly (HDG_STATUS_DP_TIMEOUT, no
 update) instead of hanging.
@@ -42,7 +43,7 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _train_main(rank, world, port, out_dir):
+def _train_main(rank, world, port, out_dir, shared=None):
     from hdgnn.engine import Engine
     _init(rank, world, port)
     cb = synth_commits(BL * world, NE, NC, SEED)
@@ -52,8 +53,9 @@ def _train_main(rank, world, port, out_dir):
         flat = layout.init_flat(5, v)
         for mode in ("eager", "graph", "calls"):
             eng = Engine(NE, NC, BL, variant=v, batch_global=BL * world,
-                         process_group=dist.group.WORLD, allreduce="xgmi")
+                         process_group=dist.group.WORLD, allreduce="xgmi", dp_shared=shared)
             assert eng.allreduce_kind == "xgmi"
+            res["flags"] = np.array(eng.xgmi.dp.flags)
             eng.set_params(flat)
             db = eng.upload(shard)
             if mode == "graph":
@@ -77,11 +79,21 @@ def _train_main(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_step_equals_single_process(tmp_path):
-    world = 2
-    mp.spawn(_train_main, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,shared", [(2, False), (2, None), (4, None)],
+                         ids=["w2-per-device-tails", "w2-auto", "w4-auto"])
+def test_xgmi_step_equals_single_process(tmp_path, world, shared):
+    """world 4 is the DP training step above world 2: on the one-GPU box the
+    four ranks share the device, so `auto` detects it and runs the shared-device tails
+    (HDG_DP_SHARED); (2, False) keeps the one-rank-per-device tails (k_dp_tail<PART> on the
+    fused path) covered, whose small grids here still fit beside each other."""
+    mp.spawn(_train_main, args=(world, _port(), str(tmp_path), shared), nprocs=world,
+             join=True)
     from hdgnn.engine import Engine
     r = [np.load(os.path.join(tmp_path, "rank%d.npz" % k)) for k in range(world)]
+    want_flags = (_lib.DP_SHARED if torch.cuda.device_count() < world else 0) \
+        if shared is None else 0
+    for k in range(world):
+        assert int(r[k]["flags"]) == want_flags
     cb = synth_commits(BL * world, NE, NC, SEED)
     for v in VARIANTS:
         single = Engine(NE, NC, BL * world, variant=v)
@@ -95,8 +107,9 @@ def test_xgmi_step_equals_single_process(tmp_path):
         for mode in ("eager", "graph", "calls"):
             k = "v%d_%s_" % (v, mode)
             # replicas bitwise equal: every rank sums the world's words in rank order
-            np.testing.assert_array_equal(r[0][k + "params"], r[1][k + "params"])
-            np.testing.assert_array_equal(r[0][k + "stats"], r[1][k + "stats"])
+            for q in range(1, world):
+                np.testing.assert_array_equal(r[0][k + "params"], r[q][k + "params"])
+                np.testing.assert_array_equal(r[0][k + "stats"], r[q][k + "stats"])
             np.testing.assert_allclose(r[0][k + "params"], want_p, rtol=0, atol=1e-6,
                                        err_msg=k)
             np.testing.assert_allclose(r[0][k + "stats"], want_s, rtol=1e-5, err_msg=k)
@@ -105,11 +118,12 @@ def test_xgmi_step_equals_single_process(tmp_path):
         np.testing.assert_array_equal(r[0]["v%d_eager_params" % v], r[0]["v%d_graph_params" % v])
 
 
-def _sum_main(rank, world, port, out_dir):
+def _sum_main(rank, world, port, out_dir, shared=None):
     from hdgnn.xgmi import XgmiGroup
     _init(rank, world, port)
     lib = _lib.load()
-    grp = XgmiGroup.create(lib, dist.group.WORLD, torch.device("cuda", 0), required=True)
+    grp = XgmiGroup.create(lib, dist.group.WORLD, torch.device("cuda", 0), required=True,
+                           shared=shared)
     dev = torch.device("cuda", 0)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     outs = []
@@ -135,9 +149,10 @@ def _sum_main(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_xgmi_allreduce_rank_order_and_timeout(tmp_path):
+@pytest.mark.parametrize("shared", [None, False], ids=["auto", "per-device-tails"])
+def test_xgmi_allreduce_rank_order_and_timeout(tmp_path, shared):
     world = 4
-    mp.spawn(_sum_main, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_sum_main, args=(world, _port(), str(tmp_path), shared), nprocs=world, join=True)
     res = [np.load(os.path.join(tmp_path, "sum%d.npz" % k)) for k in range(world)]
     for i, n in enumerate((1, 17, 2131, _lib.DP_MAX_LEN)):
         xs = [np.random.default_rng(100 * n + k).standard_normal(n).astype(np.float32)
