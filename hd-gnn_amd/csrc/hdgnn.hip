@@ -4392,6 +4392,18 @@ int hdg_ckpt_writer_flush(void* writer) {
   return rc;
 }
 
+int hdg_ckpt_writer_poll(void* writer) {
+  auto* w = static_cast<hdg_ckpt_writer_s*>(writer);
+  if (!w) return fail(HDG_EINVAL, "hdg_ckpt_writer_poll: NULL writer");
+  std::lock_guard<std::mutex> lk(w->mu);
+  const int rc = w->err_code;
+  if (rc) {
+    snprintf(hdg::g_err, sizeof(hdg::g_err), "%s", w->err);
+    w->err_code = 0;
+  }
+  return rc;
+}
+
 int hdg_ckpt_writer_destroy(void* writer) {
   auto* w = static_cast<hdg_ckpt_writer_s*>(writer);
   if (!w) return 0;

@@ -2328,6 +2328,19 @@ __host__ __device__ inline size_t hs_lds_bytes(int Nc, int nvec) {   // nvec: 1 
   return ((size_t)KPW * NcP + (size_t)Nc * (nvec == 1 ? HS_RSF : HS_RSB)) * 4;
 }
 __host__ __device__ inline int hs_tiles(int Nc) { return (Nc + HSG - 1) / HSG; }
+// the all-unit shape runs for Nc <= HS_ALL_MAX unless HDG_FLAG_HUNK_GROUP asks for the group
+// shape; the two differ in the order of a node's label-walk sum: the all-unit kernels walk
+// the list in two halves on separate waves (dense + (half 0 + half 1)), the group kernels in
+// one chain (dense + all), so their results differ by fp32 re-association
+// (tests/test_general_gpu.py::test_sorted_all_unit_vs_group_shape pins it)
+__host__ inline bool hs_all_shape(const hdg_shape* s) {
+  return s->nc <= HS_ALL_MAX && !(s->flags & HDG_FLAG_HUNK_GROUP);
+}
+__host__ inline size_t hs_shape_lds_bytes(const hdg_shape* s, int nvec) {
+  const size_t NcP = (s->nc + 3) & ~3;
+  if (hs_all_shape(s)) return hs_lds_bytes(s->nc, nvec);
+  return ((size_t)KPW * NcP + (size_t)s->nc * (nvec == 1 ? HS_RSF : HS_RSB)) * 4;
+}
 
 // copy n16 16-byte words src -> dst with every load of the thread in flight first
 template <int U>
@@ -4744,15 +4757,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
 #undef HDG_SORT
     WTRY(kmark("kw_hunk_sort", st));
-    if (Nc <= HS_ALL_MAX) {
+    if (hs_all_shape(s)) {
       hipLaunchKernelGGL(kw_hunk_fwd_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(HS_NT),
-                         hs_lds_bytes(Nc, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         hs_shape_lds_bytes(s, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.hsv), (const double*)F(w.hsx), prep, YL, F(w.G), F(w.Hh),
                          F(w.sig), F(w.tau));
       WTRY(kmark("kw_hunk_fwd_s", st));
     } else {
       hipLaunchKernelGGL(kw_hunk_fwd_g, dim3(4 * hs_tiles(Nc), B, 2), dim3(NT),
-                         hs_lds_bytes(Nc, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         hs_shape_lds_bytes(s, 1), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.hsv), (const double*)F(w.hsx), prep, YL, F(w.G), F(w.Hh));
       WTRY(kmark("kw_hunk_fwd_g", st));
       hipLaunchKernelGGL(kw_hunk_sig, dim3(tc, B, 2), dim3(NT), 0, st, D, Nc, F(w.G), F(w.Hh),
@@ -4822,15 +4835,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     }
 #undef HDG_WSUM
     WTRY(kmark("kw_hunk_wsum", st));
-    if (Nc <= HS_ALL_MAX) {
+    if (hs_all_shape(s)) {
       hipLaunchKernelGGL(kw_hunk_mlpb_s, dim3((Nc + HSN - 1) / HSN, B, 2), dim3(HS_NT),
-                         hs_lds_bytes(Nc, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         hs_shape_lds_bytes(s, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.dG), F(w.dH), F(w.nvec), F(w.hsv), (const double*)F(w.hsw), prep,
                          YL, F(w.Dal), F(w.Dbe), part, w.segs);
       WTRY(kmark("kw_hunk_mlpb_s", st));
     } else {
       hipLaunchKernelGGL(kw_hunk_mlpb_g, dim3(4 * hs_tiles(Nc), B, 2), dim3(NT),
-                         hs_lds_bytes(Nc, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
+                         hs_shape_lds_bytes(s, 2), st, bt->ybits, yT, D, Nc, F(w.alpha), F(w.beta),
                          F(w.dG), F(w.dH), F(w.nvec), F(w.hsv), (const double*)F(w.hsw), prep,
                          YL, F(w.Dal), F(w.Dbe), part, w.segs);
       WTRY(kmark("kw_hunk_mlpb_g", st));

@@ -22,6 +22,7 @@ class Shape(ctypes.Structure):
 
 PATH_AUTO, PATH_FUSED, PATH_GENERAL = 0, 1, 2
 FLAG_NO_SPLIT, FLAG_HUNK_DENSE, FLAG_HUNK_SORTED, FLAG_HUNK_TILED = 1, 2, 4, 8
+FLAG_HUNK_GROUP = 16
 # the general path's automatic hunk pair-sum form (include/hdgnn.h): tiled from nc >= 1024,
 # sorted from nc >= 384 below that, dense otherwise
 HUNK_SORTED_MIN_NC, HUNK_TILED_MIN_NC = 384, 1024
@@ -74,7 +75,7 @@ EXPORTS = ["hdg_version", "hdg_last_error", "hdg_resolve_path", "hdg_param_count
            "hdg_dp_mailbox_free", "hdg_train_step_dp", "hdg_adam_dp", "hdg_dp_allreduce",
            "hdg_pack_classes", "hdg_crc32c", "hdg_fwd_bwd_kernel_events",
            "hdg_bundle_write", "hdg_ckpt_writer_create", "hdg_ckpt_writer_submit",
-           "hdg_ckpt_writer_flush", "hdg_ckpt_writer_destroy", "hdg_memcpy_async",
+           "hdg_ckpt_writer_flush", "hdg_ckpt_writer_poll", "hdg_ckpt_writer_destroy", "hdg_memcpy_async",
            "hdg_event_create", "hdg_event_record", "hdg_event_synchronize", "hdg_event_destroy"]
 
 _lib = None
@@ -132,6 +133,7 @@ def load(path=None):
                                            vp, i32, vp, i32, P(vp)]
     lib.hdg_ckpt_writer_submit.argtypes = [vp, vp, cp, cp, cp, cp, cp, i32]
     lib.hdg_ckpt_writer_flush.argtypes = [vp]
+    lib.hdg_ckpt_writer_poll.argtypes = [vp]
     lib.hdg_ckpt_writer_destroy.argtypes = [vp]
     lib.hdg_memcpy_async.argtypes = [vp, vp, ctypes.c_size_t, vp]
     lib.hdg_event_create.argtypes = [P(vp)]

@@ -89,6 +89,7 @@ class Saver(object):
         self._model = model
         self.max_to_keep = max_to_keep
         self._last = []              # prefixes saved by this Saver, oldest first
+        self._dropped = []           # prefixes whose removal is queued on the writer
         self._tmpl = None
         self._writer = None
         self._dirs = set()           # directories known to exist
@@ -124,6 +125,7 @@ class Saver(object):
         removes = []
         while self.max_to_keep and len(self._last) > self.max_to_keep:
             old = self._last.pop(0)
+            self._dropped.append(old)
             removes += [old + ".index", old + ".data-00000-of-00001"]
         text = tfckpt.state_file_text(os.path.basename(prefix),
                                       [os.path.basename(q) for q in self._last
@@ -142,13 +144,32 @@ class Saver(object):
         if not background:
             self.flush()
             return self._write(prefix, state)
+        self._check(self.writer().poll)    # an earlier background save failed: raise now
         removes, spath, text = self._book(prefix)
         self.writer().submit(prefix, state, removes, spath, text)
         return prefix
 
     def flush(self):
         if self._writer is not None:
-            self._writer.flush()
+            self._check(self._writer.flush)
+            self._dropped = []           # every queued removal has run
+
+    def _check(self, op):
+        """Run the writer's flush / poll; on a failed background job re-book the keep-list
+        from the files on disk before raising: the failed prefix (no index file: bundles
+        are written under .tmp and renamed) leaves it, and the older bundles that job
+        would have removed (it stopped before its removals) come back, oldest first, so
+        the next save's max_to_keep bookkeeping deletes them and no state file lists a
+        bundle that was never written."""
+        try:
+            op()
+        except tfckpt.CheckpointError:
+            def there(q):
+                return os.path.exists(q + ".index")
+            back = [q for q in self._dropped if there(q) and q not in self._last]
+            self._last = back + [q for q in self._last if there(q)]
+            self._dropped = []
+            raise
 
     def _write(self, prefix, state):
         self._template().write(prefix, state)

@@ -584,6 +584,11 @@ class BundleWriter(object):
         if self._h is not None and self._lib.hdg_ckpt_writer_flush(self._h):
             raise CheckpointError(self._lib.hdg_last_error().decode(errors="replace"))
 
+    def poll(self):
+        """Raise the first failure since the last flush / poll, without waiting."""
+        if self._h is not None and self._lib.hdg_ckpt_writer_poll(self._h):
+            raise CheckpointError(self._lib.hdg_last_error().decode(errors="replace"))
+
     def close(self):
         h, self._h = self._h, None
         if h is not None and self._lib.hdg_ckpt_writer_destroy(h):

@@ -68,6 +68,11 @@ typedef struct hdg_shape {
  * one sweep over blocks of the pair grid giving row and column sums together (the fused
  * kernel's pair tiles), instead of a row pass and a column pass over every pair.        */
 #define HDG_FLAG_HUNK_TILED 8
+/* HDG_FLAG_HUNK_GROUP (ABI 9): the sorted form's per-node passes as one block per unit group
+ * (their shape for nc > 512) at any nc; below that the default is one block for all 20 units,
+ * which sums each node's label walk in two halves -- the two shapes differ by fp32
+ * re-association only (a diagnostic / test flag).                                         */
+#define HDG_FLAG_HUNK_GROUP 16
 /* Without a form flag the general path picks by nc: tiled from HDG_HUNK_TILED_MIN_NC, sorted
  * from HDG_HUNK_SORTED_MIN_NC below that, dense otherwise (the measured crossovers at the
  * default 10% label density).                                              */
@@ -315,6 +320,10 @@ int hdg_ckpt_writer_submit(void* writer, const float* state, const char* data_pa
                            const char* index_path, const char* removes, const char* text_path,
                            const char* text, int32_t text_append);
 int hdg_ckpt_writer_flush(void* writer);
+/* the first failure since the last flush / poll without waiting for the queue (ABI 9): 0 or
+ * the failed job's code (message in hdg_last_error), reported once.  A job whose bundle
+ * write fails skips its removals and text, so the caller re-books its keep-list.        */
+int hdg_ckpt_writer_poll(void* writer);
 int hdg_ckpt_writer_destroy(void* writer);
 /* Host utility: hipMemcpyAsync (kind default) and completion events without timing, for
  * the training loop's stream-ordered reads into pinned host memory.                     */

@@ -387,3 +387,41 @@ def test_hunk_forms_deterministic_and_garbage_free(form):
     dirty.fwd_bwd(dirty.upload(cb))
     torch.cuda.synchronize()
     assert torch.equal(g1, dirty.grad) and torch.equal(p1, dirty.probs)
+
+
+@pytest.mark.parametrize("nc", [130, 300, 512])
+@pytest.mark.parametrize("v", [2, 4])
+def test_sorted_all_unit_vs_group_shape(nc, v):
+    """The sorted form's two block shapes at an Nc both handle (the all-unit kernels
+    kw_hunk_fwd_s / kw_hunk_mlpb_s, the default up to Nc 512, sum a node's label walk in two
+    halves: dense + (half 0 + half 1); the group kernels _g, forced by FLAG_HUNK_GROUP, in one
+    chain: dense + all).  They differ by fp32 re-association only: logits within 2e-6 of the
+    commit's max |logit|, each variable's gradient within 1e-5 of its max |g|, the same
+    top_ACC count -- and both match the oracle."""
+    B, ne = 2, 64
+    cb = synth_commits(B, ne, nc, 31)
+    flat = layout.init_flat(6, v)
+    outs = []
+    for fl in (SORTED, SORTED | _lib.FLAG_HUNK_GROUP):
+        eng = _engine(B, ne, nc, v, GEN, fl)
+        eng.set_params(flat)
+        eng.fwd_bwd(eng.upload(cb))
+        torch.cuda.synchronize()
+        outs.append((eng.logits.cpu().numpy().astype(np.float64),
+                     eng.grad.cpu().numpy().astype(np.float64)))
+    (l1, g1), (l2, g2) = outs
+    scale = np.maximum(1.0, np.abs(l1).max())
+    d = np.abs(l1 - l2).max()
+    _errlog.record("logits:all_vs_group", d / scale, d / (2e-6 * scale))
+    assert d <= 2e-6 * scale
+    np_ = layout.n_params(v)
+    for name, (o, shape) in layout.offsets(v).items():
+        n = int(np.prod(shape))
+        a, r = g2[o:o + n], g1[o:o + n]
+        sc = max(np.abs(r).max(), 1e-12)
+        e = np.abs(a - r).max()
+        _errlog.record("grad_all_vs_group:" + name, e / sc, e / (1e-5 * sc))
+        assert e <= 1e-5 * sc, name
+    assert _lib.trailer_count(g1[np_:]) == _lib.trailer_count(g2[np_:])
+    out, g_ref = _oracle(flat, cb, v)
+    _grad_close(g2[:np_] + _reg_grad(flat), g_ref, v)

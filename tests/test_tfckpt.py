@@ -5,6 +5,7 @@ reference snapshot); the container format is pinned piece by piece: CRC-32C know
 (RFC 3720 B.4), a Snappy stream and an SSTable assembled by hand from the published
 formats, then round trips and corruption detection.
 """
+import os
 import struct
 
 import numpy as np
@@ -295,3 +296,47 @@ def test_native_writer_order_text_and_errors(tmp_path):
     w.flush()                                                 # reported once
     assert open(res).read().endswith("Epoch 3\nafter\n")
     w.close()
+
+
+def test_background_saver_failure_surfaces_at_next_save(tmp_path):
+    """A background bundle write that fails (here: its .tmp data path is a directory) is
+    reported by the next save() -- not only at the end of training -- and the keep-list is
+    re-booked from the files on disk: the failed prefix is not listed in the state file, and
+    the older bundle that the failed job would have removed is removed by a later save."""
+    import time
+    import types
+
+    import torch
+
+    from hdgnn.model import Saver
+    v = 2
+    so = layout.state_offsets(v)
+    eng = types.SimpleNamespace(state=torch.zeros(so["len"]))
+    sv = Saver(types.SimpleNamespace(engine=eng, variant=v), max_to_keep=2)
+    pre = str(tmp_path / "g2g.model")
+    st = np.zeros(so["len"], np.float32)
+    for step in (1, 2):
+        sv.save(None, pre, global_step=step, background=True, state=st + step)
+    sv.flush()
+    # step 3 cannot be written; its job would have removed bundle 1
+    os.makedirs(pre + "-3.data-00000-of-00001.tmp")
+    sv.save(None, pre, global_step=3, background=True, state=st + 3)
+    with pytest.raises(tfckpt.CheckpointError):
+        sv.flush()
+    assert not os.path.exists(pre + "-3.index")
+    assert os.path.exists(pre + "-1.index")    # the failed job stopped before its removals
+    assert sv._last == [pre + "-1", pre + "-2"]
+    sv.save(None, pre, global_step=4, background=True, state=st + 4)
+    sv.flush()
+    assert not os.path.exists(pre + "-1.index")   # re-booked: removed now
+    assert os.path.exists(pre + "-2.index") and os.path.exists(pre + "-4.index")
+    assert tfckpt.latest(str(tmp_path)) == "g2g.model-4"
+    assert "g2g.model-3" not in open(tmp_path / "checkpoint").read()
+    # the next save() itself raises a failed background job's error (no flush needed)
+    os.makedirs(pre + "-5.data-00000-of-00001.tmp")
+    sv.save(None, pre, global_step=5, background=True, state=st + 5)
+    time.sleep(1.0)                            # the writer thread reaches the failure
+    with pytest.raises(tfckpt.CheckpointError):
+        sv.save(None, pre, global_step=6, background=True, state=st + 6)
+    assert sv._last == [pre + "-2", pre + "-4"]
+    sv.flush()
