@@ -21,7 +21,7 @@ pmc() {   # pmc <name> <counters...>
   local name=$1
   shift
   timeout -k 5 -s KILL 180 rocprofv3 --pmc "$@" -f csv -d "$OUT/$name" -o run -- \
-      python3 $BENCH --steps 3 --warmup 1 --no-graph > "$OUT/bench_$name.log" 2>&1 || exit $?
+      python3 $BENCH --steps 3 --warmup 1 --no-graph --no-steady > "$OUT/bench_$name.log" 2>&1 || exit $?
   echo "$TAG $name ok"
 }
 pmc fetch FETCH_SIZE
