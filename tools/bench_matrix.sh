@@ -7,9 +7,9 @@ source "$R/tools/configs.sh"
 mkdir -p gpurun_out/matrix
 run() {   # run <tag> <bench args...>
   local tag=$1; shift
-  timeout -k 10 300 python bench.py --no-cpu --e2e 0 --steps 20 --warmup 3 "$@" > gpurun_out/matrix/$tag.log 2>&1
+  timeout -k 10 300 python bench.py --no-cpu --e2e 0 --steps 20 --warmup 5 "$@" > gpurun_out/matrix/$tag.log 2>&1
   local rc=$?
-  echo "$tag rc=$rc $(grep -h '^{' gpurun_out/matrix/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms/step")' 2>/dev/null)"
+  echo "$tag rc=$rc $(grep -h '^{' gpurun_out/matrix/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms/step; steady", (d.get("steady_state") or {}).get("value"))' 2>/dev/null)"
   [ $rc -eq 0 ] || exit $rc
 }
 for t in ${*:-$ORDER}; do
