@@ -73,6 +73,9 @@ def _evaluation_funcs():
         return metrics
 
 
+_COUNT_W = np.array([1, 1 << 16, 1 << 32], dtype=np.int64)   # trailer count parts
+
+
 class Saver(object):
     """tf.train.Saver() of build_model (model_2.py:139): every variable of the graph
     (tf.global_variables() at that point: the model's weights) saved
@@ -90,6 +93,7 @@ class Saver(object):
         self.max_to_keep = max_to_keep
         self._last = []              # prefixes saved by this Saver, oldest first
         self._dropped = []           # prefixes whose removal is queued on the writer
+        self._splits = {}            # prefix -> (directory, basename)
         self._tmpl = None
         self._writer = None
         self._dirs = set()           # directories known to exist
@@ -115,10 +119,21 @@ class Saver(object):
             os.makedirs(d, exist_ok=True)
             self._dirs.add(d)
 
+    def _split(self, prefix):
+        """(directory, basename) of a prefix, memoised (the training loop books one save
+        per epoch against the same few prefixes)."""
+        r = self._splits.get(prefix)
+        if r is None:
+            if len(self._splits) > 4096:
+                self._splits.clear()
+            d, base = os.path.split(prefix)
+            r = self._splits[prefix] = (d or ".", base)
+        return r
+
     def _book(self, prefix):
         """max_to_keep bookkeeping of a save at prefix: (paths to delete, state-file path,
         state-file text)."""
-        d = os.path.dirname(prefix) or "."
+        d, base = self._split(prefix)
         if prefix in self._last:
             self._last.remove(prefix)
         self._last.append(prefix)
@@ -127,10 +142,8 @@ class Saver(object):
             old = self._last.pop(0)
             self._dropped.append(old)
             removes += [old + ".index", old + ".data-00000-of-00001"]
-        text = tfckpt.state_file_text(os.path.basename(prefix),
-                                      [os.path.basename(q) for q in self._last
-                                       if (os.path.dirname(q) or ".") == d])
-        return removes, os.path.join(d, "checkpoint"), text
+        kept = [b for dq, b in map(self._split, self._last) if dq == d]
+        return removes, os.path.join(d, "checkpoint"), tfckpt.state_file_text(base, kept)
 
     def save(self, sess, save_path, global_step=None, background=False, state=None):
         """background=True: the writer thread writes the bundle of this state (a host copy
@@ -140,7 +153,7 @@ class Saver(object):
         statistics), instead of a fresh device read."""
         prefix = save_path if global_step is None else "%s-%d" % (save_path, int(global_step))
         state = self._host_state() if state is None else state
-        self._mkdir(os.path.dirname(prefix) or ".")
+        self._mkdir(self._split(prefix)[0])
         if not background:
             self.flush()
             return self._write(prefix, state)
@@ -435,8 +448,8 @@ class graph2graph(object):
                                                          # prints nan as the reference would
             tr_loss_Hedge = float(host[:nb, 0].sum())
             tr_loss_map = float(host[:nb, 1].sum())
-            correct = sum(int(round(r[4])) + (int(round(r[5])) << 16) + (int(round(r[6])) << 32)
-                          for r in host[:nb])
+            # the trailer's three 16-bit count parts per step, summed exactly in int64
+            correct = int((np.rint(host[:nb, 4:7]).astype(np.int64) * _COUNT_W).sum())
             state = hst[i % 3].numpy()
             if nb:
                 self.loss_Hedge_mse, self.loss_map, self.loss_para = (float(host[nb - 1, 0]),
