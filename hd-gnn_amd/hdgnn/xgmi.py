@@ -31,18 +31,18 @@ SELFTEST_WAIT_S = 5.0
 
 
 def device_identity(device):
-    """A string naming the physical GPU behind `device` (its UUID when torch reports one,
-    else the PCI location, else the index): equal for two ranks on the same GPU.  A CPU
-    device (the set-up protocol's tests) names the process: never shared."""
+    """A string naming the physical GPU behind `device`: its UUID and PCI location as torch
+    reports them (every one available, so a runtime that leaves the UUID blank or equal on
+    all GPUs still tells them apart by bus), else its index: equal for two ranks on the
+    same GPU.  A CPU device (the set-up protocol's tests) names the process: never shared."""
     device = torch.device(device)
     if device.type != "cuda":
         return "%s:pid%d" % (device.type, os.getpid())
     p = torch.cuda.get_device_properties(device)
-    for attr in ("uuid", "pci_bus_id"):
-        v = getattr(p, attr, None)
-        if v is not None and str(v):
-            return "%s:%s:%s" % (attr, getattr(p, "pci_domain_id", ""), v)
-    return "index:%d" % device.index
+    parts = ["%s=%s" % (a, getattr(p, a)) for a in ("uuid", "pci_domain_id", "pci_bus_id",
+                                                    "pci_device_id")
+             if getattr(p, a, None) is not None and str(getattr(p, a))]
+    return ";".join(parts) if parts else "index:%d" % device.index
 
 
 class XgmiGroup:
