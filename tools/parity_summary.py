@@ -14,8 +14,7 @@ def main(src, dst):
     for r in rows:
         f = r["test"].split("::")[0].split("/")[-1]
         q = r["quantity"]
-        q = "grad:*" if q.startswith("grad:") else ("free_weights@50:*" if q.startswith(
-            "free_weights@50:") else q)
+        q = q.split(":")[0] + ":*" if ":" in q else q    # per-variable records: one row
         k = (f, q)
         w = worst.get(k)
         if w is None:
