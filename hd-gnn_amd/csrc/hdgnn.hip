@@ -3337,13 +3337,14 @@ __global__ __launch_bounds__(1024) void k_dp_tail(const float* __restrict__ src,
 }
 
 // k_dp_tail's SUM / GRAD modes for ranks that share a device (hdg_dp.flags HDG_DP_SHARED):
-// HDG_DP_SHARED_BLOCKS blocks per rank, block b owning the slot groups b, b + G, ... .  A
+// G blocks per rank (dp_shared_grid: (W - 1) G <= CUs / 2, G >= HDG_DP_SHARED_BLOCKS),
+// block b owning the slot groups b, b + G, ... .  A
 // block first sends the words of all its groups (the values are src[p], the epoch of group
 // k is ep[k] + 1 as in k_dp_tail), then receives, sums and updates its groups in order:
 // the same words, tags, rank-order sums and Adam arithmetic as one k_dp_tail block per
 // group, so the two kernels give the same bits and keep the same per-group launch counters.
 // Only G blocks per rank spin, so the W-1 ranks waiting for the last one cover at most
-// (W-1)*G CUs and the last rank's step kernel always finds CUs to run on.
+// half the CUs and the last rank's step kernel always finds CUs to run on.
 template <int MODE>
 __global__ __launch_bounds__(DP_NT_LIGHT) void k_dp_tail_shared(
     const float* __restrict__ src, const int np, const int glen, float* __restrict__ gout,
@@ -4499,9 +4500,15 @@ int dp_args(const hdg_dp* dp, DpArgs& a) {
   return 0;
 }
 bool dp_shared(const hdg_dp* dp) { return (dp->flags & HDG_DP_SHARED) != 0; }
-unsigned dp_shared_grid(int n) {
+// blocks per rank of the shared-device tail: as many as keep the W - 1 waiting ranks'
+// spinning blocks on at most half of the CUs (at least HDG_DP_SHARED_BLOCKS: 15 x 8 = 120
+// <= 128 at HDG_DP_MAX_WORLD), at most one per slot group
+unsigned dp_shared_grid(int n, int world) {
   const int groups = (n + RED_P - 1) / RED_P;
-  return (unsigned)(groups < HDG_DP_SHARED_BLOCKS ? groups : HDG_DP_SHARED_BLOCKS);
+  const int cus = cu_count() > 0 ? cu_count() : 256;
+  int g = cus / (2 * (world > 1 ? world - 1 : 1));
+  if (g < HDG_DP_SHARED_BLOCKS) g = HDG_DP_SHARED_BLOCKS;
+  return (unsigned)(groups < g ? groups : g);
 }
 float* dp_aux(const hdg_dp* dp) {
   return (float*)((char*)dp->mailbox[dp->rank] + dpk::OFF_AUX);
@@ -4518,7 +4525,7 @@ int hdg_dp_allreduce(const hdg_dp* dp, const float* in, float* out, int32_t n, u
     return fail(HDG_EINVAL, "hdg_dp_allreduce: NULL buffer or n=%d outside [1, %d]", n,
                 HDG_DP_MAX_LEN);
   if (dp_shared(dp))
-    hipLaunchKernelGGL(k_dp_tail_shared<dpk::SUM>, dim3(dp_shared_grid(n)), dim3(DP_NT_LIGHT), 0,
+    hipLaunchKernelGGL(k_dp_tail_shared<dpk::SUM>, dim3(dp_shared_grid(n, a.world)), dim3(DP_NT_LIGHT), 0,
                        (hipStream_t)stream, in, 0, n, out, nullptr, nullptr, nullptr, nullptr,
                        nullptr, 0.f, 0.f, nullptr, status, a);
   else
@@ -4544,7 +4551,7 @@ int hdg_adam_dp(const hdg_shape* s, hdg_state* state, const float* grad_local, f
   hipLaunchKernelGGL(k_dp_aux, dim3(1), dim3(1024), 0, st, state->params, np, state->beta_pow,
                      aux);
   if (dp_shared(dp))
-    hipLaunchKernelGGL(k_dp_tail_shared<dpk::GRAD>, dim3(dp_shared_grid(glen)), dim3(DP_NT_LIGHT),
+    hipLaunchKernelGGL(k_dp_tail_shared<dpk::GRAD>, dim3(dp_shared_grid(glen, a.world)), dim3(DP_NT_LIGHT),
                        0, st, grad_local, np, glen, grad_out, state->params, state->adam_m,
                        state->adam_v, state->beta_pow, aux, lr, 1.f / pair_count(s), stats,
                        status, a);

@@ -130,8 +130,8 @@ class XgmiGroup:
             grp.dp.wait_ticks = int(wait_s * TICKS_PER_S)
             cls.verdict = ("passed: exact rank-order sums of %d floats over %d ranks through "
                            "the mailboxes%s" % (_lib.DP_MAX_LEN, world,
-                                                " (ranks share a device: %d light tail blocks "
-                                                "per rank)" % _lib.DP_SHARED_BLOCKS
+                                                " (ranks share a device: light tails, the "
+                                                "waiting ranks on at most half the CUs)"
                                                 if shared else ""))
             return grp
 

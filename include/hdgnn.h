@@ -274,12 +274,12 @@ typedef struct hdg_dp {
  * nothing else needs that CU, but a peer rank on the SAME device still has to place its
  * step kernel, whose 1024-thread blocks each take a whole CU (all VGPRs, up to all of the
  * LDS).  The tails of W-1 waiting ranks must therefore never cover every CU: with this
- * flag every exchange runs as HDG_DP_SHARED_BLOCKS light blocks per rank that loop over
- * the slot groups (all of a block's words sent first, then its groups received in order),
- * and the fused path reduces its partial rows with the non-spinning k_grad_reduce before
- * the exchange (hdg_fwd_bwd -> hdg_adam_dp) instead of inside the spinning tail.  At most
- * (HDG_DP_MAX_WORLD - 1) * HDG_DP_SHARED_BLOCKS = 120 spinning blocks per device.  Same
- * bits as the one-rank-per-device calls.                                               */
+ * flag every exchange runs as G light blocks per rank that loop over the slot groups (all
+ * of a block's words sent first, then its groups received in order), G chosen so that the
+ * W-1 waiting ranks hold at most half of the device's CUs (G >= HDG_DP_SHARED_BLOCKS:
+ * (HDG_DP_MAX_WORLD - 1) * 8 = 120 <= 128), and the fused path reduces its partial rows
+ * with the non-spinning k_grad_reduce before the exchange (hdg_fwd_bwd -> hdg_adam_dp)
+ * instead of inside the spinning tail.  Same bits as the one-rank-per-device calls.    */
 #define HDG_DP_SHARED 1
 #define HDG_DP_SHARED_BLOCKS 8
 
