@@ -362,6 +362,11 @@ __host__ __device__ inline ListLayout ylist_layout(int B, int Ne, int Nc, bool e
   return Y;
 }
 
+// model_4, after everything above (kw_prep_order; the entity-edge kernels' dispatch orders):
+//   the commits by decreasing relation rows, u32 [B4] (B4 = B rounded up to 4; kw_ee_clsb),
+//   the (commit, 32-row tile) pairs b * te + T by decreasing work, u32 [te B] (kw_ee_fwd)
+constexpr int EE_ORDER_MAX = 12288;   // te B: kw_prep_order's LDS rank table; blockIdx order beyond
+
 // per-block partial gradient rows: segment s holds n consecutive parameters starting at
 // flat index p0, laid out [n][rows] at part + off
 constexpr int MAXSEG = 16;
@@ -1112,7 +1117,8 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
                                                  const float* __restrict__ D, int Ne, int Nc,
                                                  const float* __restrict__ rho,
                                                  const float* __restrict__ gmm,
-                                                 unsigned long long* __restrict__ ncpart) {
+                                                 unsigned long long* __restrict__ ncpart,
+                                                 int snake, const uint32_t* __restrict__ sorder) {
 #pragma clang fp contract(off)
   (void)W;
   (void)o;
@@ -1122,9 +1128,18 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   float* gdl = gl + Ne * H;                                                   // gam + d
   EE_STAMP(0);
   WSTAMP(5, 0);
-  const int b = blockIdx.y, t0 = blockIdx.x * TF;
+  int b = blockIdx.y, tile = blockIdx.x;
+  if (snake > 0) {   // (b, tile) by the dispatch order (the note above kw_ee_clsb)
+    const int te = gridDim.x, total = te * gridDim.y, i = blockIdx.y * te + blockIdx.x;
+    const int r = i / snake, q = i - r * snake;
+    const int len = total - r * snake < snake ? total - r * snake : snake;
+    const int sg = (int)sorder[r * snake + ((r & 1) ? len - 1 - q : q)];   // (kw_prep_order)
+    b = sg >= 0 && sg < total ? sg / te : 0;
+    tile = sg >= 0 && sg < total ? sg - b * te : 0;
+  }
+  const int t0 = tile * TF;
   const int t = threadIdx.x, lane = t & 63, wv = uni(t >> 6), half = lane >> 5;
-  unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + blockIdx.x) * 2 * Nc;
+  unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + tile) * 2 * Nc;
   const float* rb = rho + (size_t)b * Ne * H;
   const float* gb = gmm + (size_t)b * Ne * H;
   // the gam table (Ne H <= 4 NTP float4 for Ne <= EE_TAB_LDS_MAX) is fetched in one batch of
@@ -3722,16 +3737,29 @@ __device__ __forceinline__ float quarters_sum(float v) {
   return x + y;
 }
 
+// Dispatch order.  A block's work is its commit's relation rows, rows_b = ceil(n_b (n_b - 1)
+// / (Ne - 1)), which varies 4x over the glide commits (n 100..200); the blocks of one launch
+// are all resident (3 per CU), so the kernel ends with the CU that drew the most rows (wave
+// times: median 24.8 us, max 36.7 us, in blockIdx order).  With `snake` = the CU count, block
+// i takes the segment (commit, tile) of rank s in the order of decreasing rows, s snaking
+// over the dispatch rounds of `snake` blocks (round r = i / snake: even rounds in order, odd
+// rounds reversed), so that a CU's first block (one of the heaviest) pairs with a light
+// second block.  Every (commit, tile) still runs in one block, so the sums are the same bits
+// in any order.  snake = 0: blockIdx order.
+__device__ __forceinline__ int ee_rows(int n, int Ne) {
+  n = n < 0 ? 0 : (n > Ne ? Ne : n);
+  if (n < 2) return 0;
+  const int r = (n * (n - 1) + Ne - 2) / (Ne - 1);
+  return r < Ne ? r : Ne;
+}
+
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw_ee_clsb(
-    const uint32_t* __restrict__ abits, const uint32_t* __restrict__ aT,
-    const int32_t* __restrict__ hidg, const int32_t* __restrict__ nleng,
-    const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int Nc,
+    const uint32_t* __restrict__ aT, const int32_t* __restrict__ hidg,
+    const int32_t* __restrict__ nleng, const float* __restrict__ D, int Ne, int Nc, int snake,
+    const uint32_t* __restrict__ order,
     const float* __restrict__ rho, const float* __restrict__ gmm, const float* __restrict__ dn,
     float* __restrict__ drho, float* __restrict__ dgam, float* __restrict__ part, Segs sg) {
 #pragma clang fp contract(off)
-  (void)abits;
-  (void)W;
-  (void)o;
   extern __shared__ float dyn[];                  // Eq[Ne] | a^T words [WE][TB]
   __shared__ __attribute__((aligned(16))) float os_[CHM * H];
   __shared__ float buf[NW * TB * HP];
@@ -3742,13 +3770,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
   __shared__ float zred[NW * 4 * H];
   __shared__ float4 gl4[(H / 4) * TB];            // the columns' gam rows, [v][column]
   __shared__ float4 gdl4[(H / 4) * TB];           // gam + d
-  const int b = blockIdx.y, t0 = blockIdx.x * TB, te = gridDim.x;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int te = gridDim.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int WE = (Ne + 31) >> 5;
+  int b = blockIdx.y, tile = blockIdx.x;
+  WSTAMP(14, 0);
+  if (snake > 0) {                                 // (b, tile) by the dispatch order (above)
+    const int B = gridDim.y, total = te * B, i = blockIdx.y * te + blockIdx.x;
+    const int r = i / snake, q = i - r * snake;
+    const int len = total - r * snake < snake ? total - r * snake : snake;
+    const int s = r * snake + ((r & 1) ? len - 1 - q : q);
+    const int cr = s / te;                         // commit rank, by decreasing rows
+    tile = s - cr * te;
+    const int ob = (int)order[cr];                 // (kw_prep_order)
+    b = ob >= 0 && ob < B ? ob : 0;
+  }
+  const int t0 = tile * TB;
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
   const int nrel = n >= 2 ? n * (n - 1) : 0;
   const int dn1 = n - 1 > 0 ? n - 1 : 1;
-  const int WE = (Ne + 31) >> 5;
   float* Eq = dyn;
   uint32_t* abl = reinterpret_cast<uint32_t*>(dyn + Ne);
   for (int e = t; e < Ne; e += NT) {
@@ -3779,12 +3819,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
   int kst[2] = {-1, -1};
   // rows holding relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
-  float* rowp = drho + ((size_t)(b * te + blockIdx.x) * Ne) * H;   // this tile's partial rows
+  float* rowp = drho + ((size_t)(b * te + tile) * Ne) * H;   // this tile's partial rows
   for (int e = rows * H + t; e < Ne * H; e += NT) rowp[e] = 0.f;   // rows past the relations
   const float* rb = rho + (size_t)b * Ne * H;
   const float inv = 1.f / (float)dn1;
   const bool aligned = n == Ne;
   __syncthreads();                                 // Eq, abl, cl, gl4, gdl4
+  WSTAMP(14, 1);
   for (int c0 = 0; c0 < rows; c0 += CHM) {
     const int c1 = c0 + CHM < rows ? c0 + CHM : rows;
     __syncthreads();
@@ -3795,6 +3836,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
                    rowp, acc0, acc1, ag, sdl, zr, kst);
   }
   prio0_e();
+  WSTAMP(14, 2);
   for (int e = lane; e < 4 * H; e += 64) zred[wv * 4 * H + e] = 0.f;
   __syncthreads();
 #pragma unroll
@@ -3838,7 +3880,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
   }
   v[20] = sdl;
   block_sum<21>(v, red, tot);
-  const int row = b * te + blockIdx.x;
+  const int row = b * te + tile;
   if (t < H) {
     // sum_pairs relu(kappa_k) dz1 = sum_i rho_ik R_ik + sum_j gam_jk C_jk + d_k sum_{a=1} s_k dz1
     // (kappa = rho + gam + a d; R, C the row / column sums of s dz1)
@@ -3868,6 +3910,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
     put(part, sb, 3 * H, row, -tot[20]);
     put(part, sb, 3 * H + 1, row, tot[20]);
   }
+  WSTAMP(14, 3);
 }
 
 // ---------------------------------------------------------------------------------
@@ -4328,8 +4371,53 @@ __global__ __launch_bounds__(NT) void kw_prep_lists(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------
+// kw_prep_order  grid (1), 1024 threads, dynamic LDS te B ints: the entity-edge kernels'
+// dispatch orders (ranks by decreasing work, ties by index; the layout note above):
+// kw_ee_clsb's commits by relation rows, kw_ee_fwd's (commit, tile) pairs by their walk
+// length (n for a tile holding index rows, T * TF < n; 0 for the others)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void rank_desc(const int* key, int N, uint32_t* __restrict__ out) {
+  for (int e = threadIdx.x; e < N; e += blockDim.x) {
+    const int re = key[e];
+    int rank = 0;
+    for (int f = 0; f < N; ++f) {
+      const int rf = key[f];
+      rank += (rf > re || (rf == re && f < e)) ? 1 : 0;
+    }
+    out[rank] = (uint32_t)e;
+  }
+}
+__global__ __launch_bounds__(1024) void kw_prep_order(const int32_t* __restrict__ nleng, int B,
+                                                      int Ne, uint32_t* __restrict__ order) {
+  extern __shared__ int rk[];
+  const int te = ee_fwd_tiles(Ne), N = te * B;
+  for (int e = threadIdx.x; e < B; e += blockDim.x) rk[e] = ee_rows(nleng[e], Ne);
+  __syncthreads();
+  rank_desc(rk, B, order);
+  __syncthreads();
+  for (int e = threadIdx.x; e < N; e += blockDim.x) {
+    const int b = e / te, T = e - b * te;
+    int n = nleng[b];
+    n = n < 0 ? 0 : (n > Ne ? Ne : n);
+    rk[e] = (n >= 2 && T * TF < n) ? n : 0;
+  }
+  __syncthreads();
+  rank_desc(rk, N, order + ((B + 3) & ~3));
+}
+
+// ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
+bool has_ee(int v);
+bool hunk_lists(const hdg_shape* s);
+bool has_ent(int v);
+// the prep words before the entity-edge order table (= the whole prep without model_4)
+size_t ee_order_off(const hdg_shape* s) {
+  const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
+  if (hunk_lists(s)) return ylist_layout(s->batch, s->ne, s->nc, has_ent(s->variant)).end;
+  if (has_ent(s->variant)) return list_layout(s->batch, s->ne, s->nc).end;
+  return B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC;
+}
 struct WideWork {
   size_t xp, ov, P, Eb, hE, rhoE;                 // entity stage   [B][Ne](*H)
   size_t R1, C1, Rn, Cn, rho, gmm, drho, dgam, phi, psi;   // EE     [B][Ne][H]
@@ -4479,23 +4567,44 @@ int set_wide_attrs() {
   return 0;
 }
 
+// the entity-edge kernels' dispatch order: snaking over rounds of one block per CU (the note
+// above kw_ee_clsb), the ranks from the batch's prep (kw_prep_order); 0: blockIdx order
+#ifndef HDG_EE_SNAKE
+#define HDG_EE_SNAKE 1
+#endif
+int ee_snake(const hdg_shape* s) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+              ? n : 0;
+  }
+  return (HDG_EE_SNAKE && (long long)ee_fwd_tiles(s->ne) * s->batch <= EE_ORDER_MAX) ? cus : 0;
+}
+size_t ee_clsb_lds(int Ne) { return (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4; }   // Eq | a^T words
+
 // kw_ee_fwd over the batch: both LDS tables up to EE_TAB_LDS_MAX nodes, the gam table alone
 // while it fits the LDS, HBM reads beyond
+int ee_snake(const hdg_shape* s);
+size_t ee_order_off(const hdg_shape* s);
 int launch_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, const float* D,
                   const float* rho, const float* gmm, unsigned long long* ncpart, hipStream_t st) {
   const int B = s->batch, Ne = s->ne, Nc = s->nc;
   const Off o = param_offsets(s->variant);
   const dim3 grid(ee_fwd_tiles(Ne), B);
   const int tm = ee_fwd_mode(Ne, Nc);
+  const int snake = ee_snake(s);
+  const uint32_t* sorder = (const uint32_t*)bt->prep + ee_order_off(s) + ((B + 3) & ~3);
   if (tm == 1)
     hipLaunchKernelGGL(kw_ee_fwd<1>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
-                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
   else if (tm == 2)
     hipLaunchKernelGGL(kw_ee_fwd<2>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
-                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
   else
     hipLaunchKernelGGL(kw_ee_fwd<0>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
-                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart);
+                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
   WTRY(kmark("kw_ee_fwd", st));
   return 0;
 }
@@ -4547,10 +4656,10 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const int te = (Ne + TN - 1) / TN;
   float* part = ws;
   if (int rc = set_wide_attrs()) return rc;
-  const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-  hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
-                     aT, bt->hid, bt->nlen, params, o, ws + w.D, Ne, Nc, F(w.rho), F(w.gmm),
-                     F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
+  const int snake = ee_snake(s);
+  hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), ee_clsb_lds(Ne), st, aT,
+                     bt->hid, bt->nlen, ws + w.D, Ne, Nc, snake, prep + ee_order_off(s), F(w.rho),
+                     F(w.gmm), F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
   WTRY(kmark("kw_ee_clsb", st));
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
                      ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
@@ -4590,10 +4699,9 @@ void wide_prep_counts_layout(const hdg_shape* s, int64_t* stride, int64_t* ks, i
 }
 
 size_t wide_prep_bytes(const hdg_shape* s) {
-  const size_t B = s->batch, WE = (s->ne + 31) / 32, WC = (s->nc + 31) / 32;
-  if (hunk_lists(s)) return ylist_layout(s->batch, s->ne, s->nc, has_ent(s->variant)).end * 4;
-  if (has_ent(s->variant)) return list_layout(s->batch, s->ne, s->nc).end * 4;
-  return (B * gen_prep(s->ne, s->nc).words + B * s->ne * WE + B * s->nc * WC) * 4;
+  const size_t words = ee_order_off(s);
+  const size_t ord = (((size_t)s->batch + 3) & ~(size_t)3) + (size_t)ee_fwd_tiles(s->ne) * s->batch;
+  return (has_ee(s->variant) ? words + ord : words) * 4;
 }
 
 int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
@@ -4619,6 +4727,12 @@ int wide_prepare(const hdg_shape* s, const hdg_batch* bt, hipStream_t st) {
                        bt->ybits, yT, (uint32_t*)bt->prep, s->nc,
                        ylist_layout(s->batch, s->ne, s->nc, has_ent(s->variant)));
     WTRY(kmark("kw_prep_lists", st));
+  }
+  if (has_ee(s->variant) && ee_snake(s) > 0) {   // the entity-edge kernels' dispatch orders
+    hipLaunchKernelGGL(kw_prep_order, dim3(1), dim3(1024),
+                       (size_t)ee_fwd_tiles(s->ne) * s->batch * 4, st, bt->nlen, s->batch, s->ne,
+                       (uint32_t*)bt->prep + ee_order_off(s));
+    WTRY(kmark("kw_prep_order", st));
   }
   return 0;
 }
@@ -4873,10 +4987,10 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     WTRY(kmark("kw_node_bwd", st));
   }
   if (ee) {
-    const size_t lds = (size_t)(Ne + TB * ((Ne + 31) / 32)) * 4;   // Eq | a^T tile words
-    hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), lds, st, bt->abits,
-                       aT, bt->hid, bt->nlen, params, o, D, Ne, Nc, F(w.rho), F(w.gmm), F(w.dn),
-                       F(w.drho), F(w.dgam), part, w.segs);
+    const int snake = ee_snake(s);
+    hipLaunchKernelGGL(kw_ee_clsb, dim3(ee_bwd_tiles(Ne), B, 1), dim3(NT), ee_clsb_lds(Ne), st,
+                       aT, bt->hid, bt->nlen, D, Ne, Nc, snake, prep + ee_order_off(s), F(w.rho),
+                       F(w.gmm), F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
     WTRY(kmark("kw_ee_clsb", st));
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, D, Ne,
                        ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
