@@ -12,9 +12,15 @@ for tag in "$@"; do
       || { tail -30 gpurun_out/clsb/$tag.tests.log; exit 1; }
   echo "$tag tests: $(tail -1 gpurun_out/clsb/$tag.tests.log)"
 done
+if [ -n "$M2" ]; then   # M2=1: model_2 general-path lines too
+  CFGS=("glide:--variant 4" "general:--variant 4 --path 2" "stress:--variant 4 --ne 1024 --nc 512 --batch 32"
+        "m2gen:--variant 2 --path 2" "m2stress:--variant 2 --ne 1024 --nc 512 --batch 32")
+else
+  CFGS=("glide:--variant 4" "general:--variant 4 --path 2" "stress:--variant 4 --ne 1024 --nc 512 --batch 32")
+fi
 for rep in 1 2; do
   for tag in orig "$@"; do
-    for cfg in "glide:--variant 4" "general:--variant 4 --path 2" "stress:--variant 4 --ne 1024 --nc 512 --batch 32"; do
+    for cfg in "${CFGS[@]}"; do
       name=${cfg%%:*}; args=${cfg#*:}
       HDG_LIB_PATH=$(lp $tag) timeout -k 10 200 python bench.py --no-cpu --e2e 0 --steps 20 --warmup 5 $args \
           > gpurun_out/clsb/$tag.$name.log 2>&1 || { tail -5 gpurun_out/clsb/$tag.$name.log; exit 1; }
@@ -22,7 +28,7 @@ for rep in 1 2; do
 import json, sys
 d = json.loads(sys.stdin.read()); s = d.get("steady_state") or {}; k = d["kernels_ms"]
 print(sys.argv[1], sys.argv[2], d["value"], d["ms_per_step"], "steady", s.get("value"), s.get("ms_per_step"),
-      "clsb", k.get("kw_ee_clsb"), "nodeb", k.get("kw_ee_nodeb"), "radam", k.get("kw_reduce_adam"))' $tag $name
+      "clsb", k.get("kw_ee_clsb"), "eefwd", k.get("kw_ee_fwd"), "scan", k.get("kw_scan"))' $tag $name
     done
   done
 done
