@@ -3819,8 +3819,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
   int kst[2] = {-1, -1};
   // rows holding relations r < nrel
   const int rows = nrel > 0 ? ((nrel + Ne - 2) / (Ne - 1) < Ne ? (nrel + Ne - 2) / (Ne - 1) : Ne) : 0;
-  float* rowp = drho + ((size_t)(b * te + tile) * Ne) * H;   // this tile's partial rows
-  for (int e = rows * H + t; e < Ne * H; e += NT) rowp[e] = 0.f;   // rows past the relations
+  // this tile's partial rows; the rows past the relations are not written (kw_ee_nodeb reads
+  // them as 0)
+  float* rowp = drho + ((size_t)(b * te + tile) * Ne) * H;
   const float* rb = rho + (size_t)b * Ne * H;
   const float inv = 1.f / (float)dn1;
   const bool aligned = n == Ne;
@@ -3920,6 +3921,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void kw
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void kw_ee_nodeb(
     const float* __restrict__ W, Off o, const float* __restrict__ D, int Ne, int np,
+    const int32_t* __restrict__ nleng,
     const float* __restrict__ R1,
     const float* __restrict__ C1, const float* __restrict__ Rn, const float* __restrict__ Cn,
     const float* __restrict__ drho, const float* __restrict__ dgam, float* __restrict__ phi,
@@ -3969,7 +3971,10 @@ __global__ __launch_bounds__(NT) void kw_ee_nodeb(
   {
     const float* src = drho + ((size_t)b * np * Ne + t0) * H + t;
     const size_t sq = (size_t)Ne * H;
-    const int nin = (Ne - t0) * H;                    // elements e < nin are in range
+    // elements e < nin are in range and hold relations (kw_ee_clsb writes no row past the
+    // commit's relation rows: they are 0)
+    const int rl = ee_rows(nleng[b], Ne) < Ne ? ee_rows(nleng[b], Ne) : Ne;
+    const int nin = rl > t0 ? (rl - t0) * H : 0;
     for (int q = 0; q < np; q += 8) {                 // 8 tiles' loads in flight, summed in order
       float v[NE_IT][8];
 #pragma unroll
@@ -4662,7 +4667,7 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
                      F(w.gmm), F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
   WTRY(kmark("kw_ee_clsb", st));
   hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, ws + w.D, Ne,
-                     ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
+                     ee_bwd_tiles(Ne), bt->nlen, F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
                      F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
   WTRY(kmark("kw_ee_nodeb", st));
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
@@ -4993,7 +4998,7 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
                        F(w.gmm), F(w.dn), F(w.drho), F(w.dgam), part, w.segs);
     WTRY(kmark("kw_ee_clsb", st));
     hipLaunchKernelGGL(kw_ee_nodeb, dim3(te, B), dim3(NT), 0, st, params, o, D, Ne,
-                       ee_bwd_tiles(Ne), F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
+                       ee_bwd_tiles(Ne), bt->nlen, F(w.R1), F(w.C1), F(w.Rn), F(w.Cn), F(w.drho),
                        F(w.dgam), F(w.phi), F(w.psi), part, w.segs);
     WTRY(kmark("kw_ee_nodeb", st));
   }
