@@ -1073,6 +1073,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
 //   which leave as one partial row per tile.
 // ---------------------------------------------------------------------------------
 constexpr int TF = 32;                // index rows per kw_ee_fwd block
+#ifndef HDG_EEF_WAVES
+#define HDG_EEF_WAVES 16              // kw_ee_fwd's waves per block in table modes 2 / 0
+#endif
 constexpr int EE_TAB_LDS_MAX = 400;   // Ne up to which gam, gam + d sit in LDS
 __host__ __device__ inline int ee_fwd_tiles(int Ne) { return (Ne + TF - 1) / TF; }
 // table modes: 1 gam and gam + d in LDS (Ne <= EE_TAB_LDS_MAX), 2 gam alone in LDS (+ a d
@@ -1109,8 +1112,10 @@ __device__ unsigned long long* g_ee_stamps;
 #define EE_FLUSH() do {} while (0)
 #endif
 
-template <int TM>   // table mode (ee_fwd_mode)
-__global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ abits,
+// NWF waves per block: 8 with the LDS tables of mode 1 (3 blocks per CU), 16 in modes 2 / 0,
+// whose one block per CU (the 80 KiB gam table at Ne = 1024) otherwise ran 8 waves per CU
+template <int TM, int NWF>   // table mode (ee_fwd_mode), waves per block
+__global__ __launch_bounds__(64 * NWF) void kw_ee_fwd(const uint32_t* __restrict__ abits,
                                                  const int32_t* __restrict__ hidg,
                                                  const int32_t* __restrict__ nleng,
                                                  const float* __restrict__ W, Off o,
@@ -1120,6 +1125,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
                                                  unsigned long long* __restrict__ ncpart,
                                                  int snake, const uint32_t* __restrict__ sorder) {
 #pragma clang fp contract(off)
+  constexpr int NTF = 64 * NWF;
   (void)W;
   (void)o;
   extern __shared__ __attribute__((aligned(16))) unsigned long long bins[];   // [Nc][2] | ...
@@ -1142,17 +1148,17 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   unsigned long long* outp = ncpart + ((size_t)b * gridDim.x + tile) * 2 * Nc;
   const float* rb = rho + (size_t)b * Ne * H;
   const float* gb = gmm + (size_t)b * Ne * H;
-  // the gam table (Ne H <= 4 NTP float4 for Ne <= EE_TAB_LDS_MAX) is fetched in one batch of
+  // the gam table (Ne H <= 4 NTF float4 for Ne <= EE_TAB_LDS_MAX) is fetched in one batch of
   // float4 loads before the commit's length is known: one memory round trip for the stage
   // instead of one per loop trip, and none waiting on nleng
-  constexpr int GQ = (EE_TAB_LDS_MAX * H / 4 + NTP - 1) / NTP;
+  constexpr int GQ = (EE_TAB_LDS_MAX * H / 4 + NTF - 1) / NTF;
   const int nq = Ne * H / 4;                       // H % 4 == 0: whole float4 per row
   constexpr bool LDS = TM == 1;
   float4 gv[LDS ? GQ : 1];
   if constexpr (LDS) {
 #pragma unroll
     for (int u = 0; u < GQ; ++u) {
-      const int q = t + u * NTP;
+      const int q = t + u * NTF;
       gv[u] = q < nq ? reinterpret_cast<const float4*>(gb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
@@ -1164,20 +1170,20 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   const int htv = hb[(t >> 1) < Ne ? (t >> 1) : Ne - 1];
   int n = nleng[b];
   n = n < 0 ? 0 : (n > Ne ? Ne : n);
-  for (int c = t; c < 2 * Nc; c += NTP) bins[c] = 0ull;
+  for (int c = t; c < 2 * Nc; c += NTF) bins[c] = 0ull;
   if (n < 2 || t0 >= n) {         // block-uniform: this tile holds no index row
-    for (int c = t; c < 2 * Nc; c += NTP) outp[c] = 0ull;
+    for (int c = t; c < 2 * Nc; c += NTF) outp[c] = 0ull;
     return;
   }
-  for (int e = t; e < 2 * n; e += NTP) tsum[e] = 0.f;
+  for (int e = t; e < 2 * n; e += NTF) tsum[e] = 0.f;
   if constexpr (TM == 2) {        // gam alone: the commit's rows, float4 copies
-    for (int q = t; q < nq; q += NTP)
+    for (int q = t; q < nq; q += NTF)
       reinterpret_cast<float4*>(gl)[q] = reinterpret_cast<const float4*>(gb)[q];
   }
   if constexpr (LDS) {
 #pragma unroll
     for (int u = 0; u < GQ; ++u) {
-      const int q = t + u * NTP;
+      const int q = t + u * NTF;
       if (q < nq) {
         const float4 d = *reinterpret_cast<const float4*>(D + D_EED + (4 * q) % H);
         reinterpret_cast<float4*>(gl)[q] = gv[u];
@@ -1193,7 +1199,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   const int ip = t0 + (lane & 31);
   const bool live = ip < n;
   const int ipc = live ? ip : 0;
-  const int part = 2 * wv + half, NPART = 2 * NWP;
+  const int part = 2 * wv + half, NPART = 2 * NWF;
   const int jlo = (n * part) / NPART, jhi = (n * (part + 1)) / NPART;
   const int trips = (n + NPART - 1) / NPART;   // >= every part's length: both halves step
   const int r0 = ipc * (n - 1) + jlo - (jlo > ipc ? 1 : 0);
@@ -1296,7 +1302,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
     }
   }
   __syncthreads();
-  for (int e = t; e < 2 * n; e += NTP) {   // target bins: column j' of the tile's rows
+  for (int e = t; e < 2 * n; e += NTF) {   // target bins: column j' of the tile's rows
     const int ht = e == t ? htv : hb[e >> 1];
     if (ht >= 0 && ht < Nc) atomicAdd(&bins[2 * ht + (e & 1)], qfix(tsum[e]));
   }
@@ -1305,7 +1311,7 @@ __global__ __launch_bounds__(NTP) void kw_ee_fwd(const uint32_t* __restrict__ ab
   // atomics: the L2s of the 8 XCDs are not coherent for device-scope atomics)
   EE_STAMP(4);
   WSTAMP(5, 4);
-  for (int c = t; c < 2 * Nc; c += NTP) outp[c] = bins[c];
+  for (int c = t; c < 2 * Nc; c += NTF) outp[c] = bins[c];
   EE_FLUSH();
 }
 
@@ -4547,11 +4553,11 @@ int set_wide_attrs() {
                              96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,    // + 15 KiB static hand-over
                              hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<1>,
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<1, NWP>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<2>,
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<2, HDG_EEF_WAVES>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<0>,
+    WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<0, HDG_EEF_WAVES>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_clsb,      // 41 KiB static + 32 KiB at Ne 4096
                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
@@ -4602,14 +4608,16 @@ int launch_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, 
   const int snake = ee_snake(s);
   const uint32_t* sorder = (const uint32_t*)bt->prep + ee_order_off(s) + ((B + 3) & ~3);
   if (tm == 1)
-    hipLaunchKernelGGL(kw_ee_fwd<1>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
+    hipLaunchKernelGGL((kw_ee_fwd<1, NWP>), grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
                        bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
   else if (tm == 2)
-    hipLaunchKernelGGL(kw_ee_fwd<2>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
-                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
+    hipLaunchKernelGGL((kw_ee_fwd<2, HDG_EEF_WAVES>), grid, dim3(64 * HDG_EEF_WAVES),
+                       ee_fwd_lds(Ne, Nc), st, bt->abits, bt->hid, bt->nlen, params, o, D, Ne,
+                       Nc, rho, gmm, ncpart, snake, sorder);
   else
-    hipLaunchKernelGGL(kw_ee_fwd<0>, grid, dim3(NTP), ee_fwd_lds(Ne, Nc), st, bt->abits,
-                       bt->hid, bt->nlen, params, o, D, Ne, Nc, rho, gmm, ncpart, snake, sorder);
+    hipLaunchKernelGGL((kw_ee_fwd<0, HDG_EEF_WAVES>), grid, dim3(64 * HDG_EEF_WAVES),
+                       ee_fwd_lds(Ne, Nc), st, bt->abits, bt->hid, bt->nlen, params, o, D, Ne,
+                       Nc, rho, gmm, ncpart, snake, sorder);
   WTRY(kmark("kw_ee_fwd", st));
   return 0;
 }
