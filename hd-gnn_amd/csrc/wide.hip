@@ -3374,7 +3374,7 @@ __global__ __launch_bounds__(NT) void kw_scan(const uint32_t* __restrict__ prep,
   }
 }
 
-template <int MODE>
+template <int MODE, int HALVES>
 __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
                                                const uint32_t* __restrict__ abits,
                                                const uint32_t* __restrict__ prep,
@@ -3387,9 +3387,11 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
 #pragma clang fp contract(off)
   const GenPrep GP = gen_prep(Ne, Nc);
   const int t0 = tx * TN, te = gridDim.x, B = gridDim.y;
-  // 8 waves: wave g + 4 hw takes hidden units g; the halves hw split each lane's neighbour
-  // list (hw 1 hands its partial sums over through LDS), hw 0 also does the dense part
-  const int lane = threadIdx.x & 63, g = uni((threadIdx.x >> 6) & 3), hw = uni(threadIdx.x >> 8);
+  // 4 HALVES waves: wave g + 4 hw takes hidden units g; with HALVES = 2 the halves hw split
+  // each lane's neighbour list (hw 1 hands its partial sums over through LDS), hw 0 also
+  // does the dense part; with HALVES = 1 the 4 waves walk whole lists (no hand-off)
+  const int lane = threadIdx.x & 63, g = uni((threadIdx.x >> 6) & 3);
+  const int hw = HALVES == 2 ? uni(threadIdx.x >> 8) : 0;
   const int i = t0 + lane;
   const bool live = i < Ne;
   const int ic = live ? i : Ne - 1;
@@ -3518,7 +3520,7 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     // (one neighbour's loads then its use: 74 VGPRs, 6 waves per SIMD -- batching the row
     // loads of 4 / 8 / 16 neighbours ahead of their use measured 35.8 / 36.2 / 44.0 us
     // against 32.8 at stress, the walk wanting waves more than loads in flight)
-    for_list(prep, 0, b, i, Ne, Nc, [&](int j0) { use(j0, ldr(j0)); }, hw, 2);
+    for_list(prep, 0, b, i, Ne, Nc, [&](int j0) { use(j0, ldr(j0)); }, hw, HALVES);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       cs[2 * h] = cs2[h].x; cs[2 * h + 1] = cs2[h].y;
@@ -3528,23 +3530,25 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
     cs[4] = cst; S1[4] = s1t; S3[4] = s3t;
   }
   WSTAMP(13, 3);
-  float* hd = hand + g * 3 * KPW * TN + lane;     // hw 1's sums, added in a fixed order
-  if (hw) {
+  if constexpr (HALVES == 2) {
+    float* hd = hand + g * 3 * KPW * TN + lane;   // hw 1's sums, added in a fixed order
+    if (hw) {
+#pragma unroll
+      for (int kk = 0; kk < KPW; ++kk) {
+        hd[kk * TN] = cs[kk];
+        hd[(KPW + kk) * TN] = S1[kk];
+        hd[(2 * KPW + kk) * TN] = S3[kk];
+      }
+    }
+    __syncthreads();
+    WSTAMP(13, 4);
+    if (hw) return;                               // no barriers below
 #pragma unroll
     for (int kk = 0; kk < KPW; ++kk) {
-      hd[kk * TN] = cs[kk];
-      hd[(KPW + kk) * TN] = S1[kk];
-      hd[(2 * KPW + kk) * TN] = S3[kk];
+      cs[kk] += hd[kk * TN];
+      S1[kk] += hd[(KPW + kk) * TN];
+      S3[kk] += hd[(2 * KPW + kk) * TN];
     }
-  }
-  __syncthreads();
-  WSTAMP(13, 4);
-  if (hw) return;                                 // no barriers below
-#pragma unroll
-  for (int kk = 0; kk < KPW; ++kk) {
-    cs[kk] += hd[kk * TN];
-    S1[kk] += hd[(KPW + kk) * TN];
-    S3[kk] += hd[(2 * KPW + kk) * TN];
   }
   float v[4 * KPW];
 #pragma unroll
@@ -3582,8 +3586,12 @@ __device__ __forceinline__ void first_bwd_body(const float* __restrict__ x,
 }
 
 // grid (te, B, stages): stage mode0 + z -- 0: E1 (ra = rb = rho_E), 1: EE (phi, psi); both
-// stages of model_4's general path in one launch
-__global__ __launch_bounds__(NTP) void kw_first_bwd(const float* __restrict__ x,
+// stages of model_4's general path in one launch.  HALVES = 2 (512 threads: the neighbour
+// lists split over two wave halves) while the grid fits 3 blocks per CU; HALVES = 1 (256
+// threads, whole lists) beyond, where the 512-thread grid ran a second round of one block
+// per CU (model_4 stress: 1,024 blocks)
+template <int HALVES>
+__global__ __launch_bounds__(256 * HALVES) void kw_first_bwd(const float* __restrict__ x,
                                                    const uint32_t* __restrict__ abits,
                                                    const uint32_t* __restrict__ prep,
                                                    const float* __restrict__ W, Off o, int Ne,
@@ -3592,13 +3600,13 @@ __global__ __launch_bounds__(NTP) void kw_first_bwd(const float* __restrict__ x,
                                                    const float* __restrict__ psi,
                                                    const double* __restrict__ tab,
                                                    float* __restrict__ part, Segs sg) {
-  __shared__ float hand[NW * 3 * KPW * TN];        // hw 1's walk sums [g][3 KPW][lane]
+  __shared__ float hand[HALVES == 2 ? NW * 3 * KPW * TN : 1];   // hw 1's walk sums [g][3 KPW][lane]
   int tx, b, zz;                                   // commit b's tiles on XCD b % 8, as kw_scan's
   xcd_commit_map(tx, b, zz);                       // blocks that wrote its tables
   if (mode0 + zz == 0)
-    first_bwd_body<0>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg, hand, tx, b);
+    first_bwd_body<0, HALVES>(x, abits, prep, W, o, Ne, Nc, r0, r0, tab, part, sg, hand, tx, b);
   else
-    first_bwd_body<1>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg, hand, tx, b);
+    first_bwd_body<1, HALVES>(x, abits, prep, W, o, Ne, Nc, phi, psi, tab, part, sg, hand, tx, b);
 }
 
 // ---------------------------------------------------------------------------------
@@ -4546,12 +4554,31 @@ WideWork wide_layout(const hdg_shape* s) {
     if (e_ != hipSuccess) return fail((int)e_, "%s: %s", #expr, hipGetErrorString(e_));   \
   } while (0)
 
+// kw_first_bwd's form by its grid: the 512-thread blocks (3 per CU at 76 VGPRs) while they
+// fit one round, the 256-thread blocks (whole lists per wave) beyond
+#ifndef HDG_FB_HALVES
+#define HDG_FB_HALVES 0   // 0: by the grid; 1 / 2: forced
+#endif
+int first_bwd_halves(long long blocks) {
+  if (HDG_FB_HALVES) return HDG_FB_HALVES;
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+              ? n : 256;
+  }
+  return blocks > 3LL * cus ? 1 : 2;
+}
+
 int set_wide_attrs() {
   static bool attr_set = false;   // > 64 KiB of dynamic LDS for Ne > 4000
   if (!attr_set) {
     WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
                              96 * 1024));
-    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd,    // + 15 KiB static hand-over
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<2>,    // + 15 KiB static hand-over
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,    // + 15 KiB static hand-over
                              hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_ee_fwd<1, NWP>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -4681,9 +4708,14 @@ int wide_ee_bwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   hipLaunchKernelGGL(kw_scan, dim3(H, B, 1), dim3(NT), 0, st, prep, params, o, Ne, Nc, 1,
                      nullptr, F(w.psi), (double*)F(w.tab));
   WTRY(kmark("kw_scan", st));
-  hipLaunchKernelGGL(kw_first_bwd, dim3(te, B), dim3(NTP), sort_lds_bytes(Ne), st, bt->x,
-                     bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
-                     (const double*)F(w.tab), part, w.segs);
+  if (first_bwd_halves(te * B) == 2)
+    hipLaunchKernelGGL(kw_first_bwd<2>, dim3(te, B), dim3(NTP), sort_lds_bytes(Ne), st, bt->x,
+                       bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
+                       (const double*)F(w.tab), part, w.segs);
+  else
+    hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
+                       bt->abits, prep, params, o, Ne, Nc, 1, nullptr, F(w.phi), F(w.psi),
+                       (const double*)F(w.tab), part, w.segs);
   WTRY(kmark("kw_first_bwd", st));
   // the entity-edge parameters [EE_W11, EC_B2 + 2): one contiguous block of the flat vector
   const int p0 = o.EE_W11, n = o.EC_B2 + 2 - o.EE_W11;
@@ -5015,9 +5047,14 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
     hipLaunchKernelGGL(kw_scan, dim3(H, B, stages), dim3(NT), 0, st, prep, params, o, Ne, Nc,
                        mode0, F(w.rhoE), F(w.psi), (double*)F(w.tab));
     WTRY(kmark("kw_scan", st));
-    hipLaunchKernelGGL(kw_first_bwd, dim3(te, B, stages), dim3(NTP), tlds, st, bt->x, bt->abits,
-                       prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi), F(w.psi),
-                       (const double*)F(w.tab), part, w.segs);
+    if (first_bwd_halves(te * B * stages) == 2)
+      hipLaunchKernelGGL(kw_first_bwd<2>, dim3(te, B, stages), dim3(NTP), tlds, st, bt->x,
+                         bt->abits, prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi),
+                         F(w.psi), (const double*)F(w.tab), part, w.segs);
+    else
+      hipLaunchKernelGGL(kw_first_bwd<1>, dim3(te, B, stages), dim3(NT), tlds, st, bt->x,
+                         bt->abits, prep, params, o, Ne, Nc, mode0, F(w.rhoE), F(w.phi),
+                         F(w.psi), (const double*)F(w.tab), part, w.segs);
     WTRY(kmark("kw_first_bwd", st));
   }
   if (adam) {
