@@ -780,22 +780,27 @@ __device__ __forceinline__ float clamp_fma1(const float x, const float a, const 
 
 // MODE 0 (E1, model_2.py:161-188): P_i = sum_{j!=i} relu(z_ij) + relu(z_ji)
 // MODE 1 (EE, model_4.py:206-243): R1_i = sum_{j!=i} relu(z'_ij), C1_i = sum relu(z'_ji)
-template <int MODE>
+// HALVES = 2 (8 waves): waves g + 4 hw; the halves hw split each node's neighbour lists (hw 1
+// hands its sums over through LDS, `hand`), hw 0 also does the dense part and the stores
+template <int MODE, int HALVES>
 __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
                                                const uint32_t* __restrict__ abits,
                                                const uint32_t* __restrict__ aT,
                                                const uint32_t* __restrict__ prep,
                                                const float* __restrict__ W, const Off& o, int Ne,
                                                int Nc, float* __restrict__ out0,
-                                               float* __restrict__ out1) {
+                                               float* __restrict__ out1, float* hand) {
 #pragma clang fp contract(off)
   const GenPrep GP = gen_prep(Ne, Nc);
   const int b = blockIdx.y, t0 = blockIdx.x * TN;
-  const int lane = threadIdx.x & 63, g = uni(threadIdx.x >> 6);
-  const int i = t0 + lane;
+  const int lane = threadIdx.x & 63, g = uni((threadIdx.x >> 6) & 3);
+  const int hw = HALVES == 2 ? uni(threadIdx.x >> 8) : 0;
+  const int i0 = t0 + lane;
   extern __shared__ __attribute__((aligned(16))) double tabs_lds[];
   const SortTabs T = stage_tabs(prep, GP, b, Ne, tabs_lds, x + (size_t)b * Ne);
-  if (i >= Ne) return;   // no barriers below
+  if (HALVES == 1 && i0 >= Ne) return;   // no barriers below (HALVES = 2: one, lanes clamped)
+  const bool live = i0 < Ne;
+  const int i = live ? i0 : Ne - 1;
   const float* xb = T.xs;
   const float xi = xb[i];
   float u[KPW], v[KPW], s1[KPW], s2[KPW], c0[KPW], wa[KPW], wb[KPW], dd[KPW];
@@ -824,6 +829,7 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
   constexpr int NS = MODE == 0 ? 2 * KPW : KPW;
   bool sinc[NS];
   int sb[NS];
+  if (!hw) {
 #pragma unroll
   for (int n = 0; n < NS; ++n) sinc[n] = (MODE == 0 && n < KPW ? wb[n] : wa[n % KPW]) >= 0.f;
   set_bounds<NS>(T, sinc, sb, [&](int n, float xq) {
@@ -858,6 +864,7 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
       dense2[kk] = acc;
     }
   }
+  }   // (hw 0)
   WSTAMP(7, 1);
   // a = 1 corrections: row bits (pairs (i, j)), column bits (pairs (j, i)), one clamped
   // packed fma per two hidden units and neighbour (clamp_coef); KPW = 5: two packed
@@ -889,13 +896,30 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
       sr[0] += clamp_fma2(xj, ra[0], rb2[0]);
       sr[1] += clamp_fma2(xj, ra[1], rb2[1]);
       srt += clamp_fma1(xj, rat, rbt);
-    });
+    }, hw, HALVES);
     for_list<2>(prep, 1, b, i, Ne, Nc, [&](int j) {
       const float xj = HDG_ABL_XJ ? xb[lane + (j & 1)] : xb[j];
       sc[0] += clamp_fma2(xj, ca[0], cb[0]);
       sc[1] += clamp_fma2(xj, ca[1], cb[1]);
       sct += clamp_fma1(xj, cat, cbt);
-    });
+    }, hw, HALVES);
+    if constexpr (HALVES == 2) {                  // hw 1's sums, added in a fixed order
+      float* hd = hand + g * 10 * TN + lane;
+      if (hw) {
+        hd[0 * TN] = sr[0].x; hd[1 * TN] = sr[0].y; hd[2 * TN] = sr[1].x; hd[3 * TN] = sr[1].y;
+        hd[4 * TN] = srt;
+        hd[5 * TN] = sc[0].x; hd[6 * TN] = sc[0].y; hd[7 * TN] = sc[1].x; hd[8 * TN] = sc[1].y;
+        hd[9 * TN] = sct;
+      }
+      __syncthreads();
+      if (hw) return;                             // no barriers below
+      sr[0] += (f2){hd[0 * TN], hd[1 * TN]};
+      sr[1] += (f2){hd[2 * TN], hd[3 * TN]};
+      srt += hd[4 * TN];
+      sc[0] += (f2){hd[5 * TN], hd[6 * TN]};
+      sc[1] += (f2){hd[7 * TN], hd[8 * TN]};
+      sct += hd[9 * TN];
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       s1[2 * h] = sr[h].x * dd[2 * h];
@@ -906,6 +930,7 @@ __device__ __forceinline__ void ent_fwd_sorted(const float* __restrict__ x,
     s1[4] = srt * dd[4];
     s2[4] = sct * dd[4];
   }
+  if (!live) return;
 #pragma unroll
   for (int kk = 0; kk < KPW; ++kk) {
     const size_t gi = ((size_t)b * Ne + i) * H + g * KPW + kk;
@@ -935,7 +960,7 @@ template <int SM = H, int SK = 1, class F>
 __device__ __forceinline__ void rows_x_w(const float* As, const float* Wm, const float* kz,
                                          F f) {
   const int lane = threadIdx.x & 63;
-  for (int tile = threadIdx.x >> 6; tile < 8; tile += NT / 64) {   // wave-uniform
+  for (int tile = threadIdx.x >> 6; tile < 8; tile += blockDim.x >> 6) {   // wave-uniform
     const int n0 = (tile >> 1) * 16, kc = (tile & 1) * 16 + (lane & 15);
     const bool cv = kc < H;
     const f4v c = mfma_tile16_p(As + (n0 + (lane & 15)) * HP, 1, cv ? Wm + kc * SK : kz,
@@ -971,7 +996,7 @@ __device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
     const float *W5 = Wl, *B5 = Wl + 400, *W1e = Wl + 420, *B1e = Wl + 840, *W2e = Wl + 860;
     stage_w(Wl, W + o.E1_W5, 420);                // W5 | b5
     stage_w(Wl + 420, W + o.E3_W1, 461);          // W1' | b1' | w2' | b2'
-    for (int e = t; e < nn * H; e += NT) A[(e / H) * HP + e % H] = P[base + e];
+    for (int e = t; e < nn * H; e += blockDim.x) A[(e / H) * HP + e % H] = P[base + e];
     __syncthreads();
     rows_x_w(A, W5, kz, [&](int n, int k, float c) {   // E_bar = P W5 + 2 (Ne-1) b5
       const float v = c + (2.f * Ne1) * B5[k];
@@ -986,7 +1011,7 @@ __device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
       if (n < nn) hE[base + n * H + k] = v;
     });
     __syncthreads();
-    for (int n = t; n < nn; n += NT) {
+    for (int n = t; n < nn; n += blockDim.x) {
       float acc = Wl[880];
       for (int k = 0; k < H; ++k) acc = fmaf(Cs[n * HP + k], W2e[k], acc);
       ov[(size_t)b * Ne + t0 + n] = acc;
@@ -997,7 +1022,7 @@ __device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
   const float *Q2 = Wl, *q2 = Wl + 400, *P1 = Wl + 420, *p1b = Wl + 860;
   stage_w(Wl, W + o.EE_W2, 420);                  // Q2 | q2
   stage_w(Wl + 420, W + o.EC_W1, 460);            // U1' (22 x 20) | b1'
-  for (int e = t; e < nn * H; e += NT) {
+  for (int e = t; e < nn * H; e += blockDim.x) {
     A[(e / H) * HP + e % H] = R1[base + e];
     Bs[(e / H) * HP + e % H] = C1[base + e];
   }
@@ -1024,8 +1049,11 @@ __device__ __forceinline__ void node_fwd_tile(const float* __restrict__ x,
 
 // grid (te (+1), B, 1 + EE): z = 0 the entity stage (variants 2 / 4), else the EE stage.
 // D != NULL: one more x column whose block (te, 0, 0) runs kw_derive's work (no kernel of
-// its own; nothing here reads D)
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw_ent_fwd(const float* __restrict__ x,
+// its own; nothing here reads D).  HALVES = 2: 8 waves, the neighbour walks split over two
+// wave halves and node_fwd_tile's 8 MFMA tiles one per wave, while the grid fits 2 blocks
+// per CU (ent_fwd_halves); HALVES = 1: 4 waves
+template <int HALVES>
+__global__ __launch_bounds__(256 * HALVES) __attribute__((amdgpu_waves_per_eu(4))) void kw_ent_fwd(const float* __restrict__ x,
                                                  const uint32_t* __restrict__ abits,
                                                  const uint32_t* __restrict__ aT,
                                                  const uint32_t* __restrict__ prep,
@@ -1035,15 +1063,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void kw
                                                  float* __restrict__ D,
                                                  const float* __restrict__ bpow, NodeFwdOut no) {
   if (D && blockIdx.x == gridDim.x - 1) {       // block-uniform
-    if (blockIdx.y == 0 && blockIdx.z == 0) derive_body(W, o, Nc, D, bpow);
+    if (blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < NT) derive_body(W, o, Nc, D, bpow);
     return;
   }
+  __shared__ float hand[HALVES == 2 ? NW * 10 * TN : 1];   // hw 1's walk sums [g][10][lane]
   WSTAMP(7, 0);
   const bool ent_part = blockIdx.z == 0 && ent;
   if (ent_part)
-    ent_fwd_sorted<0>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr);
+    ent_fwd_sorted<0, HALVES>(x, abits, aT, prep, W, o, Ne, Nc, P, nullptr, hand);
   else
-    ent_fwd_sorted<1>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1);
+    ent_fwd_sorted<1, HALVES>(x, abits, aT, prep, W, o, Ne, Nc, R1, C1, hand);
   // the per-node products on the tile (node_fwd_tile): its inputs are this block's outputs
   // (global writes made visible to the block by the barrier)
   WSTAMP(7, 2);
@@ -4571,11 +4600,30 @@ int first_bwd_halves(long long blocks) {
   return blocks > 3LL * cus ? 1 : 2;
 }
 
+// kw_ent_fwd's form by its grid: 8 waves per block (2 blocks per CU at 126 VGPRs) while the
+// tile blocks fit one round, 4 waves beyond
+#ifndef HDG_EF_HALVES
+#define HDG_EF_HALVES 0   // 0: by the grid; 1 / 2: forced
+#endif
+int ent_fwd_halves(long long blocks) {
+  if (HDG_EF_HALVES) return HDG_EF_HALVES;
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+              ? n : 256;
+  }
+  return blocks <= 2LL * cus ? 2 : 1;
+}
+
 int set_wide_attrs() {
   static bool attr_set = false;   // > 64 KiB of dynamic LDS for Ne > 4000
   if (!attr_set) {
-    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd<1>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    WTRY(hipFuncSetAttribute((const void*)kw_ent_fwd<2>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<2>,    // + 15 KiB static hand-over
                              hipFuncAttributeMaxDynamicSharedMemorySize, 112 * 1024));
     WTRY(hipFuncSetAttribute((const void*)kw_first_bwd<1>,    // + 15 KiB static hand-over
@@ -4676,9 +4724,14 @@ int wide_ee_fwd(const hdg_shape* s, const hdg_batch* bt, const float* params, vo
   const int te = (Ne + TN - 1) / TN;
   if (int rc = set_wide_attrs()) return rc;
   const NodeFwdOut no{F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.Rn), F(w.Cn), F(w.rho), F(w.gmm)};
-  hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, 1), dim3(NT), sort_lds_bytes(Ne), st, bt->x,
-                     bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1), F(w.C1),
-                     ws + w.D, bpow, no);
+  if (ent_fwd_halves((long long)te * B) == 2)
+    hipLaunchKernelGGL(kw_ent_fwd<2>, dim3(te + 1, B, 1), dim3(NTP), sort_lds_bytes(Ne), st,
+                       bt->x, bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1),
+                       F(w.C1), ws + w.D, bpow, no);
+  else
+    hipLaunchKernelGGL(kw_ent_fwd<1>, dim3(te + 1, B, 1), dim3(NT), sort_lds_bytes(Ne), st,
+                       bt->x, bt->abits, aT, prep, params, o, Ne, Nc, 0, F(w.P), F(w.R1),
+                       F(w.C1), ws + w.D, bpow, no);
   WTRY(kmark("kw_ent_fwd", st));
   unsigned long long* ncpart = (unsigned long long*)F(w.ncpart);
   return launch_ee_fwd(s, bt, params, ws + w.D, F(w.rho), F(w.gmm), ncpart, st);
@@ -4885,9 +4938,15 @@ int wide_run(const hdg_shape* s, const hdg_batch* bt, const float* params, float
   if (ent || ee) {   // + kw_derive's work in one more block column, node_fwd_tile per tile
     const NodeFwdOut no{F(w.Eb), F(w.hE), F(w.ov), F(w.xp), F(w.Rn), F(w.Cn), F(w.rho),
                         F(w.gmm)};
-    hipLaunchKernelGGL(kw_ent_fwd, dim3(te + 1, B, (ent && ee) ? 2 : 1), dim3(NT), tlds, st,
-                       bt->x, bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P),
-                       F(w.R1), F(w.C1), D, bpow, no);
+    const int ez = (ent && ee) ? 2 : 1;
+    if (ent_fwd_halves((long long)te * B * ez) == 2)
+      hipLaunchKernelGGL(kw_ent_fwd<2>, dim3(te + 1, B, ez), dim3(NTP), tlds, st, bt->x,
+                         bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P), F(w.R1),
+                         F(w.C1), D, bpow, no);
+    else
+      hipLaunchKernelGGL(kw_ent_fwd<1>, dim3(te + 1, B, ez), dim3(NT), tlds, st, bt->x,
+                         bt->abits, aT, prep, params, o, Ne, Nc, ent ? 1 : 0, F(w.P), F(w.R1),
+                         F(w.C1), D, bpow, no);
     WTRY(kmark("kw_ent_fwd", st));
   }
   unsigned long long* ncpart = ee ? (unsigned long long*)F(w.ncpart) : nullptr;
